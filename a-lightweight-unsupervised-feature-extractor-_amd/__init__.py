@@ -1,0 +1,26 @@
+"""MI355X-native tracker hot path (ROI Align -> encoder -> cost -> assignment).
+
+Drop-in for the per-frame path of ImChouOWO/A-lightweight-Unsupervised-
+Feature-Extractor- (reference tracking.py:193-329, model/mainTracking.py):
+
+  roi_align / roi_align_from_input_boxes   torchvision.ops.roi_align (HIP)
+  Model                                    encoderAndHead.Model (PyTorch-ROCm)
+  cal_cost / bbox_cost / conf_cost         costCard (HIP fused cost)
+  hungarian_assign / linear_sum_assignment hung.py / scipy LSAP (HIP SAP)
+  Tracking                                 mainTracking.Tracking
+  StreamBatchTracker                       device-resident multi-stream tracker
+
+Import with importlib (the directory name is not an identifier):
+    trk = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd")
+"""
+from ._lib import TrkError, lib, header_symbols
+from .ops import (roi_align, roi_align_from_input_boxes, build_cost, cost_combine, lsap_batched,
+                  linear_sum_assignment, default_cost_params, CostParams)
+from .hung import hungarian_assign
+from .costcard import cal_cost, bbox_cost, conf_cost
+from .encoder import Model
+
+__all__ = ["TrkError", "lib", "header_symbols", "roi_align", "roi_align_from_input_boxes",
+           "build_cost", "cost_combine", "lsap_batched", "linear_sum_assignment",
+           "default_cost_params", "CostParams", "hungarian_assign", "cal_cost", "bbox_cost",
+           "conf_cost", "Model"]

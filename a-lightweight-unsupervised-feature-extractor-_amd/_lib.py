@@ -1,0 +1,99 @@
+"""ctypes binding of libtrk_amd.so (the C ABI declared in include/trk_amd.h).
+
+There is no CPU fallback anywhere in this package: if the shared library is
+missing, or a call is made with host tensors, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtrk_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "trk_amd.h")
+
+TRK_F32, TRK_BF16, TRK_F64 = 0, 1, 2
+TRK_NCHW, TRK_NHWC = 0, 1
+TRK_LSAP_MAX_DIM = 2048
+
+_lock = threading.Lock()
+_lib = None
+
+
+class TrkError(RuntimeError):
+    """A libtrk_amd entry point returned a non-zero status."""
+
+
+class CostParams(ctypes.Structure):
+    # mirrors trk_cost_params (include/trk_amd.h)
+    _fields_ = [("w_app", ctypes.c_float), ("w_bbox", ctypes.c_float),
+                ("w_conf", ctypes.c_float), ("alpha", ctypes.c_float),
+                ("beta", ctypes.c_float), ("maha_thr", ctypes.c_double),
+                ("inf_cost", ctypes.c_float), ("topk", ctypes.c_int), ("gate", ctypes.c_int)]
+
+
+def _declare(L):
+    P, i32, i64, sz, f32, f64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t,
+                                 ctypes.c_float, ctypes.c_double)
+    L.trk_abi_version.argtypes = []
+    L.trk_abi_version.restype = i32
+    L.trk_last_error.argtypes = []
+    L.trk_last_error.restype = ctypes.c_char_p
+    L.trk_roi_align_workspace_bytes.argtypes = [i64, i64, i64, i64, i32]
+    L.trk_roi_align_workspace_bytes.restype = sz
+    L.trk_roi_align_fwd.argtypes = [P, i64, i64, i64, i64, i32, P, i64, f32, i32, i32, i32, i32,
+                                    P, i32, i32, P, sz, P]
+    L.trk_roi_align_fwd.restype = i32
+    L.trk_build_cost.argtypes = [i64, i64, i64, P, P, P, i64, P, P, P, P, P, P, P, P, P, P,
+                                 ctypes.POINTER(CostParams), P, P, P, P, P, P]
+    L.trk_build_cost.restype = i32
+    L.trk_cost_combine.argtypes = [i64, i64, P, P, P, P, P, P, P, P, ctypes.POINTER(CostParams),
+                                   P, P, P, P, P]
+    L.trk_cost_combine.restype = i32
+    L.trk_lsap.argtypes = [i64, P, i32, i64, i64, P, P, i64, P, P, P, P, P, i64, f64, P]
+    L.trk_lsap.restype = i32
+    for name, (args, res) in _EXTRA.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+# entry points added by later modules register here before first load
+_EXTRA: dict = {}
+
+
+def lib():
+    """The loaded library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise TrkError(
+                        f"{LIB_PATH} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')}` "
+                        "or __graft_entry__.build() (there is no CPU fallback)")
+                L = ctypes.CDLL(LIB_PATH)
+                _declare(L)
+                if L.trk_abi_version() != 1:
+                    raise TrkError("libtrk_amd ABI version mismatch")
+                _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().trk_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        if rc == -3:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise TrkError(f"{what} failed ({rc}): {msg}")
+
+
+def header_symbols():
+    """Every function the public header declares (for the ABI export test)."""
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(trk_[a-z0-9_]+)\s*\(", src)))

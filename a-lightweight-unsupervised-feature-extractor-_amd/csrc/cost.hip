@@ -1,0 +1,340 @@
+// Fused association-cost kernel for gfx950 (MI355X), batched over frames.
+//
+// One launch replaces, per frame (video stream):
+//   Tracking.build_C_app_topk      reference model/mainTracking.py:141-211
+//   costCard.bbox_cost / conf_cost model/utils/costTool/costCard.py:109-203
+//   costCard.cal_cost C_total      costCard.py:264-268
+//   Tracking.apply_kalman_gating   mainTracking.py:306-338 +
+//   gating_distance_maha           model/utils/costTool/KalmanFilter.py:105-116
+// Restated in SURVEY.md A.3/A.4 and oracle/trk_oracle.c:ora_cost_build.
+//
+// Work decomposition:
+//   workgroup = (frame f, 32-detection tile, block of 16 track rows); 4 waves,
+//   each wave owns 4 track rows.  The 32x128 detection tile is normalised once
+//   and held in registers as the B operand of v_mfma_f32_32x32x2_f32 (exact
+//   f32, 64 k-steps; lane half h supplies k = s + 64h).  Per track the <=30x128
+//   memory bank is read straight into the A operand (16-B loads, L1-resident),
+//   the next track's bank is prefetched during the MFMA chain.  The 32x32
+//   accumulator holds sim[t][j] with the column on the lane, so the per-column
+//   top-k over t is a register sort of 16 values per lane + one __shfl_xor(32)
+//   merge.  bbox / conf / Mahalanobis terms are fused into the epilogue.
+// Built with -ffp-contract=off: scalar f32 ops round as torch's separate ops do;
+// the one FMA torch's CPU norm performs is written as an explicit fmaf.
+#include "trk_common.h"
+
+namespace {
+
+constexpr int D = 128;           // embedding dim (mainTracking.py:109-110,267-268)
+constexpr int kMaxFrames = 64;   // frames per launch (kernarg-resident shapes)
+constexpr int kMaxTopk = 8;
+constexpr int kRowsPerWave = 4;
+constexpr int kWavesPerWG = 4;
+constexpr int kRowsPerWG = kRowsPerWave * kWavesPerWG;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct CostArgs {
+  int F, Mmax, Nmax, Tmax;
+  const int32_t* row_slot;
+  const float* bank;
+  const int32_t* bank_len;
+  const float* pbox;
+  const float* conf_prev;
+  const double* gmean;
+  const double* gsinv;
+  const int32_t* gate_on;
+  const float* det_emb;
+  const float* dbox;
+  const float* conf_cur;
+  float* C_total;
+  float* C_app;
+  float* C_center;
+  float* C_scale;
+  float* C_conf;
+  trk_cost_params p;
+  int M[kMaxFrames];
+  int N[kMaxFrames];
+};
+
+__device__ __forceinline__ void load_a_frag(const float* __restrict__ rowp, bool ok, float (&a)[64]) {
+  // lane (t, h): elements 64h + 0..63 of bank row t (16 x 16-B loads)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    float4 v = ok ? *reinterpret_cast<const float4*>(rowp + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    a[4 * q + 0] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+  }
+}
+
+// insert x into a descending list of length K (K <= kMaxTopk, compile-time bound)
+__device__ __forceinline__ void topk_insert(float (&v)[kMaxTopk], float x) {
+#pragma unroll
+  for (int q = 0; q < kMaxTopk; ++q) {
+    float hi = fmaxf(v[q], x);
+    x = fminf(v[q], x);
+    v[q] = hi;
+  }
+}
+
+// costCard.bbox_cost / conf_cost / cal_cost C_total (costCard.py:141-168,
+// :196-201, :264-268) + the Mahalanobis gate (mainTracking.py:327-336) for one
+// (track, detection) pair.  Track-side inputs are wave-uniform.
+__device__ __forceinline__ float combine(const trk_cost_params& p, float app, const float* bp,
+                                         float conf_prev, float ccx, float ccy, float Ac, float ccv,
+                                         bool gate, const double* gm, const double* S, double z0,
+                                         double z1, double z2, double z3, float& cen, float& scl,
+                                         float& cf) {
+  const float px1 = bp[0], py1 = bp[1], px2 = bp[2], py2 = bp[3];
+  const float cpx = 0.5f * (px1 + px2), cpy = 0.5f * (py1 + py2);
+  const float wp = fmaxf(px2 - px1, 1.0f), hp = fmaxf(py2 - py1, 1.0f);
+  const float sp = fmaxf(sqrtf(wp * wp + hp * hp), 1.0f);
+  const float Ap = wp * hp;
+  const float cpv = fmaxf(conf_prev, 1e-6f);
+  const float dx = cpx - ccx, dy = cpy - ccy;
+  const float dist = sqrtf(fmaf(dy, dy, dx * dx));  // torch.norm CPU rounding
+  cen = dist / sp;
+  scl = fabsf(logf(fmaxf(Ac / Ap, 1e-6f)));
+  cf = fabsf(logf(ccv / cpv));
+  const float bbox = p.alpha * cen + p.beta * scl;
+  float tot = p.w_app * app + p.w_bbox * bbox;
+  tot = tot + p.w_conf * cf;
+  if (gate) {
+    const double y[4] = {z0 - gm[0], z1 - gm[1], z2 - gm[2], z3 - gm[3]};
+    double d2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double t = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t += S[r * 4 + c] * y[c];
+      d2 += y[r] * t;
+    }
+    if (d2 > p.maha_thr) tot = p.inf_cost;
+  }
+  return tot;
+}
+
+// detection-side terms: centre, area, clamped conf and KF measurement z
+// (bbox_xyxy_to_z, KalmanFilter.py:5-16: double arithmetic, float32 result)
+__device__ __forceinline__ void det_terms(const float* bc, float conf, float& ccx, float& ccy,
+                                          float& Ac, float& ccv, double& z0, double& z1,
+                                          double& z2, double& z3) {
+  const float x1 = bc[0], y1 = bc[1], x2 = bc[2], y2 = bc[3];
+  ccx = 0.5f * (x1 + x2);
+  ccy = 0.5f * (y1 + y2);
+  const float wc = fmaxf(x2 - x1, 1.0f), hc = fmaxf(y2 - y1, 1.0f);
+  Ac = wc * hc;
+  ccv = fmaxf(conf, 1e-6f);
+  const double dx1 = x1, dy1 = y1, dx2 = x2, dy2 = y2;
+  const double w = fmax(dx2 - dx1, 1.0), hh = fmax(dy2 - dy1, 1.0);
+  z0 = (float)(dx1 + 0.5 * w);
+  z1 = (float)(dy1 + 0.5 * hh);
+  z2 = (float)(w / hh);
+  z3 = (float)hh;
+}
+
+__global__ void __launch_bounds__(256)
+cost_kernel(const CostArgs A) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int f = blockIdx.z;
+  const int j0 = blockIdx.x * 32;
+  const int i0 = blockIdx.y * kRowsPerWG + wave * kRowsPerWave;
+  const int M = A.M[f], N = A.N[f];
+  if (j0 >= N || blockIdx.y * kRowsPerWG >= M) return;
+  const int col = lane & 31, h = lane >> 5;
+  const int j = j0 + col;
+  const bool jok = j < N;
+
+  // ---- detection tile: B operand, renormalised (build_C_app_topk :167-169)
+  float b[64];
+  {
+    const float* dp = A.det_emb + ((int64_t)f * A.Nmax + (jok ? j : 0)) * D + 64 * h;
+    load_a_frag(dp, jok, b);
+    double ss = 0.0;
+#pragma unroll
+    for (int s = 0; s < 64; ++s) ss += (double)b[s] * (double)b[s];
+    ss += __shfl_xor(ss, 32);
+    const float nrm = (float)sqrt(ss) + 1e-12f;
+#pragma unroll
+    for (int s = 0; s < 64; ++s) b[s] = b[s] / nrm;
+  }
+  // ---- detection-side box / conf terms for column j
+  float ccx = 0.f, ccy = 0.f, Ac = 1.f, ccv = 1.f;
+  double z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+  if (jok)
+    det_terms(A.dbox + ((int64_t)f * A.Nmax + j) * 4, A.conf_cur[(int64_t)f * A.Nmax + j], ccx, ccy,
+              Ac, ccv, z0, z1, z2, z3);
+
+  const int Tmax = A.Tmax;
+  const int topk = A.p.topk;
+  auto slot_of = [&](int i) -> int64_t {
+    return A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.Mmax + i] : (int64_t)f * A.Mmax + i;
+  };
+
+  float a[64];
+  int iend = min(i0 + kRowsPerWave, M);
+  if (i0 < iend) {
+    const int64_t s0 = slot_of(i0);
+    const int T0 = min(A.bank_len[s0], Tmax);
+    load_a_frag(A.bank + (s0 * Tmax + col) * D + 64 * h, col < T0, a);
+  }
+  for (int i = i0; i < iend; ++i) {
+    const int64_t slot = slot_of(i);
+    const int T = min(A.bank_len[slot], Tmax);
+    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    // prefetch the next row's bank while the MFMA chain drains
+    if (i + 1 < iend) {
+      const int64_t sn = slot_of(i + 1);
+      const int Tn = min(A.bank_len[sn], Tmax);
+      load_a_frag(A.bank + (sn * Tmax + col) * D + 64 * h, col < Tn, a);
+    }
+    // ---- top-k over t for column j (torch.topk(dim=0) + mean, :201-203)
+    float tk[kMaxTopk];
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float x = t < T ? acc[r] : -INFINITY;
+      topk_insert(tk, x);
+    }
+    float other[kMaxTopk];
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) other[q] = __shfl_xor(tk[q], 32);
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) topk_insert(tk, other[q]);
+    const int k = min(topk, T);
+    float app;
+    if (k <= 0) {
+      app = 1.0f;  // empty bank, no EMA fallback (:180-186 / :197-199)
+    } else {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < kMaxTopk; ++q)
+        if (q < k) sum = sum + tk[q];
+      app = 1.0f - sum / (float)k;
+    }
+    if (h != 0 || !jok) continue;
+
+    float cen, scl, cf;
+    const float tot = combine(A.p, app, A.pbox + slot * 4, A.conf_prev[slot], ccx, ccy, Ac, ccv,
+                              A.p.gate && A.gate_on[slot], A.gmean + slot * 4, A.gsinv + slot * 16,
+                              z0, z1, z2, z3, cen, scl, cf);
+    const int64_t o = ((int64_t)f * A.Mmax + i) * A.Nmax + j;
+    if (A.C_total) A.C_total[o] = tot;
+    if (A.C_app) A.C_app[o] = app;
+    if (A.C_center) A.C_center[o] = cen;
+    if (A.C_scale) A.C_scale[o] = scl;
+    if (A.C_conf) A.C_conf[o] = cf;
+  }
+}
+
+// C_app given (costCard.cal_cost API): elementwise combine over [M, N].
+__global__ void __launch_bounds__(256)
+combine_kernel(int M, int N, const float* __restrict__ C_app, const float* __restrict__ pbox,
+               const float* __restrict__ conf_prev, const float* __restrict__ dbox,
+               const float* __restrict__ conf_cur, const double* __restrict__ gmean,
+               const double* __restrict__ gsinv, const int32_t* __restrict__ gate_on,
+               trk_cost_params p, float* C_total, float* C_center, float* C_scale, float* C_conf) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)M * N) return;
+  const int i = (int)(q / N), j = (int)(q % N);
+  float ccx, ccy, Ac, ccv;
+  double z0, z1, z2, z3;
+  det_terms(dbox + (int64_t)j * 4, conf_cur[j], ccx, ccy, Ac, ccv, z0, z1, z2, z3);
+  const bool g = p.gate && gate_on[i];
+  float cen, scl, cf;
+  const float tot = combine(p, C_app[q], pbox + (int64_t)i * 4, conf_prev[i], ccx, ccy, Ac, ccv, g,
+                            g ? gmean + (int64_t)i * 4 : nullptr, g ? gsinv + (int64_t)i * 16 : nullptr,
+                            z0, z1, z2, z3, cen, scl, cf);
+  if (C_total) C_total[q] = tot;
+  if (C_center) C_center[q] = cen;
+  if (C_scale) C_scale[q] = scl;
+  if (C_conf) C_conf[q] = cf;
+}
+
+}  // namespace
+
+extern "C" int trk_cost_combine(int64_t M, int64_t N, const float* C_app, const float* pbox,
+                                const float* conf_prev, const float* dbox, const float* conf_cur,
+                                const double* gmean, const double* gsinv, const int32_t* gate_on,
+                                const trk_cost_params* host_params, float* C_total,
+                                float* C_center, float* C_scale, float* C_conf, void* stream) {
+  TRK_REQUIRE(M >= 0 && N >= 0 && M * N < ((int64_t)1 << 31), "cost_combine: bad shape");
+  TRK_REQUIRE(host_params, "cost_combine: null params");
+  if (M == 0 || N == 0) return TRK_OK;
+  TRK_REQUIRE(C_app && pbox && conf_prev && dbox && conf_cur, "cost_combine: null input pointer");
+  TRK_REQUIRE(!host_params->gate || (gmean && gsinv && gate_on),
+              "cost_combine: gating needs gmean/gsinv/gate_on");
+  const int64_t n = M * N;
+  hipLaunchKernelGGL(combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (int)M, (int)N, C_app, pbox, conf_prev,
+                     dbox, conf_cur, gmean, gsinv, gate_on, *host_params, C_total, C_center, C_scale,
+                     C_conf);
+  return trk::check_launch("combine_kernel");
+}
+
+extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* host_M,
+                              const int32_t* host_N, const int32_t* row_slot, int64_t Tmax,
+                              const float* bank, const int32_t* bank_len, const float* pbox,
+                              const float* conf_prev, const double* gmean, const double* gsinv,
+                              const int32_t* gate_on, const float* det_emb, const float* dbox,
+                              const float* conf_cur, const trk_cost_params* host_params,
+                              float* C_total, float* C_app, float* C_center, float* C_scale,
+                              float* C_conf, void* stream) {
+  TRK_REQUIRE(F >= 0 && Mmax >= 0 && Nmax >= 0, "build_cost: negative shape");
+  TRK_REQUIRE(host_params, "build_cost: null params");
+  TRK_REQUIRE(Tmax >= 1 && Tmax <= 32, "build_cost: Tmax (hist_max) must be in [1, 32], got %lld",
+              (long long)Tmax);
+  TRK_REQUIRE(host_params->topk >= 0 && host_params->topk <= kMaxTopk,
+              "build_cost: topk must be in [0, %d]", kMaxTopk);
+  TRK_REQUIRE(Mmax < (1 << 30) && Nmax < (1 << 30), "build_cost: shape too large");
+  if (F == 0 || Mmax == 0 || Nmax == 0) return TRK_OK;
+  TRK_REQUIRE(host_M && host_N, "build_cost: null shape arrays");
+  TRK_REQUIRE(bank && bank_len && pbox && conf_prev && det_emb && dbox && conf_cur,
+              "build_cost: null input pointer");
+  TRK_REQUIRE(!host_params->gate || (gmean && gsinv && gate_on), "build_cost: gating needs gmean/gsinv/gate_on");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t f0 = 0; f0 < F; f0 += kMaxFrames) {
+    const int nf = (int)std::min<int64_t>(kMaxFrames, F - f0);
+    CostArgs a;
+    memset(&a, 0, sizeof a);
+    int mmax = 0, nmax = 0;
+    for (int q = 0; q < nf; ++q) {
+      TRK_REQUIRE(host_M[f0 + q] >= 0 && host_M[f0 + q] <= Mmax && host_N[f0 + q] >= 0 &&
+                      host_N[f0 + q] <= Nmax,
+                  "build_cost: frame %lld M/N outside [0, Mmax/Nmax]", (long long)(f0 + q));
+      a.M[q] = host_M[f0 + q];
+      a.N[q] = host_N[f0 + q];
+      mmax = std::max(mmax, a.M[q]);
+      nmax = std::max(nmax, a.N[q]);
+    }
+    if (mmax == 0 || nmax == 0) continue;
+    const int64_t fr = f0;
+    a.F = nf; a.Mmax = (int)Mmax; a.Nmax = (int)Nmax; a.Tmax = (int)Tmax;
+    a.row_slot = row_slot ? row_slot + fr * Mmax : nullptr;
+    // without row_slot, slot = f*Mmax + i indexes the per-frame-packed arrays
+    const int64_t so = row_slot ? 0 : fr * Mmax;
+    a.bank = bank + so * Tmax * D;
+    a.bank_len = bank_len + so;
+    a.pbox = pbox + so * 4;
+    a.conf_prev = conf_prev + so;
+    a.gmean = gmean ? gmean + so * 4 : nullptr;
+    a.gsinv = gsinv ? gsinv + so * 16 : nullptr;
+    a.gate_on = gate_on ? gate_on + so : nullptr;
+    a.det_emb = det_emb + fr * Nmax * D;
+    a.dbox = dbox + fr * Nmax * 4;
+    a.conf_cur = conf_cur + fr * Nmax;
+    const int64_t co = fr * Mmax * Nmax;
+    a.C_total = C_total ? C_total + co : nullptr;
+    a.C_app = C_app ? C_app + co : nullptr;
+    a.C_center = C_center ? C_center + co : nullptr;
+    a.C_scale = C_scale ? C_scale + co : nullptr;
+    a.C_conf = C_conf ? C_conf + co : nullptr;
+    a.p = *host_params;
+    dim3 grid((unsigned)((nmax + 31) / 32), (unsigned)((mmax + kRowsPerWG - 1) / kRowsPerWG), (unsigned)nf);
+    hipLaunchKernelGGL(cost_kernel, grid, dim3(256), 0, st, a);
+    if (int e = trk::check_launch("cost_kernel")) return e;
+  }
+  return TRK_OK;
+}

@@ -1,0 +1,38 @@
+// Shared helpers for the gfx950 tracker kernels (C-ABI error plumbing, bf16).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/trk_amd.h"
+
+namespace trk {
+
+void set_error(const char* fmt, ...);
+
+// Report the first launch error of the preceding kernel; 0 if clean.
+int check_launch(const char* what);
+
+#define TRK_REQUIRE(cond, ...)            \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::trk::set_error(__VA_ARGS__);      \
+      return TRK_EINVAL;                  \
+    }                                     \
+  } while (0)
+
+// Round-to-nearest-even f32 -> bf16 (NaN stays NaN: MI355X_MICROARCH.md
+// correctness table; hipcc lowers the plain conversion to v_cvt_pk_bf16_f32).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+constexpr int kWave = 64;
+
+}  // namespace trk

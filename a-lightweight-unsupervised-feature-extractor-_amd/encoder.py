@@ -1,0 +1,165 @@
+"""The lightweight ROI encoder -- drop-in for reference
+model/utils/modules/encoderAndHead.py:11-26 (Model) built from card.py's RMB +
+ProjectionHead.
+
+The module tree reproduces the reference's 35 state_dict keys so a reference
+checkpoint ``ckpt["model"]`` loads with ``strict=True`` (tracking.py:180-182).
+The forward is a re-derivation of the eval graph for MI355X,
+not a module-by-module replay:
+
+  * the four first 1x1 convs (depth/point x reinforce/normal) read the same
+    input, so they are ONE GEMM  [N*S*S, 512] x [512, 1024] on NHWC rows;
+  * the four depthwise 5x5 convs are one 1024-group depthwise conv;
+  * each DSC's ``depth.2(d) + point.2(p)`` is one GEMM over the concatenated
+    [d | p] columns with eval-BN folded into its weights and bias;
+  * only the spatial mean of the RMB output feeds the head, so the shake/fuse
+    blend and the GAP are applied to per-ROI means:
+        mean(0.5*x_cat + 0.5*(0.5*x_f*s + 0.5*x_n))
+      = 0.5*mean(SiLU(T)) + 0.25*s*mean(x_f) + 0.25*mean(x_n)
+    and the SE scale s is applied to the transition GEMM's input rows.
+Input: [N, 512, S, S] ROI features in any memory format; channels_last
+(what trk roi_align writes with channels_last=True) makes the first GEMM's
+operand a zero-copy view.  Compute dtype = input dtype (fp32 for parity,
+bf16 for throughput); reductions, SE and the head run in fp32.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class DSC(nn.Module):
+    """Parameter container matching card.DSC (card.py:8-46)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=5):
+        super().__init__()
+        hidden = in_channels // 2
+
+        def branch():
+            return nn.Sequential(
+                nn.Conv2d(in_channels, hidden, 1, bias=False),
+                nn.Conv2d(hidden, hidden, kernel_size, padding=kernel_size // 2, groups=hidden, bias=False),
+                nn.Conv2d(hidden, out_channels, 1, bias=False))
+
+        self.depth = branch()
+        self.point = branch()
+        self.bn = nn.BatchNorm2d(out_channels)
+
+
+class SEBlock(nn.Module):
+    """card.SEBlock (card.py:59-78) parameters."""
+
+    def __init__(self, in_channels, reduction=4):
+        super().__init__()
+        hid = in_channels // reduction
+        self.excitation = nn.Sequential(nn.Linear(in_channels, hid), nn.ReLU(),
+                                        nn.Linear(hid, in_channels), nn.Hardsigmoid())
+
+
+class RMB(nn.Module):
+    """card.RMB (card.py:105-148) parameters; warmup/epoch semantics kept."""
+
+    def __init__(self, in_channels, out_channels, stride=1, warmup_epochs=0):
+        super().__init__()
+        if stride != 1:
+            raise NotImplementedError("RMB stride != 1 is not used by the reference")
+        self.warmup_epochs = warmup_epochs
+        self.current_epoch = 0
+        self.dsc_reinforce = DSC(in_channels, out_channels)
+        self.dsc_normal = DSC(in_channels, out_channels)
+        self.se = SEBlock(out_channels)
+        self.transition = nn.Sequential(nn.Conv2d(2 * out_channels, out_channels, 1), nn.SiLU())
+
+    def set_epoch(self, epoch: int):
+        self.current_epoch = epoch
+
+
+class ProjectionHead(nn.Module):
+    """card.ProjectionHead (card.py:151-169) parameters."""
+
+    def __init__(self, in_dim, proj_dim=128, dropout=0.2, init_logit_scale=10.0):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(in_dim, in_dim, bias=False), nn.LayerNorm(in_dim), nn.SiLU(),
+                                 nn.Dropout(p=dropout), nn.Linear(in_dim, proj_dim))
+        self.logit_scale = nn.Parameter(torch.tensor(math.log(init_logit_scale), dtype=torch.float32),
+                                        requires_grad=False)
+        self.logit_bias = nn.Parameter(torch.tensor(0.0, dtype=torch.float32), requires_grad=False)
+
+
+class Model(nn.Module):
+    """encoderAndHead.Model(in_channels, out_channels, warmup_epochs, proj_dim)."""
+
+    def __init__(self, in_channels=None, out_channels=None, warmup_epochs=10, proj_dim=128):
+        super().__init__()
+        self.rmb = RMB(in_channels, out_channels, stride=1, warmup_epochs=warmup_epochs)
+        self.head = ProjectionHead(out_channels, proj_dim=proj_dim, dropout=0.2)
+        self._fused = None
+        self._fused_key = None
+
+    # -------------------------------------------------------------- weights --
+    def _fused_weights(self, dtype, device):
+        key = (dtype, device, tuple(p._version for p in self.parameters()),
+               tuple(b._version for b in self.buffers()))
+        if self._fused is not None and self._fused_key == key:
+            return self._fused
+        r = self.rmb
+        with torch.no_grad():
+            w = {}
+            dr, dn = r.dsc_reinforce, r.dsc_normal
+            w1 = torch.cat([m[0].weight.flatten(1) for m in (dr.depth, dr.point, dn.depth, dn.point)], 0)
+            w["w1t"] = w1.t().contiguous().to(device, dtype)                              # [C, 4h]
+            w["dw"] = torch.cat([m[1].weight for m in (dr.depth, dr.point, dn.depth, dn.point)],
+                                0).to(device, dtype).contiguous(memory_format=torch.channels_last)
+            for tag, dsc in (("r", dr), ("n", dn)):
+                bn = dsc.bn
+                scale = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+                shift = bn.bias.float() - bn.running_mean.float() * scale
+                w2 = torch.cat([dsc.depth[2].weight.flatten(1), dsc.point[2].weight.flatten(1)], 1).float()
+                w[f"w2{tag}"] = (w2 * scale[:, None]).t().contiguous().to(device, dtype)  # [2h, C]
+                w[f"b{tag}"] = shift.to(device, dtype)
+            wt = r.transition[0].weight.flatten(1).float()                               # [C, 2C]
+            C = wt.shape[0]
+            w["wt1"] = wt[:, :C].t().contiguous().to(device, dtype)
+            w["wt2"] = wt[:, C:].t().contiguous().to(device, dtype)
+            w["bt"] = r.transition[0].bias.to(device, dtype)
+        self._fused, self._fused_key = w, key
+        return w
+
+    # -------------------------------------------------------------- forward --
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training:
+            raise NotImplementedError("training-mode forward is out of scope (inference hot path only)")
+        N, C, S1, S2 = x.shape
+        dt, dev = x.dtype, x.device
+        W = self._fused_weights(dt, dev)
+        h4 = W["w1t"].shape[1]
+        h2 = h4 // 2
+        ss = S1 * S2
+        X = x.permute(0, 2, 3, 1).reshape(N * ss, C)                 # view when channels_last
+        Y1 = X @ W["w1t"]                                            # [N*ss, 4h]
+        Y1 = Y1.view(N, S1, S2, h4).permute(0, 3, 1, 2)               # NCHW logical, NHWC storage
+        Y2 = F.conv2d(Y1, W["dw"], padding=W["dw"].shape[-1] // 2, groups=h4)
+        Y2 = Y2.permute(0, 2, 3, 1).reshape(N * ss, h4)
+        xr = F.silu(torch.addmm(W["br"], Y2[:, :h2], W["w2r"]))        # DSC reinforce + BN + SiLU
+        xn = F.hardswish(torch.addmm(W["bn"], Y2[:, h2:], W["w2n"]))   # DSC normal + BN + Hardswish
+        xr3 = xr.view(N, ss, C)
+        m_r = xr3.mean(1, dtype=torch.float32)                        # SE squeeze
+        se = self.rmb.se.excitation
+        s = F.hardsigmoid(F.linear(F.relu(F.linear(m_r, se[0].weight, se[0].bias)), se[2].weight, se[2].bias))
+        xfs = (xr3 * s.to(dt)[:, None, :]).view(N * ss, C)
+        T = torch.addmm(W["bt"], xfs, W["wt1"])
+        T.addmm_(xn, W["wt2"])                                        # transition over cat[x_f*s, x_n]
+        m_cat = F.silu(T).view(N, ss, C).mean(1, dtype=torch.float32)
+        m_n = xn.view(N, ss, C).mean(1, dtype=torch.float32)
+        r = self.rmb
+        alpha = 0.5 if r.current_epoch < r.warmup_epochs else float(torch.rand(1))
+        m_fuse = alpha * (s * m_r) + (1 - alpha) * m_n               # RMB.forward :141-142
+        g = 0.5 * m_cat + 0.5 * m_fuse                                # Shake2 eval :94-96, GAP
+        hd = self.head.net
+        z = F.linear(g, hd[0].weight.float())
+        z = F.layer_norm(z, (z.shape[1],), hd[1].weight.float(), hd[1].bias.float(), hd[1].eps)
+        z = F.linear(F.silu(z), hd[4].weight.float(), hd[4].bias.float())
+        return F.normalize(z, dim=1)

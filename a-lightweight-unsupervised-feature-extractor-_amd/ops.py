@@ -1,0 +1,236 @@
+"""Torch-facing wrappers over the libtrk_amd C ABI.
+
+Every function here launches the hand-written gfx950 kernels on the current
+HIP stream of the input's device.  Host (CPU) tensors are rejected: there is no
+CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import CostParams, check, lib
+
+__all__ = ["roi_align", "roi_align_from_input_boxes", "build_cost", "cost_combine", "lsap_batched",
+           "linear_sum_assignment", "CostParams", "default_cost_params"]
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _need_gpu(t: torch.Tensor, what: str):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise RuntimeError(f"{what}: expected a ROCm device tensor (this package has no CPU fallback)")
+
+
+# ------------------------------------------------------------- ROI Align --
+def _rois_tensor(boxes, device, dtype) -> torch.Tensor:
+    if isinstance(boxes, torch.Tensor):
+        if boxes.dim() != 2 or boxes.size(1) != 5:
+            raise ValueError("boxes must be a Tensor[K, 5] or a list of Tensor[L, 4]")
+        return boxes.to(device=device, dtype=dtype).contiguous()
+    parts = []
+    for b, bb in enumerate(boxes):
+        bb = torch.as_tensor(bb, device=device, dtype=dtype).reshape(-1, 4)
+        parts.append(torch.cat([torch.full((bb.size(0), 1), float(b), device=device, dtype=dtype), bb], 1))
+    if not parts:
+        return torch.zeros((0, 5), device=device, dtype=dtype)
+    return torch.cat(parts, 0).contiguous()
+
+
+def roi_align(input: torch.Tensor, boxes: Union[torch.Tensor, List[torch.Tensor]],
+              output_size, spatial_scale: float = 1.0, sampling_ratio: int = -1,
+              aligned: bool = False, *, out_dtype: Optional[torch.dtype] = None,
+              channels_last: bool = False) -> torch.Tensor:
+    """``torchvision.ops.roi_align`` on gfx950 (drop-in for the call at reference
+    tracking.py:214-221).  Returns [K, C, PH, PW]; with ``channels_last=True`` the
+    same logical tensor is stored NHWC (the encoder's GEMM layout).  An input
+    already in channels_last memory format skips the per-call NCHW->NHWC copy."""
+    _need_gpu(input, "roi_align")
+    if input.dim() != 4:
+        raise ValueError(f"roi_align: expected input of shape [B, C, H, W], got {tuple(input.shape)}")
+    PH, PW = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
+    if sampling_ratio <= 0:
+        raise NotImplementedError("roi_align: adaptive sampling (sampling_ratio <= 0) is not "
+                                  "implemented; the reference always passes sampling_ratio=2")
+    in_dtype = input.dtype
+    if out_dtype is None:
+        out_dtype = in_dtype
+    x = input if input.dtype == torch.float32 else input.float()  # fp16/bf16 -> f32 is exact
+    rois = _rois_tensor(boxes, x.device, torch.float32)
+    B, C, H, W = x.shape
+    K = rois.size(0)
+    if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        in_layout, src = _lib.TRK_NHWC, x
+    else:
+        in_layout, src = _lib.TRK_NCHW, x.contiguous()
+    kdt = _lib.TRK_BF16 if out_dtype == torch.bfloat16 else _lib.TRK_F32
+    tdt = torch.bfloat16 if kdt == _lib.TRK_BF16 else torch.float32
+    if channels_last:
+        out = torch.empty((K, PH, PW, C), device=x.device, dtype=tdt).permute(0, 3, 1, 2)
+    else:
+        out = torch.empty((K, C, PH, PW), device=x.device, dtype=tdt)
+    if K == 0:
+        return out.to(out_dtype)
+    ws_bytes = lib().trk_roi_align_workspace_bytes(B, C, H, W, in_layout)
+    ws = torch.empty(max(ws_bytes, 1), device=x.device, dtype=torch.uint8) if ws_bytes else None
+    rc = lib().trk_roi_align_fwd(_ptr(src), B, C, H, W, in_layout, _ptr(rois), K,
+                                 float(spatial_scale), PH, PW, int(sampling_ratio), int(bool(aligned)),
+                                 _ptr(out), kdt, _lib.TRK_NHWC if channels_last else _lib.TRK_NCHW,
+                                 _ptr(ws), ws_bytes, _stream(x.device))
+    check(rc, "roi_align")
+    return out if out.dtype == out_dtype else out.to(out_dtype)
+
+
+def roi_align_from_input_boxes(feat: torch.Tensor, boxes_in: Sequence[Sequence[float]],
+                               input_hw: Tuple[int, int], out_size=(7, 7), aligned: bool = True,
+                               sampling_ratio: int = 2, **kw) -> torch.Tensor:
+    """MainInfer.roi_align_from_input_boxes (reference tracking.py:193-221):
+    rois = [[0, x1, y1, x2, y2]] cast to feat.dtype, spatial_scale = Hf / H_in."""
+    H_in, W_in = input_hw
+    _, _, Hf, Wf = feat.shape
+    spatial_scale = Hf / float(H_in)
+    rois = torch.tensor([[0.0, b[0], b[1], b[2], b[3]] for b in boxes_in], dtype=feat.dtype,
+                        device=feat.device).reshape(-1, 5)
+    return roi_align(feat, rois, out_size, spatial_scale=spatial_scale,
+                     sampling_ratio=sampling_ratio, aligned=aligned, **kw)
+
+
+# ------------------------------------------------------------------ cost --
+def default_cost_params(conf: Optional[dict] = None, *, gate: bool = True) -> CostParams:
+    """Constants of conf.yaml's tracker section (reference model/conf/conf.yaml:3-24)."""
+    c = conf or {}
+    return CostParams(float(c.get("w_app", 1.0)), float(c.get("w_bbox", 0.3)),
+                      float(c.get("w_conf", 0.2)), float(c.get("alpha", 1.0)),
+                      float(c.get("beta", 0.5)), float(c.get("maha_thr", 9.49)), 1e9,
+                      int(c.get("emb_top_k", 5)), 1 if gate else 0)
+
+
+def build_cost(*, M: Sequence[int], N: Sequence[int], bank: torch.Tensor, bank_len: torch.Tensor,
+               pbox: torch.Tensor, conf_prev: torch.Tensor, det_emb: torch.Tensor,
+               dbox: torch.Tensor, conf_cur: torch.Tensor, params: CostParams,
+               gmean: Optional[torch.Tensor] = None, gsinv: Optional[torch.Tensor] = None,
+               gate_on: Optional[torch.Tensor] = None, row_slot: Optional[torch.Tensor] = None,
+               out: Optional[dict] = None, want=("C_total",)) -> dict:
+    """Batched fused cost (trk_build_cost).  Shapes: det_emb [F, Nmax, 128],
+    dbox [F, Nmax, 4], conf_cur [F, Nmax]; track arrays indexed by slot
+    (bank [S, Tmax, 128] ...), rows mapped through row_slot [F, Mmax] if given,
+    else slot = f*Mmax + i.  Returns {name: [F, Mmax, Nmax] f32}."""
+    _need_gpu(det_emb, "build_cost")
+    F, Nmax, D = det_emb.shape
+    if D != 128:
+        raise ValueError(f"det_embs must be 128D, got {D}")
+    Mmax = row_slot.shape[1] if row_slot is not None else bank.shape[0] // max(F, 1)
+    Tmax = bank.shape[1]
+    dev = det_emb.device
+    if out is None:
+        out = {k: torch.empty((F, Mmax, Nmax), device=dev, dtype=torch.float32) for k in want}
+    hM = (ctypes.c_int32 * max(F, 1))(*[int(m) for m in M])
+    hN = (ctypes.c_int32 * max(F, 1))(*[int(n) for n in N])
+    rc = lib().trk_build_cost(F, Mmax, Nmax, hM, hN, _ptr(row_slot), Tmax, _ptr(bank), _ptr(bank_len),
+                              _ptr(pbox), _ptr(conf_prev), _ptr(gmean), _ptr(gsinv), _ptr(gate_on),
+                              _ptr(det_emb), _ptr(dbox), _ptr(conf_cur), ctypes.byref(params),
+                              _ptr(out.get("C_total")), _ptr(out.get("C_app")), _ptr(out.get("C_center")),
+                              _ptr(out.get("C_scale")), _ptr(out.get("C_conf")), _stream(dev))
+    check(rc, "build_cost")
+    return out
+
+
+def cost_combine(C_app: torch.Tensor, pbox: torch.Tensor, conf_prev: torch.Tensor,
+                 dbox: torch.Tensor, conf_cur: torch.Tensor, params: CostParams,
+                 gmean=None, gsinv=None, gate_on=None) -> dict:
+    """costCard.cal_cost combine given C_app (trk_cost_combine)."""
+    _need_gpu(C_app, "cost_combine")
+    M, N = C_app.shape
+    dev = C_app.device
+    out = {k: torch.empty((M, N), device=dev, dtype=torch.float32)
+           for k in ("C_total", "C_center", "C_scale", "C_conf")}
+    rc = lib().trk_cost_combine(M, N, _ptr(C_app.contiguous()), _ptr(pbox), _ptr(conf_prev), _ptr(dbox),
+                                _ptr(conf_cur), _ptr(gmean), _ptr(gsinv), _ptr(gate_on),
+                                ctypes.byref(params), _ptr(out["C_total"]), _ptr(out["C_center"]),
+                                _ptr(out["C_scale"]), _ptr(out["C_conf"]), _stream(dev))
+    check(rc, "cost_combine")
+    return out
+
+
+# ------------------------------------------------------------------ LSAP --
+def lsap_batched(C: torch.Tensor, nr: Sequence[int], nc: Sequence[int], *,
+                 cost_max: Optional[float] = None, out: Optional[dict] = None) -> dict:
+    """Batched scipy-exact LSAP (trk_lsap).  C: [F, R, ld] f32/f64 device tensor
+    (matrix f = C[f, :nr[f], :nc[f]]).  Returns device tensors rows/cols [F, kmax]
+    int64, count/status [F] int32 and, if cost_max is given, assign [F, R] int32
+    (matched column or -1 after hungarian_assign's cost gate, hung.py:35-40)."""
+    _need_gpu(C, "lsap")
+    if C.dim() != 3:
+        raise ValueError("lsap_batched expects C of shape [F, R, ld]")
+    if C.dtype not in (torch.float32, torch.float64):
+        C = C.double()
+    C = C.contiguous()
+    F, R, ld = C.shape
+    kmax = max(1, max((min(a, b) for a, b in zip(nr, nc)), default=1))
+    dev = C.device
+    if out is None:
+        out = {"rows": torch.empty((F, kmax), device=dev, dtype=torch.int64),
+               "cols": torch.empty((F, kmax), device=dev, dtype=torch.int64),
+               "count": torch.empty((F,), device=dev, dtype=torch.int32),
+               "status": torch.empty((F,), device=dev, dtype=torch.int32)}
+        if cost_max is not None:
+            out["assign"] = torch.empty((F, R), device=dev, dtype=torch.int32)
+    kmax = out["rows"].shape[1]
+    hr = (ctypes.c_int32 * max(F, 1))(*[int(x) for x in nr])
+    hc = (ctypes.c_int32 * max(F, 1))(*[int(x) for x in nc])
+    dt = _lib.TRK_F32 if C.dtype == torch.float32 else _lib.TRK_F64
+    assign = out.get("assign")
+    rc = lib().trk_lsap(F, _ptr(C), dt, ld, R * ld, hr, hc, kmax, _ptr(out["rows"]), _ptr(out["cols"]),
+                        _ptr(out["count"]), _ptr(out["status"]), _ptr(assign),
+                        R if assign is not None else 0,
+                        float(cost_max) if cost_max is not None else 0.0, _stream(dev))
+    check(rc, "lsap")
+    return out
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("linear_sum_assignment: no ROCm device (this package has no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def linear_sum_assignment(cost_matrix, maximize: bool = False):
+    """scipy.optimize.linear_sum_assignment drop-in (reference hung.py:28),
+    solved on the GPU; returns host int64 (row_ind, col_ind) like scipy."""
+    if isinstance(cost_matrix, torch.Tensor):
+        t = cost_matrix
+        if t.dim() != 2:
+            raise ValueError("expected a matrix (2-D array), got a %r array" % (tuple(t.shape),))
+    else:
+        a = np.asarray(cost_matrix)
+        if a.ndim != 2:
+            raise ValueError("expected a matrix (2-D array), got a %r array" % (a.shape,))
+        if a.dtype == np.bool_:
+            a = a.astype(np.float64)
+        if a.dtype not in (np.float32, np.float64):
+            a = a.astype(np.float64)
+        t = torch.from_numpy(np.ascontiguousarray(a))
+    if maximize:
+        t = -t.double()
+    nr, nc = t.shape
+    if nr == 0 or nc == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    t = t.to(_device(), non_blocking=False)
+    res = lsap_batched(t.reshape(1, nr, nc), [nr], [nc])
+    status = int(res["status"][0].item())
+    if status == -1:
+        raise ValueError("matrix contains invalid numeric entries")
+    if status == -2:
+        raise ValueError("cost matrix is infeasible")
+    k = int(res["count"][0].item())
+    return res["rows"][0, :k].cpu().numpy(), res["cols"][0, :k].cpu().numpy()

@@ -1,0 +1,137 @@
+/*
+ * trk_amd.h -- C ABI of the MI355X (gfx950) tracker hot-path library
+ * (libtrk_amd.so, built from a-lightweight-unsupervised-feature-extractor-_amd/csrc).
+ *
+ * The reference has no FFI layer; its boundary is a set of
+ * Python call signatures.  Each entry point below replaces the third-party
+ * native call the reference makes at that signature, and is bound from Python
+ * with ctypes (INTEGRATION.md shows the stub).  Conventions:
+ *   - all pointers are DEVICE pointers unless the name says host_;
+ *   - `stream` is a hipStream_t passed as void*; every call is asynchronous on
+ *     it and never synchronises the device (no malloc/free inside: callers pass
+ *     workspaces, so calls are hipGraph-capturable);
+ *   - return 0 on success; a negative TRK_E* code otherwise, with a message in
+ *     trk_last_error() (thread-local).  Argument errors are detected on the host
+ *     before any launch.
+ */
+#ifndef TRK_AMD_H
+#define TRK_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRK_ABI_VERSION 1
+
+enum {
+  TRK_OK = 0,
+  TRK_EINVAL = -1,     /* bad argument (shape, dtype, null pointer)        */
+  TRK_ELAUNCH = -2,    /* HIP launch / runtime error                        */
+  TRK_EUNSUPPORTED = -3/* shape outside what the kernel implements          */
+};
+
+enum { TRK_F32 = 0, TRK_BF16 = 1, TRK_F64 = 2 };
+enum { TRK_NCHW = 0, TRK_NHWC = 1 };
+
+int trk_abi_version(void);
+const char* trk_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * ROI Align forward.  Replaces torchvision.ops.roi_align as called by
+ *   MainInfer.roi_align_from_input_boxes   reference tracking.py:193-221
+ *   MainInfer._roi_align_from_input_boxes  reference model/utils/inferScr/infer.py:143-170
+ *   PreProcess._preprocess_roi             reference model/utils/trainingScr/trainingCard.py:24-79
+ * Semantics: torchvision 0.20.1 CPU kernel, bit-exact in f32.
+ *   input  [B,C,H,W] f32, layout TRK_NCHW (torchvision contract) or TRK_NHWC
+ *   rois   [K,5] f32 (batch_index, x1, y1, x2, y2) in input coordinates
+ *   out    [K,C,PH,PW] (TRK_NCHW, torchvision contract) or [K,PH,PW,C]
+ *          (TRK_NHWC, the encoder's GEMM layout); dtype TRK_F32 or TRK_BF16
+ *   workspace: >= trk_roi_align_workspace_bytes(...) bytes when the input is
+ *          NCHW (the map is transposed once to NHWC so the 4-tap gathers read
+ *          whole channel vectors); may be NULL for NHWC input.
+ * ---------------------------------------------------------------------- */
+size_t trk_roi_align_workspace_bytes(int64_t B, int64_t C, int64_t H, int64_t W, int in_layout);
+int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64_t H, int64_t W, int in_layout,
+                      const float* rois, int64_t K, float spatial_scale,
+                      int PH, int PW, int sampling_ratio, int aligned,
+                      void* out, int out_dtype, int out_layout,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Association cost, batched over F frames (one frame per video stream).
+ * Replaces, fused into one launch:
+ *   Tracking.build_C_app_topk     reference model/mainTracking.py:141-211
+ *   costCard.cal_cost/bbox_cost/conf_cost  model/utils/costTool/costCard.py:109-268
+ *   Tracking.apply_kalman_gating  model/mainTracking.py:306-338 with
+ *   gating_distance_maha          model/utils/costTool/KalmanFilter.py:105-116
+ * Per frame f (rows i < host_M[f], dets j < host_N[f]; leading dims Mmax, Nmax;
+ * host_M / host_N are HOST arrays):
+ *   track data is addressed through slot = row_slot[f*Mmax+i] (or f*Mmax+i
+ *   when row_slot == NULL):
+ *     bank      [slot][Tmax][128] f32 unit rows (already renormalised)
+ *     bank_len  [slot] int32 (<= Tmax <= 32); 0 -> C_app row of ones
+ *     pbox      [slot][4] f32 KF-predicted xyxy box (mainTracking.py:340-345)
+ *     conf_prev [slot] f32 last matched det conf
+ *     gmean     [slot][4] f64 H x_pred;  gsinv [slot][16] f64 (H P H^T + R + 1e-9 I)^-1
+ *     gate_on   [slot] int32, nonzero = apply the Mahalanobis gate to this row
+ *   dets:  det_emb [f][Nmax][128] f32, dbox [f][Nmax][4] f32, conf_cur [f][Nmax] f32
+ *   outputs [f][Mmax][Nmax] f32 (any may be NULL): C_total (gated), C_app,
+ *     C_center, C_scale, C_conf.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  float w_app, w_bbox, w_conf, alpha, beta; /* conf.yaml:8-12              */
+  double maha_thr;                          /* conf.yaml:21 (9.49)          */
+  float inf_cost;                           /* mainTracking.py:511 (1e9)    */
+  int topk;                                 /* conf.yaml:4 (emb_top_k = 5)  */
+  int gate;                                 /* 0 = no gating at all         */
+} trk_cost_params;
+
+int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* host_M, const int32_t* host_N,
+                   const int32_t* row_slot, int64_t Tmax,
+                   const float* bank, const int32_t* bank_len, const float* pbox,
+                   const float* conf_prev, const double* gmean, const double* gsinv,
+                   const int32_t* gate_on,
+                   const float* det_emb, const float* dbox, const float* conf_cur,
+                   const trk_cost_params* host_params,
+                   float* C_total, float* C_app, float* C_center, float* C_scale, float* C_conf,
+                   void* stream);
+
+/* Combine-only variant for the costCard.cal_cost API (reference
+ * model/utils/costTool/costCard.py:206-300), where C_app [M,N] is given:
+ * C_total = w_app*C_app + w_bbox*(alpha*C_center + beta*C_scale) + w_conf*C_conf,
+ * optionally Mahalanobis-gated per row (gate_on [M]).  Track arrays are [M,...],
+ * detection arrays [N,...]; outputs [M,N] f32 (any may be NULL). */
+int trk_cost_combine(int64_t M, int64_t N, const float* C_app, const float* pbox,
+                     const float* conf_prev, const float* dbox, const float* conf_cur,
+                     const double* gmean, const double* gsinv, const int32_t* gate_on,
+                     const trk_cost_params* host_params, float* C_total,
+                     float* C_center, float* C_scale, float* C_conf, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Rectangular linear sum assignment, batched over F independent matrices.
+ * Replaces scipy.optimize.linear_sum_assignment at reference
+ *   model/utils/costTool/hung.py:28 (hungarian_assign, hung.py:5-45),
+ * index-for-index identical (Crouse SAP, float64 duals, scipy tie rule).
+ *   C       [f][ld * nr[f]] f32 or f64 (TRK_F32 / TRK_F64), row-major, row
+ *           stride ld >= nc[f]; matrix f starts at C + f*batch_stride elements.
+ *   rows,cols [f][kmax] int64 (kmax >= min(nr,nc)); count [f] int32 = min(nr,nc)
+ *   status  [f] int32: 0 ok, -1 invalid numeric entries (NaN / -inf),
+ *           -2 infeasible
+ *   If assign != NULL: assign[f][nr_max] int32 = column of row i if matched and
+ *           C[i,col] <= cost_max, else -1 (hung.py:35-40's cost gate).
+ *   nr, nc are HOST arrays (shapes are decided on the host).
+ * One 64-lane wavefront per matrix; nc and nr up to TRK_LSAP_MAX_DIM.
+ * ---------------------------------------------------------------------- */
+#define TRK_LSAP_MAX_DIM 2048
+int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stride,
+             const int32_t* host_nr, const int32_t* host_nc, int64_t kmax,
+             int64_t* rows, int64_t* cols, int32_t* count, int32_t* status,
+             int32_t* assign, int64_t nr_max, double cost_max, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRK_AMD_H */

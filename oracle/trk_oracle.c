@@ -1,0 +1,350 @@
+/*
+ * trk_oracle.c -- CPU restatement of the reference's per-frame hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * kernels in a-lightweight-unsupervised-feature-extractor-_amd/csrc.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * The product path never links or calls it.
+ *
+ * Pinning:
+ *   - ora_lsap:        pinned against scipy.optimize.linear_sum_assignment
+ *                      index fixtures (tests/golden/lsap_golden.npz).
+ *   - ora_cost_build:  pinned against the reference's own costCard.cal_cost
+ *                      and Tracking.build_C_app_topk / apply_kalman_gating
+ *                      outputs (tests/golden/track_golden_*.npz).
+ *   - ora_roi_align:   torchvision is absent from the reference tree and this
+ *                      image: parity UNPINNED by a reference run; pinned by the
+ *                      analytic known-answer tests in tests/test_oracle.py.
+ *
+ * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off; no FMA contraction so
+ * every float op rounds exactly where the restated C++ source rounds).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* ROI Align forward.  Restates torchvision 0.20.1 CPU kernel semantics       */
+/* (roi_align_forward_kernel_impl + pre_calc_for_bilinear_interpolate),       */
+/* called at reference tracking.py:214-221 / infer.py:163-170 /               */
+/* trainingCard.py:70-77.  SURVEY.md Appendix A.1.                            */
+/* input [B,C,H,W] f32, rois [K,5] f32 (b,x1,y1,x2,y2), out [K,C,PH,PW] f32.  */
+/* ------------------------------------------------------------------------ */
+typedef struct { int p1, p2, p3, p4; float w1, w2, w3, w4; } ora_pc;
+
+void ora_roi_align(const float* input, int B, int C, int H, int W,
+                   const float* rois, int K, float spatial_scale,
+                   int PH, int PW, int sampling_ratio, int aligned,
+                   float* out) {
+  (void)B;
+  for (int n = 0; n < K; ++n) {
+    const float* r = rois + (size_t)n * 5;
+    int b = (int)r[0];
+    float off = aligned ? 0.5f : 0.0f;
+    float sw = r[1] * spatial_scale - off;
+    float sh = r[2] * spatial_scale - off;
+    float ew = r[3] * spatial_scale - off;
+    float eh = r[4] * spatial_scale - off;
+    float rw = ew - sw, rh = eh - sh;
+    if (!aligned) {
+      if (rw < 1.f) rw = 1.f;
+      if (rh < 1.f) rh = 1.f;
+    }
+    float bh = rh / (float)PH, bw = rw / (float)PW;
+    int gh = sampling_ratio > 0 ? sampling_ratio : (int)ceilf(rh / (float)PH);
+    int gw = sampling_ratio > 0 ? sampling_ratio : (int)ceilf(rw / (float)PW);
+    int cnt_i = gh * gw; if (cnt_i < 1) cnt_i = 1;
+    float count = (float)cnt_i;
+    int npc = gh * gw * PH * PW;
+    ora_pc* pc = (ora_pc*)malloc(sizeof(ora_pc) * (size_t)(npc > 0 ? npc : 1));
+    int idx = 0;
+    for (int ph = 0; ph < PH; ++ph)
+      for (int pw = 0; pw < PW; ++pw)
+        for (int iy = 0; iy < gh; ++iy) {
+          float t0 = sh + (float)ph * bh;
+          float yy = t0 + ((float)iy + .5f) * bh / (float)gh;
+          for (int ix = 0; ix < gw; ++ix) {
+            float s0 = sw + (float)pw * bw;
+            float xx = s0 + ((float)ix + .5f) * bw / (float)gw;
+            float x = xx, y = yy;
+            ora_pc q;
+            if ((double)y < -1.0 || y > (float)H || (double)x < -1.0 || x > (float)W) {
+              memset(&q, 0, sizeof q);
+              pc[idx++] = q;
+              continue;
+            }
+            if (y <= 0) y = 0;
+            if (x <= 0) x = 0;
+            int yl = (int)y, xl = (int)x, yhh, xhh;
+            if (yl >= H - 1) { yhh = yl = H - 1; y = (float)yl; } else yhh = yl + 1;
+            if (xl >= W - 1) { xhh = xl = W - 1; x = (float)xl; } else xhh = xl + 1;
+            float ly = y - (float)yl, lx = x - (float)xl;
+            float hy = (float)(1. - ly), hx = (float)(1. - lx);
+            q.w1 = hy * hx; q.w2 = hy * lx; q.w3 = ly * hx; q.w4 = ly * lx;
+            q.p1 = yl * W + xl; q.p2 = yl * W + xhh;
+            q.p3 = yhh * W + xl; q.p4 = yhh * W + xhh;
+            pc[idx++] = q;
+          }
+        }
+    for (int c = 0; c < C; ++c) {
+      const float* f = input + ((size_t)b * C + c) * (size_t)H * W;
+      float* o = out + ((size_t)n * C + c) * (size_t)PH * PW;
+      int k = 0;
+      for (int ph = 0; ph < PH; ++ph)
+        for (int pw = 0; pw < PW; ++pw) {
+          float v = 0.f;
+          for (int s = 0; s < gh * gw; ++s, ++k) {
+            ora_pc q = pc[k];
+            float t = q.w1 * f[q.p1];
+            t = t + q.w2 * f[q.p2];
+            t = t + q.w3 * f[q.p3];
+            t = t + q.w4 * f[q.p4];
+            v = v + t;
+          }
+          o[ph * PW + pw] = v / count;
+        }
+    }
+    free(pc);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Association cost.  Restates                                                */
+/*   Tracking.build_C_app_topk   (reference model/mainTracking.py:141-211)     */
+/*   costCard.bbox_cost          (model/utils/costTool/costCard.py:109-174)    */
+/*   costCard.conf_cost          (costCard.py:178-203)                        */
+/*   costCard.cal_cost C_total   (costCard.py:264-268)                        */
+/*   Tracking.apply_kalman_gating (mainTracking.py:306-338) with               */
+/*   KalmanFilter.gating_distance_maha (costTool/KalmanFilter.py:105-116)      */
+/* bank [M,Tmax,D] f32, bank_len [M], det [N,D] f32, pbox [M,4], dbox [N,4],   */
+/* conf_prev [M], conf_cur [N], gmean [M,4] f64 (H x_pred),                   */
+/* gsinv [M,16] f64 ((H P H^T + R + 1e-9 I)^-1), gate_mask [M] (0 = no gate). */
+/* Outputs (any may be NULL): C_total, C_app, C_center, C_scale, C_conf.      */
+/* ------------------------------------------------------------------------ */
+static void ora_normalize(const float* x, int D, float* y) {
+  double s = 0.0;
+  for (int d = 0; d < D; ++d) s += (double)x[d] * (double)x[d];
+  float nrm = (float)sqrt(s);
+  nrm = nrm + 1e-12f;
+  for (int d = 0; d < D; ++d) y[d] = x[d] / nrm;
+}
+
+static int cmp_desc(const void* a, const void* b) {
+  float x = *(const float*)a, y = *(const float*)b;
+  return (x < y) - (x > y);
+}
+
+void ora_cost_app_topk(const float* bank, const int* bank_len, int M, int Tmax,
+                       const float* det, int N, int D, int topk, float* C_app) {
+  float* dn = (float*)malloc(sizeof(float) * (size_t)N * D);
+  float* bn = (float*)malloc(sizeof(float) * (size_t)(Tmax > 0 ? Tmax : 1) * D);
+  float* col = (float*)malloc(sizeof(float) * (size_t)(Tmax > 0 ? Tmax : 1));
+  for (int j = 0; j < N; ++j) ora_normalize(det + (size_t)j * D, D, dn + (size_t)j * D);
+  for (int i = 0; i < M; ++i) {
+    int T = bank_len[i];
+    if (T > Tmax) T = Tmax;
+    int k = topk < T ? topk : T;
+    if (k <= 0) {
+      for (int j = 0; j < N; ++j) C_app[(size_t)i * N + j] = 1.0f;
+      continue;
+    }
+    for (int t = 0; t < T; ++t)
+      ora_normalize(bank + ((size_t)i * Tmax + t) * D, D, bn + (size_t)t * D);
+    for (int j = 0; j < N; ++j) {
+      for (int t = 0; t < T; ++t) {
+        double s = 0.0;
+        for (int d = 0; d < D; ++d) s += (double)bn[(size_t)t * D + d] * (double)dn[(size_t)j * D + d];
+        col[t] = (float)s;
+      }
+      qsort(col, (size_t)T, sizeof(float), cmp_desc);
+      float acc = 0.f;
+      for (int q = 0; q < k; ++q) acc = acc + col[q];
+      float mean = acc / (float)k;
+      C_app[(size_t)i * N + j] = 1.0f - mean;
+    }
+  }
+  free(dn); free(bn); free(col);
+}
+
+typedef struct {
+  float w_app, w_bbox, w_conf, alpha, beta;
+  double maha_thr;
+  float inf_cost;
+  int topk;
+} ora_cost_params;
+
+/* C_total / components from a given C_app (costCard.cal_cost + gating).    */
+void ora_cost_combine(const float* C_app, int M, int N,
+                      const float* pbox, const float* dbox,
+                      const float* conf_prev, const float* conf_cur,
+                      const double* gmean, const double* gsinv, const int* gate_mask,
+                      const ora_cost_params* prm,
+                      float* C_total, float* C_center_out,
+                      float* C_scale_out, float* C_conf_out) {
+  for (int i = 0; i < M; ++i) {
+    const float* bp = pbox + (size_t)i * 4;
+    float cpx = 0.5f * (bp[0] + bp[2]), cpy = 0.5f * (bp[1] + bp[3]);
+    float wp = bp[2] - bp[0]; if (wp < 1.0f) wp = 1.0f;
+    float hp = bp[3] - bp[1]; if (hp < 1.0f) hp = 1.0f;
+    float sp = sqrtf(wp * wp + hp * hp); if (sp < 1.0f) sp = 1.0f;
+    float Ap = wp * hp;
+    float cpv = conf_prev[i] < 1e-6f ? 1e-6f : conf_prev[i];
+    for (int j = 0; j < N; ++j) {
+      const float* bc = dbox + (size_t)j * 4;
+      float ccx = 0.5f * (bc[0] + bc[2]), ccy = 0.5f * (bc[1] + bc[3]);
+      float dx = cpx - ccx, dy = cpy - ccy;
+      /* torch.norm(diff, dim=-1) on the reference CPU path (AVX512 build)
+       * rounds as sqrtf(fmaf(dy, dy, dx*dx)) -- probed bit-exact on 200k
+       * random pairs in this container; see DESIGN.md §Oracle. */
+      float dist = sqrtf(fmaf(dy, dy, dx * dx));
+      float cen = dist / sp;
+      float wc = bc[2] - bc[0]; if (wc < 1.0f) wc = 1.0f;
+      float hc = bc[3] - bc[1]; if (hc < 1.0f) hc = 1.0f;
+      float Ac = wc * hc;
+      float ratio = Ac / Ap; if (ratio < 1e-6f) ratio = 1e-6f;
+      float scl = fabsf(logf(ratio));
+      float bbox = prm->alpha * cen + prm->beta * scl;
+      float ccv = conf_cur[j] < 1e-6f ? 1e-6f : conf_cur[j];
+      float cf = fabsf(logf(ccv / cpv));
+      float app = C_app[(size_t)i * N + j];
+      float tot = prm->w_app * app + prm->w_bbox * bbox;
+      tot = tot + prm->w_conf * cf;
+      if (gate_mask && gate_mask[i]) {
+        /* bbox_xyxy_to_z in double, rounded to float32 (KalmanFilter.py:5-16) */
+        double x1 = bc[0], y1 = bc[1], x2 = bc[2], y2 = bc[3];
+        double w = x2 - x1; if (w < 1.0) w = 1.0;
+        double h = y2 - y1; if (h < 1.0) h = 1.0;
+        double z[4] = {(float)(x1 + 0.5 * w), (float)(y1 + 0.5 * h), (float)(w / h), (float)h};
+        double y[4];
+        for (int a = 0; a < 4; ++a) y[a] = z[a] - gmean[(size_t)i * 4 + a];
+        const double* S = gsinv + (size_t)i * 16;
+        double d2 = 0.0;
+        for (int a = 0; a < 4; ++a) {
+          double t = 0.0;
+          for (int c = 0; c < 4; ++c) t += S[a * 4 + c] * y[c];
+          d2 += y[a] * t;
+        }
+        if (d2 > prm->maha_thr) tot = prm->inf_cost;
+      }
+      size_t o = (size_t)i * N + j;
+      if (C_total) C_total[o] = tot;
+      if (C_center_out) C_center_out[o] = cen;
+      if (C_scale_out) C_scale_out[o] = scl;
+      if (C_conf_out) C_conf_out[o] = cf;
+    }
+  }
+}
+
+void ora_cost_build(const float* bank, const int* bank_len, int M, int Tmax,
+                    const float* det, int N, int D,
+                    const float* pbox, const float* dbox,
+                    const float* conf_prev, const float* conf_cur,
+                    const double* gmean, const double* gsinv, const int* gate_mask,
+                    const ora_cost_params* prm,
+                    float* C_total, float* C_app_out, float* C_center_out,
+                    float* C_scale_out, float* C_conf_out) {
+  float* C_app = C_app_out ? C_app_out : (float*)malloc(sizeof(float) * (size_t)(M > 0 ? M : 1) * (N > 0 ? N : 1));
+  ora_cost_app_topk(bank, bank_len, M, Tmax, det, N, D, prm->topk, C_app);
+  ora_cost_combine(C_app, M, N, pbox, dbox, conf_prev, conf_cur, gmean, gsinv, gate_mask,
+                   prm, C_total, C_center_out, C_scale_out, C_conf_out);
+  if (!C_app_out) free(C_app);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Rectangular LSAP.  Restates scipy.optimize.linear_sum_assignment          */
+/* (Crouse shortest augmenting path, scipy/optimize/rectangular_lsap) as     */
+/* called at reference model/utils/costTool/hung.py:28.  SURVEY.md A.5.       */
+/* C [nr,nc] f64 row-major.  rows/cols: min(nr,nc) int64 each.               */
+/* Returns 0 ok, -1 invalid entries (NaN / -inf), -2 infeasible.             */
+/* ------------------------------------------------------------------------ */
+int ora_lsap(const double* Cin, int64_t nr, int64_t nc, int64_t* rows, int64_t* cols) {
+  if (nr == 0 || nc == 0) return 0;
+  int transpose = nc < nr;
+  const double* C = Cin;
+  double* tmp = NULL;
+  if (transpose) {
+    tmp = (double*)malloc(sizeof(double) * (size_t)(nr * nc));
+    for (int64_t i = 0; i < nr; ++i)
+      for (int64_t j = 0; j < nc; ++j) tmp[j * nr + i] = Cin[i * nc + j];
+    int64_t t = nr; nr = nc; nc = t;
+    C = tmp;
+  }
+  for (int64_t q = 0; q < nr * nc; ++q)
+    if (C[q] != C[q] || C[q] == -INFINITY) { free(tmp); return -1; }
+  double* u = (double*)calloc((size_t)nr, sizeof(double));
+  double* v = (double*)calloc((size_t)nc, sizeof(double));
+  double* spc = (double*)malloc(sizeof(double) * (size_t)nc);
+  int64_t* path = (int64_t*)malloc(sizeof(int64_t) * (size_t)nc);
+  int64_t* col4row = (int64_t*)malloc(sizeof(int64_t) * (size_t)nr);
+  int64_t* row4col = (int64_t*)malloc(sizeof(int64_t) * (size_t)nc);
+  char* SR = (char*)malloc((size_t)nr);
+  char* SC = (char*)malloc((size_t)nc);
+  int64_t* rem = (int64_t*)malloc(sizeof(int64_t) * (size_t)nc);
+  for (int64_t j = 0; j < nc; ++j) { path[j] = -1; row4col[j] = -1; }
+  for (int64_t i = 0; i < nr; ++i) col4row[i] = -1;
+  int status = 0;
+  for (int64_t cur = 0; cur < nr; ++cur) {
+    double minVal = 0.0;
+    int64_t nrem = nc;
+    for (int64_t it = 0; it < nc; ++it) rem[it] = nc - it - 1;
+    memset(SR, 0, (size_t)nr);
+    memset(SC, 0, (size_t)nc);
+    for (int64_t j = 0; j < nc; ++j) spc[j] = INFINITY;
+    int64_t sink = -1, i = cur;
+    while (sink == -1) {
+      int64_t index = -1;
+      double lowest = INFINITY;
+      SR[i] = 1;
+      for (int64_t it = 0; it < nrem; ++it) {
+        int64_t j = rem[it];
+        double r = minVal + C[i * nc + j] - u[i] - v[j];
+        if (r < spc[j]) { path[j] = i; spc[j] = r; }
+        if (spc[j] < lowest || (spc[j] == lowest && row4col[j] == -1)) {
+          lowest = spc[j];
+          index = it;
+        }
+      }
+      minVal = lowest;
+      if (minVal == INFINITY) { status = -2; goto done; }
+      int64_t j = rem[index];
+      if (row4col[j] == -1) sink = j; else i = row4col[j];
+      SC[j] = 1;
+      rem[index] = rem[--nrem];
+    }
+    u[cur] += minVal;
+    for (int64_t r = 0; r < nr; ++r)
+      if (SR[r] && r != cur) u[r] += minVal - spc[col4row[r]];
+    for (int64_t j = 0; j < nc; ++j)
+      if (SC[j]) v[j] -= minVal - spc[j];
+    {
+      int64_t j = sink;
+      for (;;) {
+        int64_t r = path[j];
+        row4col[j] = r;
+        int64_t t = col4row[r]; col4row[r] = j; j = t;
+        if (r == cur) break;
+      }
+    }
+  }
+  if (transpose) {
+    /* argsort(col4row): values are distinct columns of the original */
+    int64_t n = nr;
+    for (int64_t q = 0; q < n; ++q) { rows[q] = -1; }
+    /* counting placement: col4row[v] is a row of the original (< original nr) */
+    int64_t orig_nr = nc;
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)orig_nr);
+    for (int64_t q = 0; q < orig_nr; ++q) pos[q] = -1;
+    for (int64_t q = 0; q < n; ++q) pos[col4row[q]] = q;
+    int64_t k = 0;
+    for (int64_t q = 0; q < orig_nr; ++q)
+      if (pos[q] >= 0) { rows[k] = q; cols[k] = pos[q]; ++k; }
+    free(pos);
+  } else {
+    for (int64_t q = 0; q < nr; ++q) { rows[q] = q; cols[q] = col4row[q]; }
+  }
+done:
+  free(u); free(v); free(spc); free(path); free(col4row); free(row4col);
+  free(SR); free(SC); free(rem); free(tmp);
+  return status;
+}

@@ -1,0 +1,71 @@
+"""C-ABI library checks that need no GPU: it loads, exports every symbol the
+public header declares, and rejects bad arguments on the host before any
+launch (SURVEY.md 8(b) error conventions)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+
+def test_library_exports_header_symbols(trk):
+    L = trk.lib()
+    syms = trk.header_symbols()
+    assert len(syms) >= 7
+    for s in syms:
+        assert hasattr(L, s), f"libtrk_amd.so does not export {s}"
+    assert L.trk_abi_version() == 1
+
+
+def test_host_side_argument_errors(trk):
+    L = trk.lib()
+    # bad input shape -> TRK_EINVAL with a message; no device pointer touched
+    rc = L.trk_roi_align_fwd(None, 0, 512, 40, 40, 0, None, 4, 1.0, 7, 7, 2, 1, None, 0, 0, None, 0, None)
+    assert rc == -1 and b"bad input shape" in L.trk_last_error()
+    rc = L.trk_roi_align_fwd(None, 1, 512, 40, 40, 0, None, 4, 1.0, 7, 7, 0, 1, ctypes.c_void_p(8),
+                             0, 0, ctypes.c_void_p(8), 1 << 30, None)
+    assert rc == -1  # null input pointer with K > 0
+    p = trk.default_cost_params()
+    rc = L.trk_build_cost(1, 4, 4, None, None, None, 40, None, None, None, None, None, None, None,
+                          None, None, None, ctypes.byref(p), None, None, None, None, None, None)
+    assert rc == -1 and b"Tmax" in L.trk_last_error()
+    nr = (ctypes.c_int32 * 1)(5000)
+    nc = (ctypes.c_int32 * 1)(5)
+    rc = L.trk_lsap(1, ctypes.c_void_p(8), 0, 5, 25000, nr, nc, 5, ctypes.c_void_p(8), ctypes.c_void_p(8),
+                    ctypes.c_void_p(8), ctypes.c_void_p(8), None, 0, 0.0, None)
+    assert rc == -1 and b"outside" in L.trk_last_error()
+    # empty problems are valid no-ops
+    assert L.trk_lsap(0, None, 0, 0, 0, None, None, 0, None, None, None, None, None, 0, 0.0, None) == 0
+
+
+def test_python_wrappers_reject_host_tensors(trk):
+    import torch
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        trk.roi_align(torch.zeros(1, 4, 8, 8), torch.zeros(1, 5), (2, 2), 1.0, 2, True)
+
+
+def test_encoder_state_dict_keys_and_strict_load(trk):
+    import torch
+    import gen_common as G
+    m = trk.Model(in_channels=512, out_channels=512, warmup_epochs=10, proj_dim=128)
+    keys = [k for k, _ in G.encoder_param_shapes()]
+    assert list(m.state_dict().keys()) == keys
+    assert sum(p.numel() for p in m.parameters()) == 2061570
+    sd = {k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}
+    m.load_state_dict(sd, strict=True)
+
+
+@pytest.mark.parametrize("s", [7, 10])
+def test_encoder_fused_graph_fp32_vs_reference_golden(trk, s):
+    """The fused encoder graph (encoder.py) is pure PyTorch: its fp32 numerics
+    are checked here on CPU and again on the GPU in test_gpu_kernels.py."""
+    import os
+    import torch
+    import gen_common as G
+    from conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()})
+    x = torch.from_numpy(G.encoder_input(int(d[f"seed_s{s}"]), 16, s))
+    with torch.no_grad():
+        z = m(x).numpy()
+    assert np.max(np.abs(z - d[f"z_s{s}"])) < 1e-5

@@ -1,0 +1,292 @@
+"""Parity of the gfx950 kernels (through the C ABI) against the CPU oracle and
+the reference's golden vectors.  Tolerances are written in each test:
+  roi_align f32: bit-exact;  bf16 output: == bf16(round-to-nearest of f32)
+  cost: |d| <= 2e-6 (f32 dot-order / logf ulp differences), gate decisions equal
+  lsap: indices bit-exact (scipy semantics)
+  encoder fp32: <= 1e-4 (north star);  bf16: cosine >= 0.999 vs fp32
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+import gen_common as G
+
+pytestmark = pytest.mark.gpu
+
+
+# ----------------------------------------------------------------- helpers
+def _boxes(rng, n, img=1280, pad=280):
+    w = rng.uniform(32, 320, n)
+    h = rng.uniform(32, 320, n)
+    x1 = rng.uniform(-8, img - w + 8)
+    y1 = rng.uniform(pad - 8, img - pad - h + 8)
+    return np.stack([x1, y1, x1 + w, y1 + h], 1).astype(np.float32)
+
+
+def _feat(rng, B, C=512, H=40, W=40):
+    return G.silu_np(rng.standard_normal((B, C, H, W)).astype(np.float32)).astype(np.float32)
+
+
+# --------------------------------------------------------------- roi_align
+@pytest.mark.parametrize("N", [16, 64, 256])
+@pytest.mark.parametrize("S", [7, 10])
+def test_roi_align_bit_exact_vs_oracle(trk, oracle, gpu, N, S):
+    rng = np.random.default_rng(N * 10 + S)
+    feat = _feat(rng, 1)
+    boxes = _boxes(rng, N)
+    rois = np.concatenate([np.zeros((N, 1), np.float32), boxes], 1)
+    exp = oracle.roi_align(feat, rois, (S, S), 40 / 1280.0, 2, True)
+    x = torch.from_numpy(feat).to(gpu)
+    r = torch.from_numpy(rois).to(gpu)
+    got = trk.roi_align(x, r, (S, S), 40 / 1280.0, 2, True)
+    assert got.shape == (N, 512, S, S) and got.is_contiguous()
+    assert np.array_equal(got.cpu().numpy(), exp)
+    nhwc = trk.roi_align(x, r, (S, S), 40 / 1280.0, 2, True, channels_last=True)
+    assert nhwc.is_contiguous(memory_format=torch.channels_last)
+    assert np.array_equal(nhwc.cpu().numpy(), exp)
+    bf = trk.roi_align(x, r, (S, S), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+    assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16())
+
+
+def test_roi_align_batched_frames_and_edges(trk, oracle, gpu):
+    rng = np.random.default_rng(3)
+    B, N = 8, 256
+    feat = _feat(rng, B)
+    boxes = _boxes(rng, B * N)
+    bidx = np.repeat(np.arange(B), N).astype(np.float32)[:, None]
+    rois = np.concatenate([bidx, boxes], 1)
+    # edge cases: fully outside, crossing every border, degenerate, tiny, huge
+    rois[0, 1:] = [2000, 2000, 2100, 2100]
+    rois[1, 1:] = [-300, -300, 100, 100]
+    rois[2, 1:] = [1200, 1200, 1400, 1500]
+    rois[3, 1:] = [500, 500, 500, 500]
+    rois[4, 1:] = [600, 610, 600.5, 611]
+    rois[5, 1:] = [-50, -50, 1330, 1330]
+    rois[6, 1:] = [700, 700, 650, 640]  # inverted
+    exp = oracle.roi_align(feat, rois, (10, 10), 1 / 32, 2, True)
+    x = torch.from_numpy(feat).to(gpu)
+    r = torch.from_numpy(rois).to(gpu)
+    got = trk.roi_align(x, r, (10, 10), 1 / 32, 2, True)
+    assert np.array_equal(got.cpu().numpy(), exp)
+    # channels_last input skips the transpose, same result
+    got2 = trk.roi_align(x.contiguous(memory_format=torch.channels_last), r, (10, 10), 1 / 32, 2, True)
+    assert np.array_equal(got2.cpu().numpy(), exp)
+    # aligned=False, other sampling ratio, non-square bins
+    exp3 = oracle.roi_align(feat, rois[:300], (7, 5), 1 / 32, 3, False)
+    got3 = trk.roi_align(x, r[:300], (7, 5), 1 / 32, 3, False)
+    assert np.array_equal(got3.cpu().numpy(), exp3)
+
+
+def test_roi_align_odd_channels_and_empty(trk, oracle, gpu):
+    rng = np.random.default_rng(4)
+    feat = rng.standard_normal((2, 37, 13, 11)).astype(np.float32)
+    rois = np.array([[1, 10, 20, 200, 300], [0, 0, 0, 30, 30]], np.float32)
+    exp = oracle.roi_align(feat, rois, (3, 4), 1 / 16, 2, True)
+    got = trk.roi_align(torch.from_numpy(feat).to(gpu), torch.from_numpy(rois).to(gpu), (3, 4), 1 / 16, 2, True)
+    assert np.array_equal(got.cpu().numpy(), exp)
+    e = trk.roi_align(torch.from_numpy(feat).to(gpu), torch.zeros((0, 5), device=gpu), (7, 7), 1.0, 2, True)
+    assert e.shape == (0, 37, 7, 7)
+
+
+def test_roi_align_from_input_boxes_reference_contract(trk, oracle, gpu):
+    rng = np.random.default_rng(5)
+    feat = _feat(rng, 1)
+    boxes = _boxes(rng, 33).astype(np.float64).tolist()
+    got = trk.roi_align_from_input_boxes(torch.from_numpy(feat).to(gpu), boxes, (1280, 1280), out_size=(7, 7))
+    rois = np.array([[0.0] + b for b in boxes], np.float32)
+    exp = oracle.roi_align(feat, rois, (7, 7), 40 / 1280.0, 2, True)
+    assert np.array_equal(got.cpu().numpy(), exp)
+
+
+# -------------------------------------------------------------------- cost
+def _state_from_golden(d, f):
+    tids = d[f"f{f}_state_tids"]
+    rows = d[f"f{f}_rows_main"]
+    sel = np.searchsorted(tids, rows)
+    return {k: d[f"f{f}_state_{k}"][sel] for k in ("bank", "bank_len", "pbox", "last_conf", "kf_x", "kf_P")}
+
+
+def _renorm(x):
+    x = np.asarray(x, np.float32)
+    n = np.sqrt((x.astype(np.float64) ** 2).sum(-1, keepdims=True)).astype(np.float32) + np.float32(1e-12)
+    return (x / n).astype(np.float32)
+
+
+def _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf, gate=True):
+    M, N = bank.shape[0], det.shape[0]
+    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(gpu, dt)
+    out = trk.build_cost(M=[M], N=[N], bank=t(_renorm(bank)), bank_len=t(blen, torch.int32), pbox=t(pbox),
+                         conf_prev=t(lconf), det_emb=t(det[None]), dbox=t(dbox[None]),
+                         conf_cur=t(dconf[None]), params=trk.default_cost_params(gate=gate),
+                         gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
+                         gate_on=t(np.ones(M, np.int32), torch.int32),
+                         want=("C_total", "C_app", "C_center", "C_scale", "C_conf"))
+    return {k: v[0].cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("name", ["s16", "s64", "reid"])
+def test_cost_kernel_vs_reference_golden(trk, oracle, gpu, name):
+    d = np.load(os.path.join(GOLDEN, f"track_golden_{name}.npz"))
+    n = 0
+    for f in d["dump_frames"]:
+        if f"f{f}_rows_main" not in d.files or f"f{f}_state_tids" not in d.files:
+            continue
+        st = _state_from_golden(d, f)
+        a, b = d["det_off"][f], d["det_off"][f + 1]
+        gm, gs = oracle.gate_params(st["kf_x"], st["kf_P"])
+        got = _run_cost(trk, gpu, st["bank"], st["bank_len"], st["pbox"], st["last_conf"], gm, gs,
+                        d["embs"][a:b], d["boxes"][a:b].astype(np.float32), d["confs"][a:b].astype(np.float32))
+        assert np.max(np.abs(got["C_app"] - d[f"f{f}_C_app"])) <= 2e-6
+        for k in ("C_center", "C_scale", "C_conf"):
+            assert np.max(np.abs(got[k] - d[f"f{f}_{k}"])) <= 2e-6, k
+        gated = d[f"f{f}_C_gated"]
+        assert np.array_equal(got["C_total"] >= 1e9, gated >= 1e9)
+        assert np.max(np.abs(got["C_total"] - gated)) <= 2e-6
+        n += 1
+    assert n >= 2
+
+
+def test_cost_kernel_full_size_vs_oracle(trk, oracle, gpu):
+    """N = M = 256, full banks (T = 30) and ragged banks, gate on."""
+    rng = np.random.default_rng(21)
+    M = N = 256
+    base = _renorm(rng.standard_normal((M, 128)))
+    bank = _renorm(base[:, None, :] + 0.05 * rng.standard_normal((M, 30, 128)))
+    blen = np.full(M, 30, np.int32)
+    blen[:40] = rng.integers(0, 30, 40)
+    bank[np.arange(30)[None, :] >= blen[:, None]] = 0
+    perm = rng.permutation(N)
+    det = _renorm(base[perm] + 0.05 * rng.standard_normal((N, 128)))
+    pbox = _boxes(rng, M)
+    dbox = pbox[perm] + rng.normal(0, 2, (N, 4)).astype(np.float32)
+    lconf = rng.uniform(0.55, 0.99, M).astype(np.float32)
+    dconf = rng.uniform(0.55, 0.99, N).astype(np.float32)
+    x = np.zeros((M, 8)); x[:, :4] = np.stack([(pbox[:, 0] + pbox[:, 2]) / 2, (pbox[:, 1] + pbox[:, 3]) / 2,
+                                               (pbox[:, 2] - pbox[:, 0]) / (pbox[:, 3] - pbox[:, 1]),
+                                               pbox[:, 3] - pbox[:, 1]], 1)
+    P = np.tile(np.diag([10., 10, 10, 10, 1000, 1000, 1000, 1000]), (M, 1, 1))
+    gm, gs = oracle.gate_params(x, P)
+    got = _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf)
+    exp = oracle.cost_build(_renorm(bank), blen, det, pbox, dbox, lconf, dconf, gm, gs, np.ones(M, np.int32))
+    assert np.max(np.abs(got["C_app"] - exp["C_app"])) <= 2e-6
+    assert np.array_equal(got["C_total"] >= 1e9, exp["C_total"] >= 1e9)
+    assert np.max(np.abs(got["C_total"] - exp["C_total"])) <= 2e-6
+    assert (exp["C_total"] >= 1e9).mean() > 0.5  # the gate is exercised
+
+
+def test_cost_batched_frames_with_row_slots(trk, oracle, gpu):
+    rng = np.random.default_rng(22)
+    F, Mmax, Nmax, S = 3, 40, 48, 200
+    bank = _renorm(rng.standard_normal((S, 30, 128)))
+    blen = rng.integers(1, 31, S).astype(np.int32)
+    pbox = _boxes(rng, S)
+    lconf = rng.uniform(0.3, 1, S).astype(np.float32)
+    Ms, Ns = [40, 17, 0], [48, 5, 9]
+    slots = np.stack([rng.permutation(S)[:Mmax] for _ in range(F)]).astype(np.int32)
+    det = _renorm(rng.standard_normal((F, Nmax, 128)))
+    dbox = np.stack([_boxes(rng, Nmax) for _ in range(F)])
+    dconf = rng.uniform(0.3, 1, (F, Nmax)).astype(np.float32)
+    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(gpu, dt)
+    out = trk.build_cost(M=Ms, N=Ns, bank=t(bank), bank_len=t(blen, torch.int32), pbox=t(pbox),
+                         conf_prev=t(lconf), det_emb=t(det), dbox=t(dbox), conf_cur=t(dconf),
+                         params=trk.default_cost_params(gate=False), row_slot=t(slots, torch.int32),
+                         want=("C_total", "C_app"))
+    for f in range(F):
+        M, N = Ms[f], Ns[f]
+        if M == 0:
+            continue
+        s = slots[f, :M]
+        exp = oracle.cost_build(bank[s], blen[s], det[f, :N], pbox[s], dbox[f, :N], lconf[s], dconf[f, :N])
+        assert np.max(np.abs(out["C_total"][f, :M, :N].cpu().numpy() - exp["C_total"])) <= 2e-6
+
+
+def test_costcard_api_vs_reference_golden(trk, gpu):
+    d = np.load(os.path.join(GOLDEN, "costcard_golden.npz"))
+    for tag in "abc":
+        out = trk.cal_cost(C_app=torch.from_numpy(d[f"{tag}_capp"]).to(gpu), boxes_prev=d[f"{tag}_bp"].tolist(),
+                           boxes_cur=d[f"{tag}_bc"].tolist(), input_hw=(1280, 1280),
+                           conf_prev=d[f"{tag}_cp"].tolist(), conf_cur=d[f"{tag}_cu"].tolist())
+        for k in ("C_total", "C_center", "C_scale", "C_conf", "C_bbox"):
+            assert np.max(np.abs(out[k].cpu().numpy() - d[f"{tag}_{k}"])) <= 2e-6, k
+
+
+# -------------------------------------------------------------------- LSAP
+def _lsap_cases():
+    d = np.load(os.path.join(GOLDEN, "lsap_golden.npz"))
+    pos = 0
+    for q, (r, c) in enumerate(d["shapes"]):
+        C = d["data"][pos:pos + r * c].reshape(r, c)
+        pos += r * c
+        yield q, C, d["rows"][d["offs"][q]:d["offs"][q + 1]], d["cols"][d["offs"][q]:d["offs"][q + 1]], int(d["status"][q])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_lsap_vs_scipy_golden(trk, gpu, dtype):
+    for q, C, rows, cols, st in _lsap_cases():
+        if st == 0:
+            r, c = trk.linear_sum_assignment(C.astype(dtype))
+            assert np.array_equal(r, rows) and np.array_equal(c, cols), f"case {q} {C.shape}"
+        else:
+            with pytest.raises(ValueError, match="invalid" if st == -1 else "infeasible"):
+                trk.linear_sum_assignment(C.astype(dtype))
+
+
+def test_lsap_batched_one_launch(trk, gpu):
+    cases = [(C, r, c) for _, C, r, c, st in _lsap_cases() if st == 0]
+    R = max(C.shape[0] for C, _, _ in cases)
+    L = max(C.shape[1] for C, _, _ in cases)
+    buf = np.zeros((len(cases), R, L), np.float32)
+    for k, (C, _, _) in enumerate(cases):
+        buf[k, :C.shape[0], :C.shape[1]] = C
+    res = trk.lsap_batched(torch.from_numpy(buf).to(gpu), [C.shape[0] for C, _, _ in cases],
+                           [C.shape[1] for C, _, _ in cases], cost_max=50.0)
+    rows, cols, cnt = res["rows"].cpu().numpy(), res["cols"].cpu().numpy(), res["count"].cpu().numpy()
+    assert (res["status"].cpu().numpy() == 0).all()
+    for k, (C, r, c) in enumerate(cases):
+        assert np.array_equal(rows[k, :cnt[k]], r) and np.array_equal(cols[k, :cnt[k]], c), k
+
+
+def test_hungarian_assign_vs_reference_golden(trk, gpu):
+    d = np.load(os.path.join(GOLDEN, "lsap_golden.npz"))
+    cases = [C for _, C, _, _, _ in _lsap_cases()]
+    for k, (q, cm) in enumerate(zip(d["hm_q"], d["hm_cost_max"])):
+        m, ut, ud = trk.hungarian_assign(cases[q], cost_max=float(cm))
+        exp = d["hm_match"][d["hm_moff"][k]:d["hm_moff"][k + 1]]
+        assert np.array_equal(np.asarray(m, np.int64).reshape(-1, 2), exp)
+        M, N = cases[q].shape
+        assert sorted(ut + [i for i, _ in m]) == list(range(M))
+        assert sorted(ud + [j for _, j in m]) == list(range(N))
+    assert trk.hungarian_assign(np.zeros((0, 3))) == ([], [], [0, 1, 2])
+    assert trk.hungarian_assign(np.zeros((2, 0))) == ([], [0, 1], [])
+
+
+def test_lsap_full_size_vs_oracle(trk, oracle, gpu):
+    rng = np.random.default_rng(30)
+    mats = [rng.random((256, 256)).astype(np.float32),
+            rng.integers(0, 3, (256, 256)).astype(np.float32),
+            np.where(rng.random((256, 256)) < 0.9, np.float32(1e9), rng.random((256, 256)).astype(np.float32)),
+            rng.random((300, 256)).astype(np.float32), rng.random((200, 512)).astype(np.float32),
+            rng.random((1024, 1024)).astype(np.float32)]
+    for C in mats:
+        r, c = trk.linear_sum_assignment(C)
+        er, ec = oracle.lsap(C)
+        assert np.array_equal(r, er) and np.array_equal(c, ec), C.shape
+
+
+# ----------------------------------------------------------------- encoder
+@pytest.mark.parametrize("s", [7, 10])
+def test_encoder_gpu_vs_reference_golden(trk, gpu, s):
+    d = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()})
+    m = m.to(gpu)
+    x = torch.from_numpy(G.encoder_input(int(d[f"seed_s{s}"]), 16, s)).to(gpu)
+    with torch.no_grad():
+        z = m(x).cpu().numpy()
+        zb = m(x.bfloat16().contiguous(memory_format=torch.channels_last)).float().cpu().numpy()
+    exp = d[f"z_s{s}"]
+    assert np.max(np.abs(z - exp)) <= 1e-4
+    assert (zb * exp).sum(1).min() >= 0.999

@@ -1,0 +1,166 @@
+"""Pin the CPU oracle against the reference's golden vectors (CPU-only)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+import gen_common as G
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+# ---------------------------------------------------------------- LSAP ----
+def _lsap_cases():
+    d = _load("lsap_golden.npz")
+    shapes, data, offs = d["shapes"], d["data"], d["offs"]
+    pos = 0
+    for q, (r, c) in enumerate(shapes):
+        C = data[pos:pos + r * c].reshape(r, c)
+        pos += r * c
+        yield q, C, d["rows"][offs[q]:offs[q + 1]], d["cols"][offs[q]:offs[q + 1]], int(d["status"][q])
+
+
+def test_lsap_matches_scipy_golden(oracle):
+    n = 0
+    for q, C, rows, cols, st in _lsap_cases():
+        if st == 0:
+            r, c = oracle.lsap(C)
+            assert np.array_equal(r, rows) and np.array_equal(c, cols), f"case {q} {C.shape}"
+        else:
+            with pytest.raises(ValueError, match="invalid" if st == -1 else "infeasible"):
+                oracle.lsap(C)
+        n += 1
+    assert n >= 150
+
+
+def test_hungarian_assign_golden(oracle):
+    d = _load("lsap_golden.npz")
+    cases = [C for _, C, _, _, _ in _lsap_cases()]
+    for k, (q, cm) in enumerate(zip(d["hm_q"], d["hm_cost_max"])):
+        m, _, _ = oracle.hungarian_assign(cases[q], cost_max=float(cm))
+        exp = d["hm_match"][d["hm_moff"][k]:d["hm_moff"][k + 1]]
+        assert np.array_equal(np.asarray(m, np.int64).reshape(-1, 2), exp)
+
+
+def test_lsap_empty_and_errors(oracle):
+    r, c = oracle.lsap(np.zeros((0, 5)))
+    assert r.shape == (0,) and c.dtype == np.int64
+    with pytest.raises(ValueError):
+        oracle.lsap(np.array([[1.0, -np.inf]]))
+
+
+# ---------------------------------------------------------------- cost ----
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_costcard_formula_bit_exact(oracle, tag):
+    d = _load("costcard_golden.npz")
+    out = oracle.cost_combine(d[f"{tag}_capp"], d[f"{tag}_bp"], d[f"{tag}_bc"],
+                              d[f"{tag}_cp"], d[f"{tag}_cu"])
+    for k in ("C_center", "C_scale", "C_conf", "C_bbox", "C_total"):
+        exp = d[f"{tag}_{k}"]
+        got = out[k]
+        # bit-exact except transcendental ulps (torch CPU log is SLEEF, C logf is glibc)
+        assert np.max(np.abs(got - exp)) <= 2e-6 * max(1.0, np.abs(exp).max()), k
+    assert np.array_equal(out["C_center"], d[f"{tag}_C_center"])
+
+
+@pytest.mark.parametrize("name", ["s16", "s64", "reid"])
+def test_cost_and_gate_vs_reference_tracker(oracle, name):
+    d = _load(f"track_golden_{name}.npz")
+    det_off = d["det_off"]
+    checked = 0
+    for f in d["dump_frames"]:
+        if f"f{f}_rows_main" not in d.files or f"f{f}_state_tids" not in d.files:
+            continue
+        tids = d[f"f{f}_state_tids"]
+        rows = d[f"f{f}_rows_main"]
+        sel = np.searchsorted(tids, rows)
+        a, b = det_off[f], det_off[f + 1]
+        st = {k: d[f"f{f}_state_{k}"][sel] for k in ("bank", "bank_len", "pbox", "last_conf", "kf_x", "kf_P")}
+        gm, gs = oracle.gate_params(st["kf_x"], st["kf_P"])
+        out = oracle.cost_build(st["bank"], st["bank_len"], d["embs"][a:b], st["pbox"], d["boxes"][a:b],
+                                st["last_conf"], d["confs"][a:b], gm, gs, np.ones(len(rows), np.int32))
+        assert np.max(np.abs(out["C_app"] - d[f"f{f}_C_app"])) < 1e-5
+        pre = oracle.cost_build(st["bank"], st["bank_len"], d["embs"][a:b], st["pbox"], d["boxes"][a:b],
+                                st["last_conf"], d["confs"][a:b])
+        assert np.max(np.abs(pre["C_total"] - d[f"f{f}_C_total"])) < 1e-5
+        for k in ("C_center", "C_scale", "C_conf"):
+            assert np.max(np.abs(pre[k] - d[f"f{f}_{k}"])) < 1e-5, k
+        gated = d[f"f{f}_C_gated"]
+        assert np.array_equal(out["C_total"] >= 1e9, gated >= 1e9)
+        assert np.max(np.abs(out["C_total"] - gated)) < 1e-5
+        checked += 1
+    assert checked >= 2
+
+
+@pytest.mark.parametrize("name", ["s16", "s64", "reid"])
+def test_stage1_assignment_on_reference_costs(oracle, name):
+    """hungarian_assign on the reference's own gated cost reproduces the
+    reference's stage-1 matches for every frame (mainTracking.py:514-534)."""
+    d = _load(f"track_golden_{name}.npz")
+    n = 0
+    for f in range(int(d["n_frames"])):
+        if f"f{f}_C_gated" not in d.files:
+            continue
+        rows = d[f"f{f}_rows_main"]
+        m, _, _ = oracle.hungarian_assign(d[f"f{f}_C_gated"], cost_max=50.0)
+        exp = d["matches"][d["m_off"][f]:d["m_off"][f + 1]]
+        got = np.array([(rows[i], j) for i, j in m], np.int64).reshape(-1, 2)
+        assert np.array_equal(got, exp[:len(got)])
+        n += 1
+    assert n > 5
+
+
+# ---------------------------------------------------------- ROI Align ----
+def test_roi_align_constant_map(oracle):
+    x = np.full((1, 3, 12, 12), 2.5, np.float32)
+    rois = np.array([[0, 1.5, 2.0, 8.0, 9.5], [0, 0.0, 0.0, 11.0, 11.0]], np.float32)
+    out = oracle.roi_align(x, rois, (7, 7), 1.0)
+    assert np.allclose(out, 2.5, atol=1e-6)
+
+
+def test_roi_align_affine_ramp_exact(oracle):
+    """f(y,x) = 3x + 2y + 1 is reproduced exactly by bilinear sampling inside
+    the map: each bin = value at the mean sample position."""
+    H = W = 16
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    x = (3 * xx + 2 * yy + 1)[None, None].astype(np.float32)
+    x1, y1, x2, y2 = 2.25, 3.0, 10.75, 12.5
+    out = oracle.roi_align(x, np.array([[0, x1, y1, x2, y2]], np.float32), (4, 4), 1.0, 2, True)
+    sw, sh = x1 - 0.5, y1 - 0.5
+    bw, bh = (x2 - x1) / 4, (y2 - y1) / 4
+    for ph in range(4):
+        for pw in range(4):
+            cy = sh + (ph + 0.5) * bh
+            cx = sw + (pw + 0.5) * bw
+            assert abs(out[0, 0, ph, pw] - (3 * cx + 2 * cy + 1)) < 1e-4
+
+
+def test_roi_align_out_of_bounds_zero(oracle):
+    x = np.random.default_rng(0).standard_normal((1, 2, 8, 8)).astype(np.float32)
+    out = oracle.roi_align(x, np.array([[0, 100, 100, 140, 150]], np.float32), (3, 3), 1.0)
+    assert np.all(out == 0)
+
+
+def test_roi_align_batch_index_and_scale(oracle):
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((2, 4, 10, 10)).astype(np.float32)
+    r = np.array([[1, 40, 48, 200, 260]], np.float32)
+    a = oracle.roi_align(x, r, (5, 5), 1 / 32)
+    r0 = r.copy(); r0[0, 0] = 0
+    b = oracle.roi_align(x[1:], r0, (5, 5), 1 / 32)
+    assert np.array_equal(a, b)
+
+
+# ------------------------------------------------------------ encoder ----
+@pytest.mark.parametrize("s", [7, 10])
+def test_encoder_restatement_vs_reference(oracle, s):
+    import torch
+    d = _load("encoder_golden.npz")
+    sd = {k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}
+    x = torch.from_numpy(G.encoder_input(int(d[f"seed_s{s}"]), 16, s))
+    with torch.no_grad():
+        z = oracle.encoder_forward(sd, x).numpy()
+    assert np.max(np.abs(z - d[f"z_s{s}"])) < 1e-5
