@@ -54,6 +54,12 @@ def _declare(L):
     L.trk_cost_combine.restype = i32
     L.trk_lsap.argtypes = [i64, P, i32, i64, i64, P, P, i64, P, P, P, P, P, i64, f64, P]
     L.trk_lsap.restype = i32
+    L.trk_dwconv5_nhwc.argtypes = [P, P, P, i64, i64, i64, i64, i32, P]
+    L.trk_dwconv5_nhwc.restype = i32
+    L.trk_act_mean.argtypes = [P, P, P, i64, i64, i64, i32, i32, P]
+    L.trk_act_mean.restype = i32
+    L.trk_scale_rows.argtypes = [P, P, i64, i64, i64, i32, P]
+    L.trk_scale_rows.restype = i32
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

@@ -132,6 +132,29 @@ class Model(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.training:
             raise NotImplementedError("training-mode forward is out of scope (inference hot path only)")
+        if x.is_cuda:
+            return self._forward_device(x)
+        return self._forward_host(x)
+
+    def _alpha(self):
+        r = self.rmb
+        return 0.5 if r.current_epoch < r.warmup_epochs else float(torch.rand(1))  # RMB.forward :141
+
+    def _head(self, g):
+        hd = self.head.net
+        z = F.linear(g, hd[0].weight.float())
+        z = F.layer_norm(z, (z.shape[1],), hd[1].weight.float(), hd[1].bias.float(), hd[1].eps)
+        z = F.linear(F.silu(z), hd[4].weight.float(), hd[4].bias.float())
+        return F.normalize(z, dim=1)
+
+    def _se(self, m_r):
+        se = self.rmb.se.excitation
+        return F.hardsigmoid(F.linear(F.relu(F.linear(m_r, se[0].weight.float(), se[0].bias.float())),
+                                      se[2].weight.float(), se[2].bias.float()))
+
+    def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
+        """GEMMs on hipBLASLt (torch), everything else in trk HIP kernels."""
+        from .ops import act_mean, dwconv5_nhwc, scale_rows
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -139,27 +162,41 @@ class Model(nn.Module):
         h2 = h4 // 2
         ss = S1 * S2
         X = x.permute(0, 2, 3, 1).reshape(N * ss, C)                 # view when channels_last
-        Y1 = X @ W["w1t"]                                            # [N*ss, 4h]
-        Y1 = Y1.view(N, S1, S2, h4).permute(0, 3, 1, 2)               # NCHW logical, NHWC storage
-        Y2 = F.conv2d(Y1, W["dw"], padding=W["dw"].shape[-1] // 2, groups=h4)
-        Y2 = Y2.permute(0, 2, 3, 1).reshape(N * ss, h4)
-        xr = F.silu(torch.addmm(W["br"], Y2[:, :h2], W["w2r"]))        # DSC reinforce + BN + SiLU
-        xn = F.hardswish(torch.addmm(W["bn"], Y2[:, h2:], W["w2n"]))   # DSC normal + BN + Hardswish
-        xr3 = xr.view(N, ss, C)
-        m_r = xr3.mean(1, dtype=torch.float32)                        # SE squeeze
-        se = self.rmb.se.excitation
-        s = F.hardsigmoid(F.linear(F.relu(F.linear(m_r, se[0].weight, se[0].bias)), se[2].weight, se[2].bias))
-        xfs = (xr3 * s.to(dt)[:, None, :]).view(N * ss, C)
+        Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)                      # 4 first 1x1 convs, one GEMM
+        Y2 = dwconv5_nhwc(Y1, W["dw"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
+        xr = torch.addmm(W["br"], Y2[:, :h2], W["w2r"]).view(N, ss, C)   # DSC reinforce (BN folded)
+        xn = torch.addmm(W["bn"], Y2[:, h2:], W["w2n"]).view(N, ss, C)   # DSC normal (BN folded)
+        m_r = act_mean(xr, "silu")                                   # SiLU + SE squeeze
+        m_n = act_mean(xn, "hardswish")                              # Hardswish + its GAP
+        s = self._se(m_r)
+        scale_rows(xr, s)                                            # x_f * s
+        T = torch.addmm(W["bt"], xr.view(N * ss, C), W["wt1"])
+        T.addmm_(xn.view(N * ss, C), W["wt2"])                       # transition over cat[x_f*s, x_n]
+        m_cat = act_mean(T.view(N, ss, C), "silu", write=False)      # SiLU + GAP, no write-back
+        a = self._alpha()
+        g = 0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n)     # Shake2 eval :94-96 + GAP
+        return self._head(g)
+
+    def _forward_host(self, x: torch.Tensor) -> torch.Tensor:
+        """The same fused graph in plain torch ops (CPU tensors)."""
+        N, C, S1, S2 = x.shape
+        dt, dev = x.dtype, x.device
+        W = self._fused_weights(dt, dev)
+        h4 = W["w1t"].shape[1]
+        h2 = h4 // 2
+        ss = S1 * S2
+        X = x.permute(0, 2, 3, 1).reshape(N * ss, C)
+        Y1 = (X @ W["w1t"]).view(N, S1, S2, h4).permute(0, 3, 1, 2)
+        Y2 = F.conv2d(Y1, W["dw"], padding=2, groups=h4).permute(0, 2, 3, 1).reshape(N * ss, h4)
+        xr = F.silu(torch.addmm(W["br"], Y2[:, :h2], W["w2r"])).view(N, ss, C)
+        xn = F.hardswish(torch.addmm(W["bn"], Y2[:, h2:], W["w2n"])).view(N, ss, C)
+        m_r = xr.mean(1, dtype=torch.float32)
+        s = self._se(m_r)
+        xfs = (xr * s.to(dt)[:, None, :]).view(N * ss, C)
         T = torch.addmm(W["bt"], xfs, W["wt1"])
-        T.addmm_(xn, W["wt2"])                                        # transition over cat[x_f*s, x_n]
+        T.addmm_(xn.reshape(N * ss, C), W["wt2"])
         m_cat = F.silu(T).view(N, ss, C).mean(1, dtype=torch.float32)
-        m_n = xn.view(N, ss, C).mean(1, dtype=torch.float32)
-        r = self.rmb
-        alpha = 0.5 if r.current_epoch < r.warmup_epochs else float(torch.rand(1))
-        m_fuse = alpha * (s * m_r) + (1 - alpha) * m_n               # RMB.forward :141-142
-        g = 0.5 * m_cat + 0.5 * m_fuse                                # Shake2 eval :94-96, GAP
-        hd = self.head.net
-        z = F.linear(g, hd[0].weight.float())
-        z = F.layer_norm(z, (z.shape[1],), hd[1].weight.float(), hd[1].bias.float(), hd[1].eps)
-        z = F.linear(F.silu(z), hd[4].weight.float(), hd[4].bias.float())
-        return F.normalize(z, dim=1)
+        m_n = xn.mean(1, dtype=torch.float32)
+        a = self._alpha()
+        g = 0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n)
+        return self._head(g)

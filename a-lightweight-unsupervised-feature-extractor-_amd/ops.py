@@ -15,7 +15,7 @@ import torch
 from . import _lib
 from ._lib import CostParams, check, lib
 
-__all__ = ["roi_align", "roi_align_from_input_boxes", "build_cost", "cost_combine", "lsap_batched",
+__all__ = ["dwconv5_nhwc", "act_mean", "scale_rows", "roi_align", "roi_align_from_input_boxes", "build_cost", "cost_combine", "lsap_batched",
            "linear_sum_assignment", "CostParams", "default_cost_params"]
 
 
@@ -30,6 +30,52 @@ def _stream(dev: torch.device):
 def _need_gpu(t: torch.Tensor, what: str):
     if not isinstance(t, torch.Tensor) or not t.is_cuda:
         raise RuntimeError(f"{what}: expected a ROCm device tensor (this package has no CPU fallback)")
+
+
+# -------------------------------------------------------- encoder helpers --
+_ACT = {None: 0, "none": 0, "silu": 1, "hardswish": 2}
+
+
+def _edt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return _lib.TRK_F32
+    if t.dtype == torch.bfloat16:
+        return _lib.TRK_BF16
+    raise TypeError(f"expected float32 or bfloat16, got {t.dtype}")
+
+
+def dwconv5_nhwc(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Depthwise 5x5 / pad 2 on NHWC storage x [N, H, W, C]; weight [C, 1, 5, 5]
+    (card.DSC depth.1/point.1).  Returns [N, H, W, C] in x.dtype."""
+    _need_gpu(x, "dwconv5_nhwc")
+    N, H, W, C = x.shape
+    x = x.contiguous()
+    w = weight.reshape(C, 25).to(torch.float32).contiguous()
+    out = torch.empty_like(x)
+    check(lib().trk_dwconv5_nhwc(_ptr(x), _ptr(w), _ptr(out), N, H, W, C, _edt(x), _stream(x.device)),
+          "dwconv5_nhwc")
+    return out
+
+
+def act_mean(x: torch.Tensor, act: Optional[str], *, inplace: bool = True,
+             write: bool = True) -> torch.Tensor:
+    """x [N, P, C] contiguous: x <- act(x) (if write), returns mean over P (f32 [N, C])."""
+    _need_gpu(x, "act_mean")
+    N, P, C = x.shape
+    mean = torch.empty((N, C), device=x.device, dtype=torch.float32)
+    out = (x if inplace else torch.empty_like(x)) if write else None
+    check(lib().trk_act_mean(_ptr(x), _ptr(out), _ptr(mean), N, P, C, _ACT[act], _edt(x),
+                             _stream(x.device)), "act_mean")
+    return mean
+
+
+def scale_rows(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """x [N, P, C] *= s[N, C] in place."""
+    _need_gpu(x, "scale_rows")
+    N, P, C = x.shape
+    s = s.to(torch.float32).contiguous()
+    check(lib().trk_scale_rows(_ptr(x), _ptr(s), N, P, C, _edt(x), _stream(x.device)), "scale_rows")
+    return x
 
 
 # ------------------------------------------------------------- ROI Align --

@@ -131,6 +131,22 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
              int64_t* rows, int64_t* cols, int32_t* count, int32_t* status,
              int32_t* assign, int64_t nr_max, double cost_max, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Encoder helpers (the non-GEMM parts of encoderAndHead.Model's eval graph,
+ * reference model/utils/modules/card.py:48-148, encoderAndHead.py:26-31).
+ * Activations are NHWC rows [N, P = S*S, C], dtype TRK_F32 or TRK_BF16.
+ * ---------------------------------------------------------------------- */
+/* depthwise 5x5, stride 1, zero pad 2 (card.py:28-29,38-39 DSC depth.1/point.1):
+ * in/out [N,H,W,C] (must not alias), weight [C][25] f32.  W <= 32. */
+int trk_dwconv5_nhwc(const void* in, const float* weight, void* out, int64_t N, int64_t H,
+                     int64_t W, int64_t C, int dtype, void* stream);
+/* y = act(x) (act 0 none, 1 SiLU, 2 Hardswish), written to out (may equal x,
+ * may be NULL); mean [N, C] f32 = mean over the P pixels of y. */
+int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, int64_t C,
+                 int act, int dtype, void* stream);
+/* x[n, p, c] *= s[n, c] in place (SE excitation, card.py:78). */
+int trk_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
