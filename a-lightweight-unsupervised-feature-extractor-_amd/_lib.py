@@ -41,6 +41,8 @@ def _declare(L):
     L.trk_abi_version.restype = i32
     L.trk_last_error.argtypes = []
     L.trk_last_error.restype = ctypes.c_char_p
+    L.trk_set_tuning.argtypes = [ctypes.c_char_p, i32]
+    L.trk_set_tuning.restype = i32
     L.trk_roi_align_workspace_bytes.argtypes = [i64, i64, i64, i64, i32]
     L.trk_roi_align_workspace_bytes.restype = sz
     L.trk_roi_align_fwd.argtypes = [P, i64, i64, i64, i64, i32, P, i64, f32, i32, i32, i32, i32,
@@ -96,6 +98,11 @@ def check(rc: int, what: str):
         if rc == -3:
             raise NotImplementedError(f"{what}: {msg}")
         raise TrkError(f"{what} failed ({rc}): {msg}")
+
+
+def set_tuning(key: str, value: int):
+    """Process-global performance knob (include/trk_amd.h trk_set_tuning)."""
+    check(lib().trk_set_tuning(key.encode(), int(value)), "set_tuning")
 
 
 def header_symbols():

@@ -41,7 +41,7 @@ constexpr int kMaxW = 32;   // max spatial width handled in registers
 // grid: (N * ceil(C/64)); block: 32 x H threads (channel pair x output row);
 // kW = compile-time row width (>= W) so the register row is exactly sized
 template <typename T, int kW>
-__global__ void dwconv5_nhwc_kernel(const T* __restrict__ in, const float* __restrict__ w,
+__global__ void __launch_bounds__(512) dwconv5_nhwc_kernel(const T* __restrict__ in, const float* __restrict__ w,
                                     T* __restrict__ out, int N, int H, int W, int C, int nchunk) {
   using PS = typename Pair<T>::S;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -52,18 +52,46 @@ __global__ void dwconv5_nhwc_kernel(const T* __restrict__ in, const float* __res
   const int npair = nch / 2;
   const int tid = threadIdx.x;
   const PS* src = reinterpret_cast<const PS*>(in + ((int64_t)n * H * W) * C + c0);
-  // stage [H*W][npair] (pixel stride C/2 pairs in global)
-  for (int q = tid; q < H * W * 32; q += blockDim.x) {
-    const int p = q / 32, cp = q % 32;
-    if (cp < npair) tile[q] = src[(int64_t)p * (C / 2) + cp];
+  // stage [H*W][32 pairs] with 16-B pieces, BATCH loads in flight per thread
+  constexpr int EPP = 16 / (int)sizeof(T);             // elements per 16-B piece
+  constexpr int PPP = kDwCh / EPP;                      // pieces per pixel
+  constexpr int BATCH = 4;
+  const int total = H * W * PPP;
+  const bool vec_ok = (C % EPP) == 0;
+  for (int q0 = tid; q0 < total; q0 += blockDim.x * BATCH) {
+    uint4 tmp[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int q = q0 + (int)blockDim.x * k;
+      const int p = q / PPP, e = (q % PPP) * EPP;
+      tmp[k] = (q < total && vec_ok && e < nch)
+                   ? *reinterpret_cast<const uint4*>(in + ((int64_t)n * H * W + p) * C + c0 + e)
+                   : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int q = q0 + (int)blockDim.x * k;
+      if (q >= total) continue;
+      const int p = q / PPP, e = (q % PPP) * EPP;
+      if (vec_ok && e < nch) {
+        *reinterpret_cast<uint4*>(reinterpret_cast<char*>(tile + p * 32) + (q % PPP) * 16) = tmp[k];
+      } else {
+        for (int kk = 0; kk < EPP; kk += 2)
+          if (e + kk < nch) tile[p * 32 + (e + kk) / 2] = src[(int64_t)p * (C / 2) + (e + kk) / 2];
+      }
+    }
   }
   __syncthreads();
   const int cp = tid % 32, y = tid / 32;
   if (cp >= npair || y >= H) return;
   const int c = c0 + 2 * cp;
-  float wa[25], wb[25];
+  float wa[25], wb[25];  // weights stored tap-major [25][C]: one 8-B load per tap
 #pragma unroll
-  for (int k = 0; k < 25; ++k) { wa[k] = w[(int64_t)c * 25 + k]; wb[k] = w[(int64_t)(c + 1) * 25 + k]; }
+  for (int k = 0; k < 25; ++k) {
+    const float2 ww = *reinterpret_cast<const float2*>(w + (int64_t)k * C + c);
+    wa[k] = ww.x;
+    wb[k] = ww.y;
+  }
   float acc_a[kW], acc_b[kW];
 #pragma unroll
   for (int x = 0; x < kW; ++x) { acc_a[x] = 0.f; acc_b[x] = 0.f; }
@@ -156,7 +184,7 @@ extern "C" int trk_dwconv5_nhwc(const void* in, const float* weight, void* out, 
                                 int64_t W, int64_t C, int dtype, void* stream) {
   TRK_REQUIRE(dtype == TRK_F32 || dtype == TRK_BF16, "dwconv5: dtype must be f32 or bf16");
   TRK_REQUIRE(N >= 0 && H >= 1 && W >= 1 && C >= 2 && C % 2 == 0, "dwconv5: bad shape");
-  TRK_REQUIRE(W <= kMaxW && 32 * H <= 1024, "dwconv5: spatial size %lldx%lld above 32x32",
+  TRK_REQUIRE(W <= kMaxW && 32 * H <= 512, "dwconv5: spatial size %lldx%lld above 16 rows x 32 cols",
               (long long)H, (long long)W);
   if (N == 0) return TRK_OK;
   TRK_REQUIRE(in && weight && out && in != out, "dwconv5: null or aliased pointer");

@@ -8,26 +8,38 @@
 //     pick it if spc[j] < lowest || (spc[j] == lowest && row4col[j] == -1)
 // which selects, among the minimum entries, the LAST unassigned column in
 // `remaining` order, else the FIRST one.  The serial scan becomes a wavefront
-// argmin over the lexicographic key (spc, unassigned ? -1-it : it).
+// argmin over the lexicographic key (spc, unassigned ? -1-pos : pos), where
+// pos is the column's position in `remaining`.
 //
-// Latency design: one 64-lane wavefront per matrix, so every
-// lane-to-lane hand-off is LDS traffic of one wave (in order), synchronised by
-// wavefront-scope fences only -- no s_barrier, no vmcnt drains.  All solver
-// state lives in LDS.  The cost matrix is cached whole in LDS when it fits;
-// otherwise the row of the NEXT augmentation (cur+1, known in advance) is
-// prefetched into registers while row cur is solved and parked in an LDS row
-// buffer, so the common tracking case (one scan per row) never waits on L2.
-// Removed columns are swapped to the tail of `remaining` (same order for the
-// live prefix as scipy's overwrite), so SC = remaining[nrem:] and the visited
-// rows are kept in a list: nothing is reset per row except spc and remaining.
-// Only +,- and comparisons touch the duals (no FMA to contract); the file is
-// still built with -ffp-contract=off.
+// Latency design.  One workgroup per matrix = 1 solver wave
+// + 3 loader waves.
+//  * Solver (wave 0): column j lives in lane j % 64, slot j / 64, and ALL
+//    per-column state (v, spc, path, row4col, position in `remaining`) is held
+//    in registers, so a scan touches LDS only for the cost row and u[i].  The
+//    swap-remove of `remaining` is one register update in the lane owning the
+//    moved column; SC = "existed and no longer alive"; the visited rows are the
+//    row4col of the removed non-sink columns, so the dual update is register-
+//    local plus one scatter to u[] in LDS.  Lane-to-lane hand-offs inside the
+//    solver wave need only a compiler barrier (LDS ops of a wave are in order).
+//  * Loaders (waves 1-3) stream the rows the solver will augment next (row cur
+//    is known in advance) into an LDS ring of RB rows, check every entry for
+//    NaN / -inf on the way (scipy's validity test), and publish each row with a
+//    per-slot ready word.  The solver spins (s_sleep) only when it outruns
+//    them.  Loaders stay at most LA rows ahead, so the RB - LA most recently
+//    solved rows remain resident and a revisited row (an assigned row on an
+//    augmenting path) is read from LDS too unless it is older than that; only
+//    then is it gathered from global memory.  When the whole matrix fits
+//    (RB >= nr) nothing is ever evicted.
+// Only +,- and comparisons touch the duals (no FMA); built -ffp-contract=off.
 #include "trk_common.h"
+
+#include <type_traits>
 
 namespace {
 
 constexpr int kMaxBatch = 64;
-constexpr int kPrefetchCols = 512;  // row prefetch up to nc <= 512 (8 regs per lane)
+constexpr int kLoaders = 3;
+constexpr uint32_t kSpinLimit = 1u << 26;  // bounded waits (never expected to trigger)
 
 struct LsapArgs {
   const void* C;
@@ -38,7 +50,7 @@ struct LsapArgs {
   int32_t* status;
   int32_t* assign;
   double cost_max;
-  int cache;  // 1: whole (working) cost matrix copied into LDS
+  int ring_rows;  // RB (ring capacity in rows) for the largest working nc of the batch
   int nr[kMaxBatch];
   int nc[kMaxBatch];
 };
@@ -47,205 +59,317 @@ __device__ __forceinline__ bool key_less(double v1, int k1, double v2, int k2) {
   return v1 < v2 || (v1 == v2 && k1 < k2);
 }
 
-// single-wavefront workgroup: order LDS traffic between lanes without s_barrier
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
-// LDS bytes used by the solver state for a WORKING (nr <= nc) problem
-__host__ __device__ inline size_t state_bytes(int nr, int nc) {
-  return 8 * (size_t)(nr + 2 * nc)          // u, v, spc
-         + 4 * (size_t)(3 * nc + 2 * nr)    // path, row4col, rem, col4row, srlist
-         + 16;
+__device__ __forceinline__ int ld_relaxed(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ int ld_acquire(int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void st_release(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// One step of a wavefront argmin over (value, key, column) with DPP lane moves
+// (no LDS crossbar): lanes whose DPP source is out of range read the identity.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void argmin_step(double& v, int& key, int& col) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(0x7ff00000, hi, CTRL, ROWMASK, 0xF, false);  // +inf
+  const int ok = __builtin_amdgcn_update_dpp(0x7fffffff, key, CTRL, ROWMASK, 0xF, false);
+  const int oc = __builtin_amdgcn_update_dpp(-1, col, CTRL, ROWMASK, 0xF, false);
+  const double ov = __hiloint2double(ohi, olo);
+  const bool take = key_less(ov, ok, v, key);
+  v = take ? ov : v;
+  key = take ? ok : key;
+  col = take ? oc : col;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(64)
+// lexicographic min over the wave; the result is returned wave-uniform
+// (row_shr 1/2/4/8 inside each row of 16, then row_bcast15 / row_bcast31,
+// total in lane 63).  (value, key) pairs are unique per column, so the order
+// of combination cannot change the result.
+__device__ __forceinline__ void wave_argmin(double& v, int& key, int& col) {
+  argmin_step<0x111, 0xF>(v, key, col);  // row_shr:1
+  argmin_step<0x112, 0xF>(v, key, col);  // row_shr:2
+  argmin_step<0x114, 0xF>(v, key, col);  // row_shr:4
+  argmin_step<0x118, 0xF>(v, key, col);  // row_shr:8
+  argmin_step<0x142, 0xA>(v, key, col);  // row_bcast:15
+  argmin_step<0x143, 0xC>(v, key, col);  // row_bcast:31
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  v = __hiloint2double(hi, lo);
+  key = __builtin_amdgcn_readlane(key, 63);
+  col = __builtin_amdgcn_readlane(col, 63);
+}
+
+template <typename T, int KS>
+__global__ void __launch_bounds__(256)
 lsap_kernel(const LsapArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int f = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nr0 = A.nr[f], nc0 = A.nc[f];
   const T* C = reinterpret_cast<const T*>(A.C) + (int64_t)f * A.batch_stride;
   int32_t* assign = A.assign ? A.assign + (int64_t)f * A.nr_max : nullptr;
   int64_t* orows = A.rows + (int64_t)f * A.kmax;
   int64_t* ocols = A.cols + (int64_t)f * A.kmax;
-  if (assign)
-    for (int r = lane; r < nr0; r += 64) assign[r] = -1;
   if (nr0 == 0 || nc0 == 0) {
-    if (lane == 0) { A.count[f] = 0; A.status[f] = 0; }
+    if (assign)
+      for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
+    if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = 0; }
     return;
   }
   const bool tr = nc0 < nr0;
-  const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;
+  const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;  // working problem: nr <= nc
   const int64_t ld = A.ld;
+  const int RB = min(A.ring_rows, nr);
+  const bool whole = RB >= nr;
+  // loaders run at most LA rows ahead of the solver, so the RB - LA most
+  // recently solved rows stay resident for revisits (rows on augmenting paths)
+  const int LA = whole ? RB : max(1, min(16, RB / 2));
 
+  // LDS: u[nr] f64 | col4row[nr] i32 | ready[RB] i32 | ctl[4] i32 | ring[RB][nc] T
   double* u = reinterpret_cast<double*>(smem);
-  double* v = u + nr;
-  double* spc = v + nc;
-  int* path = reinterpret_cast<int*>(spc + nc);
-  int* row4col = path + nc;
-  int* rem = row4col + nc;
-  int* col4row = rem + nc;
-  int* srlist = col4row + nr;
-  T* extra = reinterpret_cast<T*>(
-      (reinterpret_cast<uintptr_t>(srlist + nr) + 15) & ~uintptr_t(15));
-  // extra = whole matrix (cache) or 2 row buffers of nc (prefetch mode)
-  const bool cache = A.cache != 0;
-  const bool prefetch = !cache && nc <= kPrefetchCols;
+  int* col4row = reinterpret_cast<int*>(u + nr);
+  int* ready = col4row + nr;     // ready[s] = q + 1 when ring slot s holds row q
+  int* ctl = ready + RB;         // ctl[0] = rows finished by the solver, ctl[1] = invalid entry seen
+  // offset arithmetic on the LDS base (an integer round trip would turn every
+  // ring access into a flat load)
+  const size_t ring_off = ((size_t)(12 * nr + 4 * RB + 16) + 15) & ~size_t(15);
+  T* ring = reinterpret_cast<T*>(smem + ring_off);
+
+  for (int q = threadIdx.x; q < RB; q += blockDim.x) ready[q] = 0;
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) { u[r] = 0.0; col4row[r] = -1; }
+  if (threadIdx.x < 4) ctl[threadIdx.x] = 0;
+  __syncthreads();
 
   auto gload = [&](int i, int j) -> T {  // working-matrix element from global
     return tr ? C[(int64_t)j * ld + i] : C[(int64_t)i * ld + j];
   };
 
-  // ---- validity scan (NaN / -inf -> "invalid numeric entries") + LDS cache
-  int bad = 0;
-  for (int64_t q = lane; q < (int64_t)nr0 * nc0; q += 64) {
-    const int r = (int)(q / nc0), c = (int)(q % nc0);
-    const T x = C[(int64_t)r * ld + c];
-    if (x != x || x == (T)-INFINITY) bad = 1;
-    if (cache) {
-      if (tr) extra[(int64_t)c * nc + r] = x;
-      else extra[q] = x;
-    }
-  }
-  if (__any(bad)) {
-    if (lane == 0) { A.count[f] = 0; A.status[f] = -1; }
-    return;
-  }
-
-  for (int r = lane; r < nr; r += 64) { u[r] = 0.0; col4row[r] = -1; }
-  for (int c = lane; c < nc; c += 64) { v[c] = 0.0; path[c] = -1; row4col[c] = -1; }
-  T pre[kPrefetchCols / 64];
-  if (prefetch) {  // row 0 straight into buffer 0
-    for (int c = lane; c < nc; c += 64) extra[c] = gload(0, c);
-  }
-  wave_sync();
-
-  int status = 0;
-  for (int cur = 0; cur < nr; ++cur) {
-    const T* rowbuf = prefetch ? extra + (int64_t)(cur & 1) * nc : nullptr;
-    // prefetch row cur+1 into registers; committed to LDS after this row
-    if (prefetch && cur + 1 < nr) {
+  if (wave > 0) {
+    // ------------------------------------------------------------ loaders
+    int bad = 0;
+    for (int q = wave - 1; q < nr; q += kLoaders) {
+      // at most LA rows ahead of the solver (ctl[0] = rows it has finished);
+      // this also keeps slot q % RB free (row q - RB is long finished)
+      uint32_t spins = 0;
+      while (q >= ld_relaxed(&ctl[0]) + LA) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kSpinLimit) break;
+      }
+      T* dst = ring + (int64_t)(q % RB) * nc;
+      constexpr int U = 8;  // loads in flight per lane
+      for (int c0 = lane; c0 < nc; c0 += 64 * U) {
+        T tmp[U];
 #pragma unroll
-      for (int k = 0; k < kPrefetchCols / 64; ++k) {
-        const int c = lane + 64 * k;
-        if (c < nc) pre[k] = gload(cur + 1, c);
-      }
-    }
-    for (int c = lane; c < nc; c += 64) {
-      rem[c] = nc - c - 1;
-      spc[c] = INFINITY;
-    }
-    wave_sync();
-    double minVal = 0.0;
-    int nrem = nc, i = cur, sink = -1, nsr = 0;
-    while (sink == -1) {
-      if (lane == 0) srlist[nsr] = i;
-      ++nsr;
-      const double ui = u[i];
-      double best = INFINITY;
-      int bkey = 0x7fffffff;
-      for (int it = lane; it < nrem; it += 64) {
-        const int j = rem[it];
-        T cij;
-        if (cache) cij = extra[(int64_t)i * nc + j];
-        else if (prefetch && i == cur) cij = rowbuf[j];
-        else cij = gload(i, j);
-        const double r = ((minVal + (double)cij) - ui) - v[j];
-        double s = spc[j];
-        if (r < s) { path[j] = i; spc[j] = r; s = r; }
-        const int key = row4col[j] == -1 ? -1 - it : it;
-        if (key_less(s, key, best, bkey)) { best = s; bkey = key; }
-      }
+        for (int k = 0; k < U; ++k) {
+          const int c = c0 + 64 * k;
+          tmp[k] = c < nc ? gload(q, c) : (T)0;
+        }
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const double ob = __shfl_xor(best, off);
-        const int ok = __shfl_xor(bkey, off);
-        if (key_less(ob, ok, best, bkey)) { best = ob; bkey = ok; }
+        for (int k = 0; k < U; ++k) {
+          const int c = c0 + 64 * k;
+          if (c < nc) {
+            if (tmp[k] != tmp[k] || tmp[k] == (T)-INFINITY) bad = 1;
+            dst[c] = tmp[k];
+          }
+        }
       }
-      minVal = best;
-      if (minVal == INFINITY) { status = -2; break; }
-      const int idx = bkey < 0 ? -1 - bkey : bkey;
+      if (__any(bad) && lane == 0) ctl[1] = 1;
       wave_sync();
-      const int j = rem[idx];
-      const int rj = row4col[j];
-      if (rj == -1) sink = j; else i = rj;
-      wave_sync();
-      if (lane == 0) {  // swap-remove: live prefix matches scipy, SC = tail
-        rem[idx] = rem[nrem - 1];
-        rem[nrem - 1] = j;
+      if (lane == 0) st_release(&ready[q % RB], q + 1);
+    }
+  } else {
+    // ------------------------------------------------------------- solver
+    double v[KS], spc[KS];
+    int path[KS], r4c[KS], pos[KS];
+    bool exists[KS], alive[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      exists[k] = lane + 64 * k < nc;
+      v[k] = 0.0;
+      path[k] = -1;
+      r4c[k] = -1;
+    }
+    int status = 0;
+    for (int cur = 0; cur < nr; ++cur) {
+      {  // wait for row cur
+        uint32_t spins = 0;
+        while (ld_acquire(&ready[cur % RB]) != cur + 1) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kSpinLimit) { status = -3; break; }
+        }
+        if (status) break;
       }
-      --nrem;
+      if (ld_relaxed(&ctl[1])) { status = -1; break; }  // invalid entry: result is the error
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        spc[k] = INFINITY;
+        alive[k] = exists[k];
+        pos[k] = nc - 1 - (lane + 64 * k);  // remaining = [nc-1, ..., 0]
+      }
+      double minVal = 0.0;
+      int nrem = nc, i = cur, sink = -1;
+      while (sink == -1) {
+        const double ui = u[i];
+        // the row comes from the LDS ring (row cur, or any row when the whole
+        // matrix is resident) or, for a revisited row, from global memory --
+        // two separate loops so the LDS one compiles to ds_read (a merged
+        // pointer would become flat_load + a full s_waitcnt per element)
+        T cv[KS];
+        // row i < cur is still resident unless a loader may be overwriting it:
+        // loaders write rows <= cur + LA - 1, evicting rows <= cur + LA - 1 - RB
+        if (i == cur || whole || i >= cur + LA - RB) {
+          const int slot = whole ? i : i % RB;
+          const T* lrow = ring + (int64_t)slot * nc;
+#pragma unroll
+          for (int k = 0; k < KS; ++k) cv[k] = exists[k] ? lrow[lane + 64 * k] : (T)0;
+        } else {
+#pragma unroll
+          for (int k = 0; k < KS; ++k) cv[k] = alive[k] ? gload(i, lane + 64 * k) : (T)0;
+        }
+        double best = INFINITY;
+        int bkey = 0x7fffffff, bcol = -1;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {  // branch-free: dead columns are masked
+          const double r = ((minVal + (double)cv[k]) - ui) - v[k];
+          const bool upd = alive[k] && r < spc[k];
+          path[k] = upd ? i : path[k];
+          spc[k] = upd ? r : spc[k];
+          const int key = r4c[k] == -1 ? -1 - pos[k] : pos[k];
+          const bool take = alive[k] && key_less(spc[k], key, best, bkey);
+          best = take ? spc[k] : best;
+          bkey = take ? key : bkey;
+          bcol = take ? lane + 64 * k : bcol;
+        }
+        wave_argmin(best, bkey, bcol);
+        minVal = best;
+        if (minVal == INFINITY) { status = -2; break; }
+        const int idx = bkey < 0 ? -1 - bkey : bkey;  // position in `remaining`
+        const int j = bcol;
+        const int jk = j >> 6;
+        int rsel = -1;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) rsel = (k == jk) ? r4c[k] : rsel;
+        const int rj = __builtin_amdgcn_readlane(rsel, j & 63);
+        if (rj == -1) sink = j; else i = rj;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {  // swap-remove: pos nrem-1 moves to idx
+          const bool me = lane + 64 * k == j;
+          pos[k] = (alive[k] && !me && pos[k] == nrem - 1) ? idx : pos[k];
+          alive[k] = alive[k] && !me;
+        }
+        --nrem;
+      }
+      if (status) break;
+      // dual update (scipy order: u[cur], the other visited rows, the columns)
+      if (lane == 0) u[cur] += minVal;
       wave_sync();
-    }
-    if (status) break;
-    // dual update (scipy order: u[cur] first, then the other visited rows,
-    // then the removed columns); visited rows are distinct, as are columns
-    if (lane == 0) u[cur] += minVal;
-    wave_sync();
-    for (int q = lane + 1; q < nsr; q += 64) {
-      const int r = srlist[q];
-      u[r] += minVal - spc[col4row[r]];
-    }
-    for (int it = nrem + lane; it < nc; it += 64) {
-      const int c = rem[it];
-      v[c] -= minVal - spc[c];
-    }
-    wave_sync();
-    if (lane == 0) {  // augment along path
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        if (!exists[k] || alive[k]) continue;
+        const double d = minVal - spc[k];
+        if (lane + 64 * k != sink) u[r4c[k]] += d;
+        v[k] -= d;
+      }
+      wave_sync();
+      // augment along path (serial; one owner lane per step)
       int j = sink;
       for (;;) {
-        const int r = path[j];
-        row4col[j] = r;
+        const int ol = j & 63, ok = j >> 6;
+        int pr = -1;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) pr = (k == ok) ? path[k] : pr;
+        const int r = __builtin_amdgcn_readlane(pr, ol);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) r4c[k] = (lane == ol && k == ok) ? r : r4c[k];
         const int t = col4row[r];
-        col4row[r] = j;
+        wave_sync();
+        if (lane == 0) col4row[r] = j;
+        wave_sync();
         j = t;
         if (r == cur) break;
       }
+      if (lane == 0) st_release(&ctl[0], cur + 1);  // slot cur % RB may be refilled
     }
-    if (prefetch && cur + 1 < nr) {
-      T* nb = extra + (int64_t)((cur + 1) & 1) * nc;
+    if (lane == 0) {
+      ctl[2] = status;
+      if (status) ctl[0] = 0x3fffffff;  // release any waiting loader
+    }
+    // the transposed result lives in r4c registers: park it in the (now idle) ring
+    if (tr) {
+      int* r4c_out = reinterpret_cast<int*>(ring);
 #pragma unroll
-      for (int k = 0; k < kPrefetchCols / 64; ++k) {
-        const int c = lane + 64 * k;
-        if (c < nc) nb[c] = pre[k];
-      }
+      for (int k = 0; k < KS; ++k)
+        if (exists[k]) r4c_out[lane + 64 * k] = r4c[k];
     }
-    wave_sync();
   }
-
+  __syncthreads();
+  int status = ctl[2];
+  if (ctl[1]) status = -1;  // an invalid entry anywhere -> scipy raises (checked first)
   if (status) {
-    if (lane == 0) { A.count[f] = 0; A.status[f] = status; }
+    if (assign)
+      for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
+    if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = status == -3 ? -2 : status; }
     return;
   }
-  const int k = nr;  // = min(nr0, nc0)
   if (!tr) {
-    for (int q = lane; q < nr; q += 64) {
+    for (int q = threadIdx.x; q < nr; q += blockDim.x) {
       const int c = col4row[q];
       orows[q] = q;
       ocols[q] = c;
       if (assign) assign[q] = ((double)C[(int64_t)q * ld + c] <= A.cost_max) ? c : -1;
     }
   } else {
-    // argsort(col4row): col4row[q] (an original row) is distinct per q
-    int* pos = reinterpret_cast<int*>(spc);  // nc (= original nr) ints fit in spc
-    for (int c = lane; c < nc; c += 64) pos[c] = -1;
-    wave_sync();
-    for (int q = lane; q < nr; q += 64) pos[col4row[q]] = q;
-    wave_sync();
-    if (lane == 0) {
-      int w = 0;
-      for (int r = 0; r < nc; ++r)
-        if (pos[r] >= 0) { orows[w] = r; ocols[w] = pos[r]; ++w; }
+    // argsort(col4row): working column j (= original row j) is matched to
+    // working row r4c[j] (= original column); emit in ascending j
+    const int* r4c_out = reinterpret_cast<const int*>(ring);
+    if (assign)
+      for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
+    if (wave == 0) {
+      int base = 0;
+      for (int j0 = 0; j0 < nc; j0 += 64) {
+        const int j = j0 + lane;
+        const int rc = j < nc ? r4c_out[j] : -1;
+        const uint64_t bal = __ballot(rc >= 0);
+        if (rc >= 0) {
+          const int w = base + __popcll(bal & ((1ull << lane) - 1));
+          orows[w] = j;
+          ocols[w] = rc;
+        }
+        base += __popcll(bal);
+      }
     }
-    for (int q = lane; q < nr; q += 64) {
-      const int r0 = col4row[q];  // original row matched to original column q
-      if (assign) assign[r0] = ((double)C[(int64_t)r0 * ld + q] <= A.cost_max) ? q : -1;
-    }
+    __syncthreads();
+    if (assign)
+      for (int j = threadIdx.x; j < nc; j += blockDim.x) {
+        const int rc = r4c_out[j];
+        if (rc >= 0) assign[j] = ((double)C[(int64_t)j * ld + rc] <= A.cost_max) ? rc : -1;
+      }
   }
-  if (lane == 0) { A.count[f] = k; A.status[f] = 0; }
+  if (threadIdx.x == 0) { A.count[f] = nr; A.status[f] = 0; }
+}
+
+template <typename T>
+int launch_ks(int wc, dim3 g, size_t lds, hipStream_t st, const LsapArgs& a) {
+  auto go = [&](auto ks) {
+    constexpr int KS = decltype(ks)::value;
+    static bool attr_set = false;
+    if (!attr_set) {  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per CU)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lsap_kernel<T, KS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL((lsap_kernel<T, KS>), g, dim3(64 * (1 + kLoaders)), lds, st, a);
+  };
+  if (wc <= 64) go(std::integral_constant<int, 1>{});
+  else if (wc <= 256) go(std::integral_constant<int, 4>{});
+  else if (wc <= 512) go(std::integral_constant<int, 8>{});
+  else if (wc <= 1024) go(std::integral_constant<int, 16>{});
+  else go(std::integral_constant<int, 32>{});
+  return trk::check_launch("lsap_kernel");
 }
 
 }  // namespace
@@ -260,12 +384,12 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
   TRK_REQUIRE(host_nr && host_nc && rows && cols && count && status, "lsap: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const size_t esz = dtype == TRK_F32 ? 4 : 8;
-  const size_t lds_limit = 150 * 1024;
+  const size_t lds_limit = 156 * 1024;
   for (int64_t f0 = 0; f0 < F; f0 += kMaxBatch) {
     const int nf = (int)std::min<int64_t>(kMaxBatch, F - f0);
     LsapArgs a;
     memset(&a, 0, sizeof a);
-    size_t lds_state = 0, lds_cache = 0, lds_rows = 0;
+    int wr_max = 1, wc_max = 1;
     for (int q = 0; q < nf; ++q) {
       const int r = host_nr[f0 + q], c = host_nc[f0 + q];
       TRK_REQUIRE(r >= 0 && c >= 0 && r <= TRK_LSAP_MAX_DIM && c <= TRK_LSAP_MAX_DIM,
@@ -276,12 +400,18 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
       TRK_REQUIRE(!assign || r <= nr_max, "lsap: nr_max %lld < nr %d", (long long)nr_max, r);
       a.nr[q] = r;
       a.nc[q] = c;
-      const int wr = std::min(r, c), wc = std::max(r, c);  // working (transposed if tall)
-      lds_state = std::max(lds_state, state_bytes(wr, wc));
-      lds_cache = std::max(lds_cache, esz * (size_t)r * c);
-      lds_rows = std::max(lds_rows, wc <= kPrefetchCols ? 2 * esz * (size_t)wc : 0);
+      wr_max = std::max(wr_max, std::min(r, c));
+      wc_max = std::max(wc_max, std::max(r, c));
     }
     TRK_REQUIRE(C, "lsap: null cost pointer");
+    // fixed part: u (8) + col4row (4) per working row, control words, alignment
+    const size_t fixed = 12 * (size_t)wr_max + 64;
+    const size_t row_bytes = esz * (size_t)wc_max + 4;  // + its ready word
+    TRK_REQUIRE(fixed + 2 * row_bytes <= lds_limit, "lsap: matrix too wide for the LDS ring");
+    int rb = (int)std::min<size_t>((lds_limit - fixed) / row_bytes, (size_t)wr_max);
+    rb = std::max(rb, 2);
+    a.ring_rows = rb;
+    const size_t lds = fixed + (size_t)rb * row_bytes + 16;
     a.C = reinterpret_cast<const char*>(C) + (size_t)f0 * batch_stride * esz;
     a.ld = ld;
     a.batch_stride = batch_stride;
@@ -293,21 +423,9 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
-    a.cache = lds_state + lds_cache <= lds_limit ? 1 : 0;
-    const size_t lds = lds_state + (a.cache ? lds_cache : lds_rows);
-    static bool attr_set = false;
-    if (!attr_set) {  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per CU)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lsap_kernel<float>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lsap_kernel<double>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
-    if (dtype == TRK_F32)
-      hipLaunchKernelGGL(lsap_kernel<float>, dim3(nf), dim3(64), lds, st, a);
-    else
-      hipLaunchKernelGGL(lsap_kernel<double>, dim3(nf), dim3(64), lds, st, a);
-    if (int e = trk::check_launch("lsap_kernel")) return e;
+    int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
+                             : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
+    if (e) return e;
   }
   return TRK_OK;
 }

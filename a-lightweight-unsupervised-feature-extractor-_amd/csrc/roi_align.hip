@@ -98,86 +98,139 @@ nchw_to_nhwc_kernel(const float* __restrict__ in, float* __restrict__ out,
   }
 }
 
-template <int VEC, bool OUT_BF16, bool OUT_NHWC>
-__global__ void __launch_bounds__(256)
-roi_align_nhwc_kernel(const float* __restrict__ in,  // [B,H,W,C]
-                      int B, int C, int H, int W,
-                      const float* __restrict__ rois, int K, float spatial_scale,
-                      int PH, int PW, int sampling_ratio, int aligned,
-                      void* __restrict__ out, int nchunks, int lds_stride) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  constexpr int CPW = 64 * VEC;  // channels per workgroup
-  const int64_t nwg = (int64_t)K * nchunks;
-  const int64_t lb = xcd_remap(blockIdx.x, nwg);
-  const int n = (int)(lb / nchunks);
-  const int chunk = (int)(lb % nchunks);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Per-wave sample tables in registers: entry q of the y (x) table lives in
+// lane q % 64, slot q / 64 (<= 2 slots: PH*gh, PW*gw <= 128).  Lookups in the
+// bin loop are readlanes with a wave-uniform index, so the per-sample weights
+// and tap offsets are scalar values and the loop issues LDS/VMEM traffic only
+// for the taps themselves.
+struct RegTab {
+  int lo[2], hi[2], valid[2];
+  float l[2], h[2];
+};
 
-  const float* r = rois + (int64_t)n * 5;
-  const int b = (int)r[0];
-  const float off = aligned ? 0.5f : 0.0f;
-  const float sw = r[1] * spatial_scale - off;
-  const float sh = r[2] * spatial_scale - off;
-  const float ew = r[3] * spatial_scale - off;
-  const float eh = r[4] * spatial_scale - off;
-  float rw = ew - sw, rh = eh - sh;
-  if (!aligned) {
-    rw = fmaxf(rw, 1.f);
-    rh = fmaxf(rh, 1.f);
+__device__ __forceinline__ void tab_put(RegTab& t, int slot, const AxisTab& a) {
+  t.lo[slot] = a.lo; t.hi[slot] = a.hi; t.valid[slot] = a.valid; t.l[slot] = a.l; t.h[slot] = a.h;
+}
+
+__device__ __forceinline__ AxisTab tab_get(const RegTab& t, int q) {
+  const int ln = q & 63, sl = q >> 6;
+  AxisTab a;
+  if (sl == 0) {
+    a.lo = __builtin_amdgcn_readlane(t.lo[0], ln);
+    a.hi = __builtin_amdgcn_readlane(t.hi[0], ln);
+    a.valid = __builtin_amdgcn_readlane(t.valid[0], ln);
+    a.l = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.l[0]), ln));
+    a.h = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.h[0]), ln));
+  } else {
+    a.lo = __builtin_amdgcn_readlane(t.lo[1], ln);
+    a.hi = __builtin_amdgcn_readlane(t.hi[1], ln);
+    a.valid = __builtin_amdgcn_readlane(t.valid[1], ln);
+    a.l = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.l[1]), ln));
+    a.h = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t.h[1]), ln));
   }
-  const float bh = rh / (float)PH, bw = rw / (float)PW;
-  const int gh = sampling_ratio > 0 ? sampling_ratio : (int)ceilf(rh / (float)PH);
-  const int gw = sampling_ratio > 0 ? sampling_ratio : (int)ceilf(rw / (float)PW);
-  const float count = (float)max(gh * gw, 1);
+  return a;
+}
 
-  // sample tables (LDS): y then x
-  AxisTab* ytab = reinterpret_cast<AxisTab*>(smem);
-  AxisTab* xtab = ytab + PH * gh;
-  float* otile = reinterpret_cast<float*>(xtab + PW * gw);  // NCHW staging
-  for (int q = threadIdx.x; q < PH * gh + PW * gw; q += blockDim.x) {
-    if (q < PH * gh) {
-      int ph = q / gh, iy = q % gh;
-      float t0 = sh + (float)ph * bh;
-      float yy = t0 + ((float)iy + .5f) * bh / (float)gh;
-      ytab[q] = axis_sample(yy, H);
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = min(x, __shfl_xor(x, o));
+  return x;
+}
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o));
+  return x;
+}
+
+// tap source: the NHWC map in global memory (pixel (y,x) at (y*W+x)*C), or
+// the ROI's source window staged in LDS (cell (y-y0, x-x0) at ((y-y0)*wx +
+// (x-x0))*CPW).  `zero` is pixel (0,0), what torchvision reads for an empty
+// sample (weights 0 at position 0 -- kept so NaN/inf propagate identically).
+struct TapSrc {
+  const float* base;
+  const float* zero;
+  int rstride, cstride, y0, x0;
+};
+
+template <int VEC, bool OUT_BF16, bool OUT_NHWC>
+__device__ __forceinline__ void store_bin(void* out, float* otile, int lds_stride, int n, int bin,
+                                          int nbins, int C, int c, int lane, const float (&v)[VEC]) {
+  if (OUT_NHWC) {
+    const int64_t o = ((int64_t)n * nbins + bin) * C + c;
+    if (OUT_BF16) {
+      uint16_t* po = reinterpret_cast<uint16_t*>(out) + o;
+      if constexpr (VEC == 4) {
+        *reinterpret_cast<uint2*>(po) = make_uint2(
+            (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16),
+            (uint32_t)trk::f32_to_bf16(v[2]) | ((uint32_t)trk::f32_to_bf16(v[3]) << 16));
+      } else if constexpr (VEC == 2) {
+        *reinterpret_cast<uint32_t*>(po) =
+            (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16);
+      } else {
+        po[0] = trk::f32_to_bf16(v[0]);
+      }
     } else {
-      int q2 = q - PH * gh;
-      int pw = q2 / gw, ix = q2 % gw;
-      float s0 = sw + (float)pw * bw;
-      float xx = s0 + ((float)ix + .5f) * bw / (float)gw;
-      xtab[q2] = axis_sample(xx, W);
+      float* po = reinterpret_cast<float*>(out) + o;
+      if constexpr (VEC == 4) {
+        *reinterpret_cast<float4*>(po) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (VEC == 2) {
+        *reinterpret_cast<float2*>(po) = make_float2(v[0], v[1]);
+      } else {
+        po[0] = v[0];
+      }
+    }
+  } else if (lds_stride > 0) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) otile[(lane * VEC + k) * lds_stride + bin] = v[k];
+  } else {  // NCHW without staging (large PH*PW): strided scalar stores
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const int64_t o = ((int64_t)n * C + c + k) * nbins + bin;
+      if (OUT_BF16) reinterpret_cast<uint16_t*>(out)[o] = trk::f32_to_bf16(v[k]);
+      else reinterpret_cast<float*>(out)[o] = v[k];
     }
   }
-  __syncthreads();
+}
 
-  const int c = chunk * CPW + lane * VEC;
-  const bool active = c < C;
-  const float* img = in + (int64_t)b * H * W * C + (active ? c : 0);
+// all bins of one (ROI, channel chunk) for one wave; exact torchvision order:
+// per sample t = w1*f1; t += w2*f2; t += w3*f3; t += w4*f4; v += t; v /= count
+template <int VEC, bool OUT_BF16, bool OUT_NHWC, int SR>
+__device__ __forceinline__ void bins_loop(const TapSrc& src, const RegTab& yt, const RegTab& xt,
+                                          int PH, int PW, int gh_rt, int gw_rt, float count, bool active,
+                                          void* out, float* otile, int lds_stride, int n, int C,
+                                          int c, int lane, int wave) {
+  // SR > 0: compile-time sampling ratio -> the sample loops unroll and all
+  // 4*SR*SR taps of a bin are in flight before the first use
+  const int gh = SR > 0 ? SR : gh_rt, gw = SR > 0 ? SR : gw_rt;
   const int nbins = PH * PW;
   for (int bin = wave; bin < nbins; bin += 4) {
     const int ph = bin / PW, pw = bin % PW;
     float v[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) v[k] = 0.f;
+#pragma unroll(SR > 0 ? SR : 1)
     for (int iy = 0; iy < gh; ++iy) {
-      const AxisTab ty = ytab[ph * gh + iy];
+      const AxisTab ty = tab_get(yt, ph * gh + iy);
+#pragma unroll(SR > 0 ? SR : 1)
       for (int ix = 0; ix < gw; ++ix) {
-        const AxisTab tx = xtab[pw * gw + ix];
+        const AxisTab tx = tab_get(xt, pw * gw + ix);
         float w1, w2, w3, w4;
-        int p1, p2, p3, p4;
+        const float *p1, *p2, *p3, *p4;
         if (ty.valid && tx.valid) {
           w1 = ty.h * tx.h; w2 = ty.h * tx.l; w3 = ty.l * tx.h; w4 = ty.l * tx.l;
-          p1 = ty.lo * W + tx.lo; p2 = ty.lo * W + tx.hi;
-          p3 = ty.hi * W + tx.lo; p4 = ty.hi * W + tx.hi;
-        } else {  // torchvision's empty PreCalc: weights 0 at position 0
+          const float* r0 = src.base + (ty.lo - src.y0) * src.rstride;
+          const float* r1 = src.base + (ty.hi - src.y0) * src.rstride;
+          const int c0 = (tx.lo - src.x0) * src.cstride, c1 = (tx.hi - src.x0) * src.cstride;
+          p1 = r0 + c0; p2 = r0 + c1; p3 = r1 + c0; p4 = r1 + c1;
+        } else {
           w1 = w2 = w3 = w4 = 0.f;
-          p1 = p2 = p3 = p4 = 0;
+          p1 = p2 = p3 = p4 = src.zero;
         }
         float f1[VEC], f2[VEC], f3[VEC], f4[VEC];
-        load_vec<VEC>(img + (int64_t)p1 * C, f1);
-        load_vec<VEC>(img + (int64_t)p2 * C, f2);
-        load_vec<VEC>(img + (int64_t)p3 * C, f3);
-        load_vec<VEC>(img + (int64_t)p4 * C, f4);
+        load_vec<VEC>(p1, f1);
+        load_vec<VEC>(p2, f2);
+        load_vec<VEC>(p3, f3);
+        load_vec<VEC>(p4, f4);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
           float t = w1 * f1[k];
@@ -190,39 +243,154 @@ roi_align_nhwc_kernel(const float* __restrict__ in,  // [B,H,W,C]
     }
 #pragma unroll
     for (int k = 0; k < VEC; ++k) v[k] = v[k] / count;
-    if (!active) continue;
-    if (OUT_NHWC) {
-      const int64_t o = ((int64_t)n * nbins + bin) * C + c;
-      if (OUT_BF16) {
-        uint16_t* po = reinterpret_cast<uint16_t*>(out) + o;
+    if (active) store_bin<VEC, OUT_BF16, OUT_NHWC>(out, otile, lds_stride, n, bin, nbins, C, c, lane, v);
+  }
+}
+
+template <int VEC, bool OUT_BF16, bool OUT_NHWC>
+__global__ void __launch_bounds__(256)
+roi_align_nhwc_kernel(const float* __restrict__ in,  // [B,H,W,C]
+                      int B, int C, int H, int W,
+                      const float* __restrict__ rois, int K, float spatial_scale,
+                      int PH, int PW, int sampling_ratio, int aligned,
+                      void* __restrict__ out, int nchunks, int lds_stride, int win_cells) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int CPW = 64 * VEC;  // channels per workgroup
+  const int64_t nwg = (int64_t)K * nchunks;
+  const int64_t lb = xcd_remap(blockIdx.x, nwg);
+  const int n = (int)(lb / nchunks);
+  const int chunk = (int)(lb % nchunks);
+  // wave index and everything derived from the ROI are wave-uniform; say so
+  // (readfirstlane) so the bin loop, the table lookups and the staged/direct
+  // branch compile to scalar control flow instead of exec-masked branches
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const float* r = rois + (int64_t)n * 5;
+  const int b = __builtin_amdgcn_readfirstlane((int)r[0]);
+  const float off = aligned ? 0.5f : 0.0f;
+  const float sw = r[1] * spatial_scale - off;
+  const float sh = r[2] * spatial_scale - off;
+  const float ew = r[3] * spatial_scale - off;
+  const float eh = r[4] * spatial_scale - off;
+  float rw = ew - sw, rh = eh - sh;
+  if (!aligned) {
+    rw = fmaxf(rw, 1.f);
+    rh = fmaxf(rh, 1.f);
+  }
+  const float bh = rh / (float)PH, bw = rw / (float)PW;
+  const int gh = sampling_ratio, gw = sampling_ratio;  // > 0 (checked on the host)
+  const float count = (float)max(gh * gw, 1);
+
+  // ---- sample tables, per wave, in registers (pre_calc restated)
+  const int ny = PH * gh, nx = PW * gw;
+  RegTab yt, xt;
+  int ylo = H, yhi = -1, xlo = W, xhi = -1;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) po[k] = trk::f32_to_bf16(v[k]);
-      } else {
-        float* po = reinterpret_cast<float*>(out) + o;
-        if constexpr (VEC == 4) {
-          *reinterpret_cast<float4*>(po) = make_float4(v[0], v[1], v[2], v[3]);
+  for (int sl = 0; sl < 2; ++sl) {
+    const int q = lane + 64 * sl;
+    AxisTab a;
+    a.lo = a.hi = a.valid = 0; a.l = a.h = 0.f;
+    if (q < ny) {
+      const int ph = q / gh, iy = q % gh;
+      const float t0 = sh + (float)ph * bh;
+      a = axis_sample(t0 + ((float)iy + .5f) * bh / (float)gh, H);
+      if (a.valid) { ylo = min(ylo, a.lo); yhi = max(yhi, a.hi); }
+    }
+    tab_put(yt, sl, a);
+    a.lo = a.hi = a.valid = 0; a.l = a.h = 0.f;
+    if (q < nx) {
+      const int pw = q / gw, ix = q % gw;
+      const float s0 = sw + (float)pw * bw;
+      a = axis_sample(s0 + ((float)ix + .5f) * bw / (float)gw, W);
+      if (a.valid) { xlo = min(xlo, a.lo); xhi = max(xhi, a.hi); }
+    }
+    tab_put(xt, sl, a);
+  }
+  // source window of the valid samples (identical in every wave)
+  const int y0 = __builtin_amdgcn_readfirstlane(wave_min(ylo));
+  const int y1 = __builtin_amdgcn_readfirstlane(wave_max(yhi));
+  const int x0 = __builtin_amdgcn_readfirstlane(wave_min(xlo));
+  const int x1 = __builtin_amdgcn_readfirstlane(wave_max(xhi));
+  const int wy = max(y1 - y0 + 1, 0), wx = max(x1 - x0 + 1, 0);
+  const bool staged = win_cells > 0 && wy * wx <= win_cells;
+
+  // LDS: [NCHW output tile?][window: win_cells x CPW][pixel (0,0)]
+  float* otile = reinterpret_cast<float*>(smem);
+  float* win = otile + (OUT_NHWC || lds_stride == 0 ? 0 : (size_t)CPW * lds_stride);
+  float* zcell = win + (size_t)win_cells * CPW;
+
+  const int cbase = chunk * CPW;
+  const int c = cbase + lane * VEC;
+  const bool active = c < C;
+  const float* img = in + (int64_t)b * H * W * C;
+  TapSrc src;
+  if (staged) {
+    // whole 16-B pieces of each cell's CPW channels; the tail chunk (C not a
+    // multiple of CPW) loads only channels < C
+    constexpr int PPC = CPW / 4;  // float4 pieces per cell
+    constexpr int BATCH = 8;      // pieces in flight per thread (no load->store chain)
+    const int ncell = wy * wx;
+    const int total = (ncell + 1) * PPC;
+    for (int q0 = threadIdx.x; q0 < total; q0 += 256 * BATCH) {
+      float4 tmp[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int q = min(q0 + 256 * k, total - 1);  // clamp: no data-dependent break
+        const int cell = q / PPC, pc = (q % PPC) * 4;
+        const int yy = cell < ncell ? y0 + cell / wx : 0, xx = cell < ncell ? x0 + cell % wx : 0;
+        const float* sp = img + ((int64_t)yy * W + xx) * C + cbase + pc;
+        if ((C & 3) == 0 && cbase + pc + 4 <= C) {
+          tmp[k] = *reinterpret_cast<const float4*>(sp);
         } else {
-#pragma unroll
-          for (int k = 0; k < VEC; ++k) po[k] = v[k];
+          tmp[k].x = cbase + pc + 0 < C ? sp[0] : 0.f;
+          tmp[k].y = cbase + pc + 1 < C ? sp[1] : 0.f;
+          tmp[k].z = cbase + pc + 2 < C ? sp[2] : 0.f;
+          tmp[k].w = cbase + pc + 3 < C ? sp[3] : 0.f;
         }
       }
-    } else if (lds_stride > 0) {
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) otile[(lane * VEC + k) * lds_stride + bin] = v[k];
-    } else {  // NCHW without staging (large PH*PW): strided scalar stores
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        const int64_t o = ((int64_t)n * C + c + k) * nbins + bin;
-        if (OUT_BF16) reinterpret_cast<uint16_t*>(out)[o] = trk::f32_to_bf16(v[k]);
-        else reinterpret_cast<float*>(out)[o] = v[k];
+      for (int k = 0; k < BATCH; ++k) {
+        const int q = q0 + 256 * k;
+        if (q >= total) continue;
+        const int cell = q / PPC, pc = (q % PPC) * 4;
+        float* dst = cell < ncell ? win + (size_t)cell * CPW + pc : zcell + pc;
+        *reinterpret_cast<float4*>(dst) = tmp[k];
       }
     }
+    __syncthreads();
+    src.base = win + lane * VEC;
+    src.zero = zcell + lane * VEC;
+    src.rstride = wx * CPW;
+    src.cstride = CPW;
+    src.y0 = y0;
+    src.x0 = x0;
+    if (sampling_ratio == 2)
+      bins_loop<VEC, OUT_BF16, OUT_NHWC, 2>(src, yt, xt, PH, PW, gh, gw, count, active, out, otile,
+                                            lds_stride, n, C, c, lane, wave);
+    else
+      bins_loop<VEC, OUT_BF16, OUT_NHWC, 0>(src, yt, xt, PH, PW, gh, gw, count, active, out, otile,
+                                            lds_stride, n, C, c, lane, wave);
+  } else {
+    const int cc = active ? c : 0;
+    src.base = img + cc;
+    src.zero = img + cc;
+    src.rstride = W * C;
+    src.cstride = C;
+    src.y0 = 0;
+    src.x0 = 0;
+    if (sampling_ratio == 2)
+      bins_loop<VEC, OUT_BF16, OUT_NHWC, 2>(src, yt, xt, PH, PW, gh, gw, count, active, out, otile,
+                                            lds_stride, n, C, c, lane, wave);
+    else
+      bins_loop<VEC, OUT_BF16, OUT_NHWC, 0>(src, yt, xt, PH, PW, gh, gw, count, active, out, otile,
+                                            lds_stride, n, C, c, lane, wave);
   }
   if (!OUT_NHWC && lds_stride > 0) {
     __syncthreads();
     // out[n][chunk*CPW .. +nch][0..nbins) is one contiguous range
-    const int nch = min(CPW, C - chunk * CPW);
-    const int64_t base = ((int64_t)n * C + (int64_t)chunk * CPW) * nbins;
+    const int nbins = PH * PW;
+    const int nch = min(CPW, C - cbase);
+    const int64_t base = ((int64_t)n * C + (int64_t)cbase) * nbins;
     const int total = nch * nbins;
     for (int e = threadIdx.x; e < total; e += blockDim.x) {
       const float val = otile[(e / nbins) * lds_stride + (e % nbins)];
@@ -232,26 +400,32 @@ roi_align_nhwc_kernel(const float* __restrict__ in,  // [B,H,W,C]
   }
 }
 
+// tuning knobs (trk_set_tuning): LDS window budget per workgroup, channels per lane
+int g_roi_window_kb = 64;
+int g_roi_vec = 0;  // 0 = auto
+
 template <int VEC, bool OUT_BF16, bool OUT_NHWC>
 int launch_roi(const float* nhwc, int B, int C, int H, int W, const float* rois, int K,
-               float scale, int PH, int PW, int sr, int aligned, void* out, int gh, int gw,
-               hipStream_t st) {
+               float scale, int PH, int PW, int sr, int aligned, void* out, hipStream_t st) {
   constexpr int CPW = 64 * VEC;
   const int nchunks = (C + CPW - 1) / CPW;
-  size_t tab = sizeof(AxisTab) * (size_t)(PH * gh + PW * gw);
-  tab = (tab + 15) & ~size_t(15);
   int lds_stride = 0;
-  size_t lds = tab;
+  size_t lds = 0;
   if (!OUT_NHWC) {
     const int stride = PH * PW + 1;  // +1: bank-conflict padding
-    const size_t need = tab + sizeof(float) * (size_t)CPW * stride;
-    if (need <= 96 * 1024) {
+    const size_t need = sizeof(float) * (size_t)CPW * stride;
+    if (need <= 64 * 1024) {
       lds_stride = stride;
       lds = need;
     }
   }
+  const size_t cell_bytes = sizeof(float) * CPW;
+  const size_t budget = (size_t)g_roi_window_kb * 1024;
+  int win_cells = lds + 2 * cell_bytes <= budget ? (int)((budget - lds) / cell_bytes) - 1 : 0;
+  win_cells = std::min(win_cells, H * W);
+  if (win_cells > 0) lds += cell_bytes * (size_t)(win_cells + 1);
   if (lds > 160 * 1024) {
-    trk::set_error("roi_align: sample tables too large (PH*gh + PW*gw = %d)", PH * gh + PW * gw);
+    trk::set_error("roi_align: LDS request %zu too large", lds);
     return TRK_EUNSUPPORTED;
   }
   const int64_t nwg = (int64_t)K * nchunks;
@@ -260,30 +434,38 @@ int launch_roi(const float* nhwc, int B, int C, int H, int W, const float* rois,
     return TRK_EUNSUPPORTED;
   }
   static bool attr_set = false;
-  if (!attr_set) {  // allow > 64 KiB dynamic LDS for the NCHW staging tile
+  if (!attr_set) {  // allow > 64 KiB dynamic LDS
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(roi_align_nhwc_kernel<VEC, OUT_BF16, OUT_NHWC>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL((roi_align_nhwc_kernel<VEC, OUT_BF16, OUT_NHWC>), dim3((unsigned)nwg), dim3(256),
                      lds, st, nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, nchunks,
-                     lds_stride);
+                     lds_stride, win_cells);
   return trk::check_launch("roi_align_nhwc_kernel");
 }
 
 template <bool OUT_BF16, bool OUT_NHWC>
 int dispatch_vec(int C, const float* nhwc, int B, int H, int W, const float* rois, int K, float scale,
-                 int PH, int PW, int sr, int aligned, void* out, int gh, int gw, hipStream_t st) {
-  // NHWC output: 4 channels per lane (16-B loads, 1 KiB per wave-instruction).
-  // NCHW output: 2 channels per lane keeps the [128][PH*PW+1] staging tile small.
-  if (OUT_NHWC && C % 4 == 0)
-    return launch_roi<4, OUT_BF16, OUT_NHWC>(nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, gh, gw, st);
-  if (C % 2 == 0)
-    return launch_roi<2, OUT_BF16, OUT_NHWC>(nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, gh, gw, st);
-  return launch_roi<1, OUT_BF16, OUT_NHWC>(nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, gh, gw, st);
+                 int PH, int PW, int sr, int aligned, void* out, hipStream_t st) {
+  int vec = g_roi_vec;
+  if (vec == 0) vec = 2;  // 128-channel chunks: 8-B conflict-free LDS tap reads, 128-cell window
+  if (vec == 4 && C % 4 == 0)
+    return launch_roi<4, OUT_BF16, OUT_NHWC>(nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, st);
+  if (vec >= 2 && C % 2 == 0)
+    return launch_roi<2, OUT_BF16, OUT_NHWC>(nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, st);
+  return launch_roi<1, OUT_BF16, OUT_NHWC>(nhwc, B, C, H, W, rois, K, scale, PH, PW, sr, aligned, out, st);
 }
 
 }  // namespace
+
+extern "C" int trk_set_tuning(const char* key, int value) {
+  TRK_REQUIRE(key, "set_tuning: null key");
+  if (!strcmp(key, "roi_window_kb")) { TRK_REQUIRE(value >= 0 && value <= 150, "roi_window_kb in [0,150]"); g_roi_window_kb = value; return TRK_OK; }
+  if (!strcmp(key, "roi_vec")) { TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "roi_vec in {0,1,2,4}"); g_roi_vec = value; return TRK_OK; }
+  trk::set_error("set_tuning: unknown key '%s'", key);
+  return TRK_EINVAL;
+}
 
 extern "C" size_t trk_roi_align_workspace_bytes(int64_t B, int64_t C, int64_t H, int64_t W, int in_layout) {
   if (in_layout == TRK_NHWC) return 0;
@@ -321,13 +503,14 @@ extern "C" int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64
   // gh/gw for adaptive sampling depend on each ROI; size the LDS tables for the
   // largest ROI on the host only when sampling_ratio <= 0 (not used by the
   // reference, which always passes 2).
-  int gh = sampling_ratio, gw = sampling_ratio;
   TRK_REQUIRE(sampling_ratio > 0,
               "roi_align: adaptive sampling (sampling_ratio <= 0) is not implemented; the reference uses 2");
+  TRK_REQUIRE(PH * sampling_ratio <= 128 && PW * sampling_ratio <= 128,
+              "roi_align: output_size x sampling_ratio must be <= 128 per axis");
   const int iB = (int)B, iC = (int)C, iH = (int)H, iW = (int)W, iK = (int)K;
   const bool bf = out_dtype == TRK_BF16, nhwc_out = out_layout == TRK_NHWC;
-  if (bf && nhwc_out) return dispatch_vec<true, true>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, gh, gw, st);
-  if (bf && !nhwc_out) return dispatch_vec<true, false>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, gh, gw, st);
-  if (!bf && nhwc_out) return dispatch_vec<false, true>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, gh, gw, st);
-  return dispatch_vec<false, false>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, gh, gw, st);
+  if (bf && nhwc_out) return dispatch_vec<true, true>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);
+  if (bf && !nhwc_out) return dispatch_vec<true, false>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);
+  if (!bf && nhwc_out) return dispatch_vec<false, true>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);
+  return dispatch_vec<false, false>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);
 }

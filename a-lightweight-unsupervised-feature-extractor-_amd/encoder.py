@@ -111,8 +111,9 @@ class Model(nn.Module):
             dr, dn = r.dsc_reinforce, r.dsc_normal
             w1 = torch.cat([m[0].weight.flatten(1) for m in (dr.depth, dr.point, dn.depth, dn.point)], 0)
             w["w1t"] = w1.t().contiguous().to(device, dtype)                              # [C, 4h]
-            w["dw"] = torch.cat([m[1].weight for m in (dr.depth, dr.point, dn.depth, dn.point)],
-                                0).to(device, dtype).contiguous(memory_format=torch.channels_last)
+            dw = torch.cat([m[1].weight for m in (dr.depth, dr.point, dn.depth, dn.point)], 0)
+            w["dw"] = dw.to(device, dtype).contiguous(memory_format=torch.channels_last)  # host path
+            w["dw_t"] = dw.reshape(dw.shape[0], 25).t().contiguous().to(device, torch.float32)  # [25, 4h]
             for tag, dsc in (("r", dr), ("n", dn)):
                 bn = dsc.bn
                 scale = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
@@ -163,7 +164,7 @@ class Model(nn.Module):
         ss = S1 * S2
         X = x.permute(0, 2, 3, 1).reshape(N * ss, C)                 # view when channels_last
         Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)                      # 4 first 1x1 convs, one GEMM
-        Y2 = dwconv5_nhwc(Y1, W["dw"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
+        Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
         xr = torch.addmm(W["br"], Y2[:, :h2], W["w2r"]).view(N, ss, C)   # DSC reinforce (BN folded)
         xn = torch.addmm(W["bn"], Y2[:, h2:], W["w2n"]).view(N, ss, C)   # DSC normal (BN folded)
         m_r = act_mean(xr, "silu")                                   # SiLU + SE squeeze

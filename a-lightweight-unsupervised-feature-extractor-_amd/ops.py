@@ -46,11 +46,15 @@ def _edt(t: torch.Tensor) -> int:
 
 def dwconv5_nhwc(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Depthwise 5x5 / pad 2 on NHWC storage x [N, H, W, C]; weight [C, 1, 5, 5]
-    (card.DSC depth.1/point.1).  Returns [N, H, W, C] in x.dtype."""
+    or already tap-major [25, C] f32 (card.DSC depth.1/point.1).  Returns
+    [N, H, W, C] in x.dtype."""
     _need_gpu(x, "dwconv5_nhwc")
     N, H, W, C = x.shape
     x = x.contiguous()
-    w = weight.reshape(C, 25).to(torch.float32).contiguous()
+    if weight.dim() == 2 and weight.shape == (25, C) and weight.dtype == torch.float32:
+        w = weight.contiguous()
+    else:
+        w = weight.reshape(C, 25).to(torch.float32).t().contiguous()
     out = torch.empty_like(x)
     check(lib().trk_dwconv5_nhwc(_ptr(x), _ptr(w), _ptr(out), N, H, W, C, _edt(x), _stream(x.device)),
           "dwconv5_nhwc")

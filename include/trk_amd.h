@@ -38,6 +38,10 @@ enum { TRK_NCHW = 0, TRK_NHWC = 1 };
 
 int trk_abi_version(void);
 const char* trk_last_error(void);
+/* Performance knobs (process-global; results are bit-identical for every value):
+ *   "roi_window_kb"  LDS budget (KiB) for staging a ROI's source window; 0 = never stage
+ *   "roi_vec"        channels per lane in roi_align (0 = auto, 1, 2, 4)            */
+int trk_set_tuning(const char* key, int value);
 
 /* ------------------------------------------------------------------------
  * ROI Align forward.  Replaces torchvision.ops.roi_align as called by
@@ -137,7 +141,7 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
  * Activations are NHWC rows [N, P = S*S, C], dtype TRK_F32 or TRK_BF16.
  * ---------------------------------------------------------------------- */
 /* depthwise 5x5, stride 1, zero pad 2 (card.py:28-29,38-39 DSC depth.1/point.1):
- * in/out [N,H,W,C] (must not alias), weight [C][25] f32.  W <= 32. */
+ * in/out [N,H,W,C] (must not alias), weight tap-major [25][C] f32.  W <= 32. */
 int trk_dwconv5_nhwc(const void* in, const float* weight, void* out, int64_t N, int64_t H,
                      int64_t W, int64_t C, int dtype, void* stream);
 /* y = act(x) (act 0 none, 1 SiLU, 2 Hardswish), written to out (may equal x,
