@@ -8,7 +8,7 @@ Feature-Extractor- (reference tracking.py:193-329, model/mainTracking.py):
   cal_cost / bbox_cost / conf_cost         costCard (HIP fused cost)
   hungarian_assign / linear_sum_assignment hung.py / scipy LSAP (HIP SAP)
   Tracking                                 mainTracking.Tracking
-  StreamBatchTracker                       device-resident multi-stream tracker
+  MultiStreamTracker                       device-resident multi-stream tracker
 
 Import with importlib (the directory name is not an identifier):
     trk = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd")
@@ -19,8 +19,10 @@ from .ops import (roi_align, roi_align_from_input_boxes, build_cost, cost_combin
 from .hung import hungarian_assign
 from .costcard import cal_cost, bbox_cost, conf_cost
 from .encoder import Model
+from .tracking import Tracking, MultiStreamTracker, TrackTable, tracker_conf, load_conf
 
 __all__ = ["TrkError", "lib", "header_symbols", "roi_align", "roi_align_from_input_boxes",
            "build_cost", "cost_combine", "lsap_batched", "linear_sum_assignment",
            "default_cost_params", "CostParams", "hungarian_assign", "cal_cost", "bbox_cost",
-           "conf_cost", "Model"]
+           "conf_cost", "Model", "Tracking", "MultiStreamTracker", "TrackTable", "tracker_conf",
+           "load_conf"]

@@ -1,26 +1,30 @@
 """Benchmark: ROIs/s for roi_align -> embed -> cost -> assign, N=256 per frame.
 
 Workload (BASELINE.json configs[2]): each GPU runs
-8 independent synthetic video streams; one step = one frame of every stream:
-  [8,512,40,40] fp32 SPP-CSPC maps (SiLU(randn)) + 256 boxes per frame
-  -> trk roi_align (HIP, NCHW f32 in, NHWC bf16 out, 10x10 bins)
-  -> encoder (PyTorch-ROCm, bf16)           -> 128-D unit embeddings
-  -> fused cost (HIP, f32 MFMA, top-5 of a 30-deep memory bank, bbox, conf,
-     Mahalanobis gate) for 256 tracks x 256 dets per stream
-  -> scipy-exact LSAP (HIP, one wavefront per stream) + hung.py cost gate
-  -> assignment indices copied to the host (the timed region ends there).
-Inputs are resident in HBM before timing starts.  Multi-GPU: one process per
-GPU (torchrun), each with its own 8 streams, no data-path collective; one
-barrier + MAX(elapsed) all-reduce per report ("scaling": "weak").
+8 independent synthetic video streams of 256 moving objects; one step = one
+frame of every stream, the full per-frame tracker hot path:
+  [8,512,40,40] fp32 SPP-CSPC maps (SiLU(randn), resident) + 256 boxes/frame
+  -> trk roi_align      (HIP: NCHW f32 in, NHWC bf16 out, 10x10 bins)
+  -> encoder            (PyTorch-ROCm GEMMs + HIP depthwise/act kernels, bf16)
+  -> MultiStreamTracker.step:
+       KF predict + gate inputs (HIP) -> fused cost: top-5 of a 30-deep memory
+       bank (f32 MFMA), bbox, conf, Mahalanobis gate (HIP) -> scipy-exact LSAP +
+       cost gate (HIP) -> assignment indices to the host -> KF update / EMA /
+       bank push (HIP), births, purge.
+Boxes move at constant velocity (bouncing), detections arrive shuffled; a
+30-frame pre-roll fills the memory banks before warm-up.  All inputs are in
+HBM before timing starts.  Multi-GPU: one process per GPU (torchrun), each
+with its own 8 streams, no data-path collective; one barrier + MAX(elapsed)
+all-reduce per report ("scaling": "weak").
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import importlib
 import json
-import math
 import os
 import sys
 import time
@@ -31,11 +35,13 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 trk = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd")
+ops = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (spec)
-F32_MFMA_PEAK_TFLOPS = 157.3   # f32-input MFMA
+F32_MFMA_PEAK_TFLOPS = 157.3   # f32-input MFMA (= f32 vector peak)
 ENC_FLOP_PER_ROI = {10: 320.61e6, 7: 157.57e6}   # BASELINE.md §4 (FlopCounterMode)
+PREROLL = 30
 
 
 # ------------------------------------------------------------ workload ----
@@ -43,135 +49,169 @@ def silu(x):
     return x / (1 + np.exp(-x))
 
 
-def make_workload(dev, streams=8, N=256, M=256, T=30, C=512, H=40, seed=0):
-    """Synthetic per-stream state after a 30-frame warm-up: full banks (T=30),
-    KF-predicted boxes near the current detections (gates not binding for the
-    true pairs), detections in shuffled order."""
+def make_scenes(dev, streams, N, frames, seed, C=512, H=40):
+    """Per stream: N objects with w, h ~ U(32, 320) px in a 1280x1280
+    letterboxed frame (rows 280..1000 = a 1080p picture), velocities
+    U(-2, 2) px/frame bouncing at the borders, 0.5 px detection jitter,
+    conf ~ U(0.55, 0.99); detection order shuffled every frame."""
     rng = np.random.default_rng(seed)
     feat = silu(rng.standard_normal((streams, C, H, H)).astype(np.float32)).astype(np.float32)
-    img, pad = 1280, 280
-    w = rng.uniform(32, 320, (streams, M)); h = rng.uniform(32, 320, (streams, M))
-    x1 = rng.uniform(-8, img - w + 8); y1 = rng.uniform(pad - 8, img - pad - h + 8)
-    pbox = np.stack([x1, y1, x1 + w, y1 + h], -1).astype(np.float32)
-    base = rng.standard_normal((streams, M, 128)).astype(np.float32)
-    base /= np.linalg.norm(base, axis=-1, keepdims=True)
-    bank = base[:, :, None, :] + 0.05 * rng.standard_normal((streams, M, T, 128)).astype(np.float32)
-    bank /= np.linalg.norm(bank, axis=-1, keepdims=True)
-    perm = np.stack([rng.permutation(M)[:N] for _ in range(streams)])
-    dbox = np.take_along_axis(pbox, perm[..., None], 1) + rng.normal(0, 1.5, (streams, N, 4)).astype(np.float32)
-    rois = np.concatenate([np.repeat(np.arange(streams), N)[:, None].astype(np.float32),
-                           dbox.reshape(-1, 4)], 1).astype(np.float32)
-    lconf = rng.uniform(0.55, 0.99, (streams, M)).astype(np.float32)
-    dconf = rng.uniform(0.55, 0.99, (streams, N)).astype(np.float32)
-    zx = np.stack([(pbox[..., 0] + pbox[..., 2]) / 2, (pbox[..., 1] + pbox[..., 3]) / 2,
-                   (pbox[..., 2] - pbox[..., 0]) / (pbox[..., 3] - pbox[..., 1]), pbox[..., 3] - pbox[..., 1]], -1)
-    P = np.array([10.0, 10.0, 0.01, 10.0])  # KF position covariance (H P H^T diag)
-    gsinv = np.zeros((streams, M, 4, 4))
-    gsinv[..., np.arange(4), np.arange(4)] = 1.0 / (P + 1.0 + 1e-9)
-    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
-    return dict(feat=t(feat), rois=t(rois), bank=t(bank.reshape(streams * M, T, 128)),
-                bank_len=t(np.full(streams * M, T, np.int32), torch.int32), pbox=t(pbox.reshape(-1, 4)),
-                conf_prev=t(lconf.reshape(-1)), gmean=t(zx.reshape(-1, 4), torch.float64),
-                gsinv=t(gsinv.reshape(-1, 16), torch.float64),
-                gate_on=t(np.ones(streams * M, np.int32), torch.int32), dbox=t(dbox), conf_cur=t(dconf),
-                perm=perm, streams=streams, N=N, M=M, T=T, np=dict(feat=feat, rois=rois, bank=bank,
-                pbox=pbox, lconf=lconf, dconf=dconf, dbox=dbox, gm=zx, gsinv=gsinv))
+    w = rng.uniform(32, 320, (streams, N)); h = rng.uniform(32, 320, (streams, N))
+    lo = np.stack([np.zeros_like(w), np.full_like(h, 280.0)], -1)
+    hi = np.stack([1280 - w, 1000 - h], -1)
+    p = lo + rng.random((streams, N, 2)) * (hi - lo)
+    v = rng.uniform(-2, 2, (streams, N, 2))
+    conf = rng.uniform(0.55, 0.99, (streams, N))
+    rois = np.zeros((frames, streams * N, 5), np.float32)
+    dbox = np.zeros((frames, streams, N, 4), np.float32)
+    dconf = np.zeros((frames, streams, N), np.float32)
+    obj = np.zeros((frames, streams, N), np.int64)
+    for f in range(frames):
+        for s in range(streams):
+            perm = rng.permutation(N)
+            obj[f, s] = perm
+            q = p[s, perm] + rng.normal(0, 0.5, (N, 2))
+            b = np.concatenate([q, q + np.stack([w[s, perm], h[s, perm]], -1)], -1)
+            dbox[f, s] = b
+            dconf[f, s] = np.clip(conf[s, perm] + rng.normal(0, 0.01, N), 0.5, 0.999)
+            rois[f, s * N:(s + 1) * N, 0] = s
+            rois[f, s * N:(s + 1) * N, 1:] = b
+        p = p + v
+        bounce = (p < lo) | (p > hi)
+        v[bounce] *= -1
+        p = np.clip(p, lo, hi)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return dict(feat=t(feat), rois=t(rois), dbox=t(dbox), dconf=t(dconf), confs_host=dconf,
+                obj=obj, streams=streams, N=N, np=dict(feat=feat, rois=rois, dbox=dbox, dconf=dconf))
 
 
 class Pipeline:
-    """One step of the per-frame hot path over a batch of streams."""
+    """The per-frame hot path over a batch of streams."""
 
-    def __init__(self, wl, model, S=10):
-        self.wl, self.model, self.S = wl, model, S
-        self.params = trk.default_cost_params(gate=True)
-        F, N, M = wl["streams"], wl["N"], wl["M"]
-        dev = wl["feat"].device
-        self.cost = {"C_total": torch.empty((F, M, N), device=dev)}
-        self.lsap_out = None
-        self.host_assign = torch.empty((F, M), dtype=torch.int32, pin_memory=True)
+    def __init__(self, sc, model, S=10):
+        self.sc, self.model, self.S = sc, model, S
+        self.tracker = trk.MultiStreamTracker(sc["streams"], capacity=1024, device=sc["feat"].device)
+        self.ids = {}
 
-    def stage_roi(self):
-        wl = self.wl
-        return trk.roi_align(wl["feat"], wl["rois"], (self.S, self.S), 40 / 1280.0, 2, True,
+    def stage_roi(self, f):
+        return trk.roi_align(self.sc["feat"], self.sc["rois"][f], (self.S, self.S), 40 / 1280.0, 2, True,
                              out_dtype=torch.bfloat16, channels_last=True)
 
     def stage_embed(self, roi):
         with torch.no_grad():
-            return self.model(roi).view(self.wl["streams"], self.wl["N"], 128)
+            return self.model(roi).view(self.sc["streams"], self.sc["N"], 128)
 
-    def stage_cost(self, emb):
-        wl = self.wl
-        F, N, M = wl["streams"], wl["N"], wl["M"]
-        return trk.build_cost(M=[M] * F, N=[N] * F, bank=wl["bank"], bank_len=wl["bank_len"],
-                              pbox=wl["pbox"], conf_prev=wl["conf_prev"], det_emb=emb, dbox=wl["dbox"],
-                              conf_cur=wl["conf_cur"], params=self.params, gmean=wl["gmean"],
-                              gsinv=wl["gsinv"], gate_on=wl["gate_on"], out=self.cost)
+    def step(self, f):
+        sc = self.sc
+        emb = self.stage_embed(self.stage_roi(f))
+        return self.tracker.step(emb, sc["dbox"][f], sc["dconf"][f], [sc["N"]] * sc["streams"],
+                                 sc["confs_host"][f], [f] * sc["streams"])
 
-    def stage_assign(self, cost):
-        wl = self.wl
-        F, N, M = wl["streams"], wl["N"], wl["M"]
-        self.lsap_out = trk.lsap_batched(cost["C_total"], [M] * F, [N] * F, cost_max=50.0, out=self.lsap_out)
-        return self.lsap_out
-
-    def step(self):
-        roi = self.stage_roi()
-        emb = self.stage_embed(roi)
-        cost = self.stage_cost(emb)
-        res = self.stage_assign(cost)
-        self.host_assign.copy_(res["assign"], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return self.host_assign
+    def check_identity(self, f, res):
+        """fraction of detections matched to the track that has followed the
+        same object since the track was created"""
+        ok = tot = 0
+        for s, r in enumerate(res):
+            objs = self.sc["obj"][f, s]
+            for tid, j in r.matches:
+                o = int(objs[j])
+                k = (s, int(tid))
+                if k not in self.ids:
+                    self.ids[k] = o
+                ok += self.ids[k] == o
+            tot += self.sc["N"]
+        return ok / max(tot, 1)
 
 
 # ----------------------------------------------------------- measurement --
-def stage_times(pipe, reps=5):
-    """Average device time per stage, HIP events on the launch stream."""
+def _ev():
+    return torch.cuda.Event(enable_timing=True)
+
+
+def kernel_pass(pipe, f, reps=10):
+    """Average device time of each hand-written kernel on the real step inputs,
+    HIP events on the stream the kernel is launched on (the current stream)."""
+    sc, tr = pipe.sc, pipe.tracker
     st = torch.cuda.current_stream()
-    names = ["roi_align", "encoder", "cost", "lsap"]
-    acc = {k: 0.0 for k in names}
-    for _ in range(reps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-        ev[0].record(st)
-        roi = pipe.stage_roi(); ev[1].record(st)
-        emb = pipe.stage_embed(roi); ev[2].record(st)
-        cost = pipe.stage_cost(emb); ev[3].record(st)
-        pipe.stage_assign(cost); ev[4].record(st)
+    out = {}
+
+    def timed(name, fn):
+        fn()
+        e0, e1 = _ev(), _ev()
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
         st.synchronize()
-        for k, n in enumerate(names):
-            acc[n] += ev[k].elapsed_time(ev[k + 1]) / reps
-    return acc
+        out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
+
+    nhwc = torch.empty((sc["streams"], 40, 40, 512), device=sc["feat"].device)
+    timed("roi_align", lambda: pipe.stage_roi(f))
+    roi = pipe.stage_roi(f)
+    m = pipe.model
+    W = m._fused_weights(torch.bfloat16, roi.device)
+    K = roi.shape[0]
+    Y1 = (roi.permute(0, 2, 3, 1).reshape(K * 100, 512) @ W["w1t"]).view(K, 10, 10, -1)
+    timed("dwconv5", lambda: ops.dwconv5_nhwc(Y1, W["dw_t"]))
+    timed("encoder", lambda: pipe.stage_embed(roi))
+    emb = pipe.stage_embed(roi)
+    # tracker kernels on the current track table (rows = all live tracks)
+    t = tr.table
+    S_, N = sc["streams"], sc["N"]
+    live = [tr.streams[s].live_sorted() for s in range(S_)]
+    M = max(len(l) for l in live)
+    row_slot = np.zeros((S_, M), np.int32)
+    for s in range(S_):
+        row_slot[s, :len(live[s])] = tr.streams[s].base + live[s]
+    rs = tr._i32(row_slot)
+    Ms = [len(l) for l in live]
+    cost_out = {"C_total": torch.empty((S_, M, N), device=emb.device)}
+    timed("cost", lambda: trk.build_cost(M=Ms, N=[N] * S_, bank=t.bank, bank_len=t.bank_len, pbox=t.pbox,
+                                         conf_prev=t.last_conf, det_emb=emb, dbox=sc["dbox"][f],
+                                         conf_cur=sc["dconf"][f], params=tr.params, gmean=t.gmean,
+                                         gsinv=t.gsinv, gate_on=t.gate_on, row_slot=rs, out=cost_out))
+    C = cost_out["C_total"]
+    lo = trk.lsap_batched(C, Ms, [N] * S_, cost_max=50.0)
+    timed("lsap", lambda: trk.lsap_batched(C, Ms, [N] * S_, cost_max=50.0, out=lo))
+    return out, M
 
 
-def cpu_baseline(wl, model_cpu, budget_s=20.0):
-    """The reference's CPU path, ported: oracle roi_align (torchvision CPU
-    semantics, C), the fp32 encoder on torch CPU, the oracle cost build
-    (bank top-k + bbox + conf + Mahalanobis gate, C) and the reference's own
-    solver scipy.optimize.linear_sum_assignment.  Bounded sample: whole frames
-    of one stream at N=256 until ~budget_s of CPU time."""
+def cpu_baseline(sc, sd, budget_s=20.0):
+    """The reference's CPU path, ported (oracle/): torchvision-semantics
+    roi_align (C), the fp32 encoder restated in plain torch, the bank top-k +
+    bbox + conf + Mahalanobis cost (C), and the reference's own solver
+    scipy.optimize.linear_sum_assignment.  Bounded sample: whole frames of one
+    stream at N=256 (tracks = the stream's objects, banks of 30) until
+    ~budget_s of CPU time."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from scipy.optimize import linear_sum_assignment
-    npw = wl["np"]
-    N, M = wl["N"], wl["M"]
+    npw = sc["np"]
+    N = sc["N"]
+    rng = np.random.default_rng(7)
+    bank = rng.standard_normal((N, 30, 128)).astype(np.float32)
+    bank /= np.linalg.norm(bank, axis=-1, keepdims=True)
+    gm = np.zeros((N, 4)); gs = np.tile(np.eye(4).reshape(1, 16) / 11.0, (N, 1))
     frames, t0 = 0, time.perf_counter()
     while True:
-        s = frames % wl["streams"]
-        rois = npw["rois"][s * N:(s + 1) * N].copy(); rois[:, 0] = 0
+        f, s = PREROLL + frames, frames % sc["streams"]
+        rois = npw["rois"][f % len(npw["rois"]), s * N:(s + 1) * N].copy()
+        rois[:, 0] = 0
         roi = O.roi_align(npw["feat"][s:s + 1], rois, (10, 10), 40 / 1280.0, 2, True)
         with torch.no_grad():
-            emb = model_cpu(torch.from_numpy(roi)).numpy()
-        out = O.cost_build(npw["bank"][s], np.full(M, wl["T"], np.int32), emb, npw["pbox"][s],
-                           npw["dbox"][s], npw["lconf"][s], npw["dconf"][s], npw["gm"][s],
-                           npw["gsinv"][s].reshape(M, 16), np.ones(M, np.int32))
+            emb = O.encoder_forward(sd, torch.from_numpy(roi)).numpy()
+        b = npw["dbox"][f % len(npw["dbox"]), s]
+        out = O.cost_build(bank, np.full(N, 30, np.int32), emb, b, b, npw["dconf"][f % len(npw["dconf"]), s],
+                           npw["dconf"][f % len(npw["dconf"]), s], gm, gs, np.ones(N, np.int32))
         linear_sum_assignment(out["C_total"])
         frames += 1
         el = time.perf_counter() - t0
         if el >= budget_s or frames >= 64:
             break
-    return dict(value=frames * N / el, unit="ROIs/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{frames} frames x N={N} of one stream, {el:.1f}s: oracle roi_align (C, 1 thread) + "
-                       f"fp32 encoder (torch CPU, {torch.get_num_threads()} threads) + oracle cost (C, 1 thread) "
-                       f"+ scipy linear_sum_assignment")
+    return dict(value=round(frames * N / el, 2), unit="ROIs/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"{frames} frames x N={N} of one stream in {el:.1f}s: oracle roi_align (C, 1 thread) + "
+                       f"fp32 encoder (plain torch CPU, {torch.get_num_threads()} threads) + oracle cost incl. "
+                       f"gate (C, 1 thread) + scipy linear_sum_assignment")
 
 
 def main():
@@ -201,26 +241,24 @@ def main():
     sd = {k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}
     model = trk.Model(512, 512, 10, 128).eval()
     model.load_state_dict(sd, strict=True)
-    model_cpu = model
-    model = trk.Model(512, 512, 10, 128).eval()
-    model.load_state_dict(sd, strict=True)
     model = model.to(dev)
 
-    wl = make_workload(dev, streams=args.streams, N=args.n, M=args.n, seed=1000 + rank)
-    pipe = Pipeline(wl, model)
-    for _ in range(args.warmup):
-        pipe.step()
-    # correctness guard on the measured workload: true pairs must be matched
-    a = pipe.step().numpy()
-    inv = np.argsort(wl["perm"], axis=1)
-    match_rate = float((a == inv).mean())
+    frames = PREROLL + args.warmup + args.steps
+    sc = make_scenes(dev, args.streams, args.n, frames, seed=1000 + rank)
+    pipe = Pipeline(sc, model)
+    f = 0
+    for _ in range(PREROLL + args.warmup):
+        pipe.step(f)
+        f += 1
 
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    results = []
     for _ in range(args.steps):
-        pipe.step()
+        results.append(pipe.step(f))
+        f += 1
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if dist is not None:
@@ -228,48 +266,49 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         dist.barrier()
-    rois_total = args.steps * wl["streams"] * wl["N"] * world
+    rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
+    ident = float(np.mean([pipe.check_identity(PREROLL + args.warmup + k, r) for k, r in enumerate(results)]))
 
-    st = stage_times(pipe)
+    kt, M = kernel_pass(pipe, f - 1)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
-    F, N, M, S = wl["streams"], wl["N"], wl["M"], 10
-    K = F * N
-    # algorithmic bytes per roi_align launch: map read once per frame,
-    # bf16 NHWC ROI tensor written once, 20 B of roi
-    roi_bytes = F * 512 * 40 * 40 * 4 + K * 512 * S * S * 2 + K * 20
-    enc_flops = K * ENC_FLOP_PER_ROI[S]
-    cost_flops = 2.0 * F * M * 32 * N * 128  # f32 MFMA incl. 30->32 padding of the bank
-    shares = {
-        "roi_align": dict(bound="hbm", achieved=roi_bytes / (st["roi_align"] * 1e-3) / 1e9, peak=HBM_PEAK_GBS,
-                          unit="GB/s"),
-        "encoder": dict(bound="mfma", achieved=enc_flops / (st["encoder"] * 1e-3) / 1e12, peak=BF16_PEAK_TFLOPS,
-                        unit="TFLOP/s"),
-        "cost": dict(bound="mfma", achieved=cost_flops / (st["cost"] * 1e-3) / 1e12, peak=F32_MFMA_PEAK_TFLOPS,
-                     unit="TFLOP/s"),
+    Fs, N, S = sc["streams"], sc["N"], 10
+    K = Fs * N
+    # algorithmic work per launch; DESIGN.md §Roofline
+    algo = {
+        "roi_align": ("hbm", Fs * 512 * 40 * 40 * 4 + K * 512 * S * S * 2 + K * 20, HBM_PEAK_GBS, "GB/s"),
+        "dwconv5": ("hbm", 2 * K * S * S * 1024 * 2 + 25 * 1024 * 4, HBM_PEAK_GBS, "GB/s"),
+        "encoder": ("mfma", K * ENC_FLOP_PER_ROI[S], BF16_PEAK_TFLOPS, "TFLOP/s"),
+        "cost": ("mfma", 2.0 * Fs * M * 32 * N * 128, F32_MFMA_PEAK_TFLOPS, "TFLOP/s"),
     }
-    dom = max(["roi_align", "encoder", "cost"], key=lambda k: st[k])
-    rf = dict(shares[dom])
-    rf["kernel"] = dom
-    rf["frac"] = rf["achieved"] / rf["peak"]
-    rf["traffic"] = None
-    rf["stage_ms"] = {k: round(v, 4) for k, v in st.items()}
-    rf["stage_frac"] = {k: round(v["achieved"] / v["peak"], 4) for k, v in shares.items()}
+    per = {}
+    for k, (bound, work, peak, unit) in algo.items():
+        ach = work / (kt[k] * 1e-6) / (1e9 if unit == "GB/s" else 1e12)
+        per[k] = dict(bound=bound, us=round(kt[k], 2), achieved=round(ach, 2), peak=peak, unit=unit,
+                      frac=round(ach / peak, 4))
+    # dominant hand-written kernel by measured time (LSAP is latency-bound: no roofline)
+    mine = {k: kt[k] for k in ("roi_align", "dwconv5", "cost", "lsap")}
+    dom = max(("roi_align", "dwconv5", "cost"), key=lambda k: mine[k])
+    rf = {"kernel": dom, "bound": per[dom]["bound"], "achieved": per[dom]["achieved"],
+          "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
+          "traffic": None, "kernel_us": {k: round(v, 2) for k, v in kt.items()},
+          "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2)}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",
         "value": round(value, 1), "unit": "ROIs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16-encoder/f32-cost/f64-lsap", "data": "synthetic",
-        "config": {"workload": "c3: 8 streams x N=256 dets x M=256 tracks per GPU, [8,512,40,40] maps, "
-                               "10x10 ROIs, bank T=30", "streams_per_gpu": F, "N": N, "M": M,
-                   "roi": S, "parallelism": f"replicas{world}"},
-        "roofline": rf, "match_rate": match_rate,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16 encoder / f32 roi+cost / f64 KF+LSAP duals",
+        "data": "synthetic (SiLU(randn) maps, moving boxes; seeded random encoder weights)",
+        "config": {"workload": f"c3: {Fs} streams x N={N} detections/frame per GPU, [{Fs},512,40,40] maps, "
+                               f"10x10 ROIs, full tracker step (bank T=30, KF, 2-stage assign)",
+                   "streams_per_gpu": Fs, "N": N, "roi": S, "parallelism": f"replicas{world}"},
+        "roofline": rf, "identity_rate": round(ident, 5),
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(wl, model_cpu, args.cpu_budget)
+        line["cpu_baseline"] = cpu_baseline(sc, sd, args.cpu_budget)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

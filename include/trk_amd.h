@@ -151,6 +151,41 @@ int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, in
 /* x[n, p, c] *= s[n, c] in place (SE excitation, card.py:78). */
 int trk_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int dtype, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Device-resident track state.  Track slots of all
+ * streams share one set of slot arrays:
+ *   x [S][8] f64, P [S][64] f64           Kalman state (float64 throughout)
+ *   pbox [S][4] f32, last_conf [S] f32     mem.last_bbox / mem.last_conf
+ *   gmean [S][4] f64, gsinv [S][16] f64    gate inputs (see trk_build_cost)
+ *   enc [S][128] f32                       mem.encoder_feat (EMA, unit)
+ *   bank [S][T][128] f32, bank_len [S], bank_head [S]   mem.feat_historical ring
+ * Detection arrays are indexed by a global detection row d: dbox [d][4],
+ * dconf [d], demb [d][128].
+ * ---------------------------------------------------------------------- */
+/* Tracking.predict_all (reference model/mainTracking.py:340-345): x = F x,
+ * P = F P F^T + Q for each listed slot; pbox = x_to_bbox_xyxy(x)
+ * (KalmanFilter.py:19-33); gmean/gsinv for the Mahalanobis gate. */
+int trk_kf_predict(int64_t n, const int32_t* slots, double* x, double* P, float* pbox,
+                   double* gmean, double* gsinv, void* stream);
+/* Tracking.update_matched (mainTracking.py:375-448) for n matched (slot, det)
+ * pairs: filterpy update (Joseph form), last_bbox/last_conf, then -- if
+ * conf >= conf_update_min, cost[cost_idx] <= cost_update_max (cost may be NULL)
+ * and the post-update Mahalanobis d2 <= maha_thr -- the EMA feature update and
+ * the bank push (ring of T = hist_max). */
+int trk_track_update(int64_t n, const int32_t* slots, const int32_t* dets,
+                     const int64_t* cost_idx, const float* cost, const float* dbox,
+                     const float* dconf, const float* demb, double* x, double* P,
+                     float* pbox, float* last_conf, float* enc, float* bank,
+                     int32_t* bank_len, int32_t* bank_head, int64_t T, float ema_alpha,
+                     float conf_update_min, float cost_update_max, double maha_thr,
+                     void* stream);
+/* Tracking.create_new_tracks / creat_item / init_kf_from_bbox
+ * (mainTracking.py:99-140,362-373, KalmanFilter.py:36-101) for n (slot, det). */
+int trk_track_init(int64_t n, const int32_t* slots, const int32_t* dets, const float* dbox,
+                   const float* dconf, const float* demb, double* x, double* P, float* pbox,
+                   float* last_conf, float* enc, float* bank, int32_t* bank_len,
+                   int32_t* bank_head, int64_t T, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
