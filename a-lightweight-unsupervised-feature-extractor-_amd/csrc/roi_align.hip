@@ -152,33 +152,37 @@ struct TapSrc {
   int rstride, cstride, y0, x0;
 };
 
+template <int VEC, bool OUT_BF16>
+__device__ __forceinline__ void store_nhwc(void* out, int64_t o, const float (&v)[VEC]) {
+  if (OUT_BF16) {
+    uint16_t* po = reinterpret_cast<uint16_t*>(out) + o;
+    if constexpr (VEC == 4) {
+      *reinterpret_cast<uint2*>(po) = make_uint2(
+          (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16),
+          (uint32_t)trk::f32_to_bf16(v[2]) | ((uint32_t)trk::f32_to_bf16(v[3]) << 16));
+    } else if constexpr (VEC == 2) {
+      *reinterpret_cast<uint32_t*>(po) =
+          (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16);
+    } else {
+      po[0] = trk::f32_to_bf16(v[0]);
+    }
+  } else {
+    float* po = reinterpret_cast<float*>(out) + o;
+    if constexpr (VEC == 4) {
+      *reinterpret_cast<float4*>(po) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (VEC == 2) {
+      *reinterpret_cast<float2*>(po) = make_float2(v[0], v[1]);
+    } else {
+      po[0] = v[0];
+    }
+  }
+}
+
 template <int VEC, bool OUT_BF16, bool OUT_NHWC>
 __device__ __forceinline__ void store_bin(void* out, float* otile, int lds_stride, int n, int bin,
                                           int nbins, int C, int c, int lane, const float (&v)[VEC]) {
   if (OUT_NHWC) {
-    const int64_t o = ((int64_t)n * nbins + bin) * C + c;
-    if (OUT_BF16) {
-      uint16_t* po = reinterpret_cast<uint16_t*>(out) + o;
-      if constexpr (VEC == 4) {
-        *reinterpret_cast<uint2*>(po) = make_uint2(
-            (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16),
-            (uint32_t)trk::f32_to_bf16(v[2]) | ((uint32_t)trk::f32_to_bf16(v[3]) << 16));
-      } else if constexpr (VEC == 2) {
-        *reinterpret_cast<uint32_t*>(po) =
-            (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16);
-      } else {
-        po[0] = trk::f32_to_bf16(v[0]);
-      }
-    } else {
-      float* po = reinterpret_cast<float*>(out) + o;
-      if constexpr (VEC == 4) {
-        *reinterpret_cast<float4*>(po) = make_float4(v[0], v[1], v[2], v[3]);
-      } else if constexpr (VEC == 2) {
-        *reinterpret_cast<float2*>(po) = make_float2(v[0], v[1]);
-      } else {
-        po[0] = v[0];
-      }
-    }
+    store_nhwc<VEC, OUT_BF16>(out, ((int64_t)n * nbins + bin) * C + c, v);
   } else if (lds_stride > 0) {
 #pragma unroll
     for (int k = 0; k < VEC; ++k) otile[(lane * VEC + k) * lds_stride + bin] = v[k];
@@ -203,15 +207,16 @@ __device__ __forceinline__ void bins_loop(const TapSrc& src, const RegTab& yt, c
   // 4*SR*SR taps of a bin are in flight before the first use
   const int gh = SR > 0 ? SR : gh_rt, gw = SR > 0 ? SR : gw_rt;
   const int nbins = PH * PW;
+  constexpr int UR = SR > 0 ? SR : 1;
   for (int bin = wave; bin < nbins; bin += 4) {
     const int ph = bin / PW, pw = bin % PW;
     float v[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) v[k] = 0.f;
-#pragma unroll(SR > 0 ? SR : 1)
+#pragma unroll UR
     for (int iy = 0; iy < gh; ++iy) {
       const AxisTab ty = tab_get(yt, ph * gh + iy);
-#pragma unroll(SR > 0 ? SR : 1)
+#pragma unroll UR
       for (int ix = 0; ix < gw; ++ix) {
         const AxisTab tx = tab_get(xt, pw * gw + ix);
         float w1, w2, w3, w4;
@@ -400,9 +405,229 @@ roi_align_nhwc_kernel(const float* __restrict__ in,  // [B,H,W,C]
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-sweep kernel (NHWC output, sampling_ratio 2: the encoder / bench path).
+//
+// One wave = (ROI, bin row ph, 256*NH-channel chunk).  The x sample table is
+// the same for every sample row and consecutive x samples mostly fall in the
+// same pair of map columns, so the wave walks the bin row left to right and
+// keeps, per sample row iy, the two current tap columns (rows ylo and yhi) in
+// registers: a column is loaded only when a sample crosses into it (~6x fewer
+// tap loads than 4 per sample for the reference's 1..10-cell ROIs; the
+// per-sample-tap kernel above is L1/TA-bound).  The 2*PW samples are fully
+// unrolled, so bin completion and store offsets are static.  Arithmetic is
+// unchanged: t = w1*f1 + w2*f2 + w3*f3 + w4*f4 per sample in torchvision's
+// order, samples added to the bin in (iy, ix) order (row iy = 1 held until
+// row iy = 0 is in), times 1/4 (== / 4 exactly).  The math runs on float2
+// pairs (v_pk_mul_f32 / v_pk_add_f32, separate mul and add: same rounding).
+// Loads are buffer loads: the frame's map is one descriptor, the cell offset
+// a scalar (soffset), the lane's channel offset the only per-lane part.
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void bload4(__amdgpu_buffer_rsrc_t rs, int voff, int soff, f2_t (&v)[2]) {
+  const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  v[0] = f2_t{__uint_as_float(x[0]), __uint_as_float(x[1])};
+  v[1] = f2_t{__uint_as_float(x[2]), __uint_as_float(x[3])};
+}
+
+// t = w1*f1 + w2*f2 + w3*f3 + w4*f4 (torchvision's order, no contraction)
+template <int NH>
+__device__ __forceinline__ void sample4(f2_t (&t)[NH][2], float w1, float w2, float w3, float w4,
+                                        const f2_t (&f1)[NH][2], const f2_t (&f2)[NH][2],
+                                        const f2_t (&f3)[NH][2], const f2_t (&f4)[NH][2]) {
+  const f2_t W1 = {w1, w1}, W2 = {w2, w2}, W3 = {w3, w3}, W4 = {w4, w4};
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      f2_t s = W1 * f1[h][p];
+      s = s + W2 * f2[h][p];
+      s = s + W3 * f3[h][p];
+      s = s + W4 * f4[h][p];
+      t[h][p] = s;
+    }
+}
+
+// Two-column register cache of one sample row: columns ca (a*) and cb (b*)
+// at rows ylo (*0) and yhi (*1).
+template <int NH>
+struct ColCache2 {
+  f2_t a0[NH][2], a1[NH][2], b0[NH][2], b1[NH][2];
+  int ca, cb;
+};
+
+template <int NH>
+__device__ __forceinline__ void cache_load(f2_t (&v0)[NH][2], f2_t (&v1)[NH][2], __amdgpu_buffer_rsrc_t rs,
+                                           const int (&voff)[NH], int s0, int s1) {
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    bload4(rs, voff[h], s0, v0[h]);
+    bload4(rs, voff[h], s1, v1[h]);
+  }
+}
+
+template <int NH, bool OUT_BF16, int PW>
+__global__ void __launch_bounds__(256)
+roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
+                 int C, int H, int W, const float* __restrict__ rois, float spatial_scale,
+                 int PH, int aligned, void* __restrict__ out, int nchunks, int64_t nitems) {
+  constexpr int CPW = 256 * NH, NS = 2 * PW;
+  static_assert(NS <= 64, "one x sample per lane");
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t item = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+  if (item >= nitems) return;  // wave-uniform
+  const int chunk = (int)(item % nchunks);
+  const int64_t t_ = item / nchunks;
+  const int ph = (int)(t_ % PH);
+  const int n = (int)(t_ / PH);
+
+  const float* r = rois + (int64_t)n * 5;
+  const int b = __builtin_amdgcn_readfirstlane((int)r[0]);
+  const float off = aligned ? 0.5f : 0.0f;
+  const float sw = r[1] * spatial_scale - off;
+  const float sh = r[2] * spatial_scale - off;
+  const float ew = r[3] * spatial_scale - off;
+  const float eh = r[4] * spatial_scale - off;
+  float rw = ew - sw, rh = eh - sh;
+  if (!aligned) {
+    rw = fmaxf(rw, 1.f);
+    rh = fmaxf(rh, 1.f);
+  }
+  const float bh = rh / (float)PH, bw = rw / (float)PW;
+
+  // the two y samples of this bin row (uniform)
+  int so[2][2], yv[2];
+  float yl[2], yh[2];
+  const float t0 = sh + (float)ph * bh;
+  const int rowb = W * C * 4, colb = C * 4;
+#pragma unroll
+  for (int iy = 0; iy < 2; ++iy) {
+    const AxisTab a = axis_sample(t0 + ((float)iy + .5f) * bh / 2.0f, H);
+    so[iy][0] = __builtin_amdgcn_readfirstlane(a.lo) * rowb;
+    so[iy][1] = __builtin_amdgcn_readfirstlane(a.hi) * rowb;
+    yv[iy] = __builtin_amdgcn_readfirstlane(a.valid);
+    yl[iy] = a.l;
+    yh[iy] = a.h;
+  }
+  // lane q = x sample q (pre_calc restated): packed lo | hi << 12 | valid << 24
+  // and the sample's four weights for each y sample (the same float products)
+  int xpk;
+  float wq[2][4];
+  {
+    AxisTab a;
+    a.lo = a.hi = a.valid = 0; a.l = a.h = 0.f;
+    if (lane < NS) {
+      const int pw = lane >> 1, ix = lane & 1;
+      const float s0 = sw + (float)pw * bw;
+      a = axis_sample(s0 + ((float)ix + .5f) * bw / 2.0f, W);
+    }
+    xpk = a.lo | (a.hi << 12) | (a.valid << 24);
+#pragma unroll
+    for (int iy = 0; iy < 2; ++iy) {
+      wq[iy][0] = yh[iy] * a.h; wq[iy][1] = yh[iy] * a.l;
+      wq[iy][2] = yl[iy] * a.h; wq[iy][3] = yl[iy] * a.l;
+    }
+  }
+
+  // the frame's map as one buffer (descriptor inputs readfirstlane'd so the
+  // compiler can prove it uniform -- otherwise every buffer op is a waterfall)
+  const uint64_t fa = reinterpret_cast<uint64_t>(in + (int64_t)b * H * W * C);
+  const uint32_t fa_lo = __builtin_amdgcn_readfirstlane((uint32_t)fa);
+  const uint32_t fa_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fa >> 32));
+  const int nbytes = __builtin_amdgcn_readfirstlane(H * W * C * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((uint64_t)fa_hi << 32) | fa_lo), 0, nbytes, 0x00020000);
+  int voff[NH];
+  bool act[NH];
+  const int cbase = chunk * CPW;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int c = cbase + h * 256 + lane * 4;
+    act[h] = c < C;
+    voff[h] = (act[h] ? c : 0) * 4;
+  }
+  f2_t zero[NH][2];  // pixel (0,0): what torchvision reads for an empty sample
+#pragma unroll
+  for (int h = 0; h < NH; ++h) bload4(rs, voff[h], 0, zero[h]);
+
+  ColCache2<NH> kc[2];
+  kc[0].ca = kc[0].cb = kc[1].ca = kc[1].cb = -1;
+  const f2_t Z = {0.f, 0.f}, Q = {0.25f, 0.25f};
+  f2_t acc[NH][2], hold[NH][2];
+  uint8_t* obase = reinterpret_cast<uint8_t*>(out) +
+                   ((((int64_t)n * PH + ph) * PW) * C + cbase + lane * 4) * (OUT_BF16 ? 2 : 4);
+
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int pk = __builtin_amdgcn_readlane(xpk, j);
+    const int lo = pk & 0xfff, hi = (pk >> 12) & 0xfff, xv = pk >> 24;
+    f2_t t[2][NH][2];
+#pragma unroll
+    for (int iy = 0; iy < 2; ++iy) {
+      if (yv[iy] && xv) {
+        ColCache2<NH>& k = kc[iy];
+        if (lo != k.ca) {
+          if (lo == k.cb) {
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+#pragma unroll
+              for (int p = 0; p < 2; ++p) { k.a0[h][p] = k.b0[h][p]; k.a1[h][p] = k.b1[h][p]; }
+          } else {
+            cache_load<NH>(k.a0, k.a1, rs, voff, so[iy][0] + lo * colb, so[iy][1] + lo * colb);
+          }
+          k.ca = lo;
+        }
+        if (hi != k.cb) {
+          if (hi == k.ca) {
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+#pragma unroll
+              for (int p = 0; p < 2; ++p) { k.b0[h][p] = k.a0[h][p]; k.b1[h][p] = k.a1[h][p]; }
+          } else {
+            cache_load<NH>(k.b0, k.b1, rs, voff, so[iy][0] + hi * colb, so[iy][1] + hi * colb);
+          }
+          k.cb = hi;
+        }
+        const float w1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][0]), j));
+        const float w2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][1]), j));
+        const float w3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][2]), j));
+        const float w4 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][3]), j));
+        sample4<NH>(t[iy], w1, w2, w3, w4, k.a0, k.b0, k.a1, k.b1);
+      } else {
+        sample4<NH>(t[iy], 0.f, 0.f, 0.f, 0.f, zero, zero, zero, zero);
+      }
+    }
+    if ((j & 1) == 0) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          acc[h][p] = Z + t[0][h][p];
+          hold[h][p] = t[1][h][p];
+        }
+    } else {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        float v[4];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          f2_t s = acc[h][p] + t[0][h][p];
+          s = s + hold[h][p];
+          s = s + t[1][h][p];
+          s = s * Q;  // == s / 4 exactly (power of two)
+          v[2 * p] = s.x;
+          v[2 * p + 1] = s.y;
+        }
+        if (act[h]) store_nhwc<4, OUT_BF16>(obase + ((int64_t)(j >> 1) * C + h * 256) * (OUT_BF16 ? 2 : 4), 0, v);
+      }
+    }
+  }
+}
+
 // tuning knobs (trk_set_tuning): LDS window budget per workgroup, channels per lane
 int g_roi_window_kb = 0;   // measured r01: direct L2 taps beat LDS window staging (229 vs 300+ us)
 int g_roi_vec = 0;  // 0 = auto
+int g_roi_sweep = 1;  // NHWC output: row-sweep kernel, 256 (1) or 512 (2) channels per wave
 
 template <int VEC, bool OUT_BF16, bool OUT_NHWC>
 int launch_roi(const float* nhwc, int B, int C, int H, int W, const float* rois, int K,
@@ -445,6 +670,28 @@ int launch_roi(const float* nhwc, int B, int C, int H, int W, const float* rois,
   return trk::check_launch("roi_align_nhwc_kernel");
 }
 
+template <int NH, bool OUT_BF16, int PW>
+int launch_sweep(const float* nhwc, int C, int H, int W, const float* rois, int K, float scale, int PH,
+                 int aligned, void* out, hipStream_t st) {
+  const int nchunks = (C + 256 * NH - 1) / (256 * NH);
+  const int64_t nitems = (int64_t)K * PH * nchunks;
+  const int64_t nwg = (nitems + 3) / 4;
+  if (nwg > 0x7fffffff) {
+    trk::set_error("roi_align: too many workgroups");
+    return TRK_EUNSUPPORTED;
+  }
+  hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, C, H, W,
+                     rois, scale, PH, aligned, out, nchunks, nitems);
+  return trk::check_launch("roi_sweep_kernel");
+}
+
+template <bool OUT_BF16, int PW>
+int dispatch_sweep(const float* nhwc, int C, int H, int W, const float* rois, int K, float scale, int PH,
+                   int aligned, void* out, hipStream_t st) {
+  if (g_roi_sweep == 2) return launch_sweep<2, OUT_BF16, PW>(nhwc, C, H, W, rois, K, scale, PH, aligned, out, st);
+  return launch_sweep<1, OUT_BF16, PW>(nhwc, C, H, W, rois, K, scale, PH, aligned, out, st);
+}
+
 template <bool OUT_BF16, bool OUT_NHWC>
 int dispatch_vec(int C, const float* nhwc, int B, int H, int W, const float* rois, int K, float scale,
                  int PH, int PW, int sr, int aligned, void* out, hipStream_t st) {
@@ -462,6 +709,7 @@ int dispatch_vec(int C, const float* nhwc, int B, int H, int W, const float* roi
 extern "C" int trk_set_tuning(const char* key, int value) {
   TRK_REQUIRE(key, "set_tuning: null key");
   if (!strcmp(key, "roi_window_kb")) { TRK_REQUIRE(value >= 0 && value <= 150, "roi_window_kb in [0,150]"); g_roi_window_kb = value; return TRK_OK; }
+  if (!strcmp(key, "roi_sweep")) { TRK_REQUIRE(value >= 0 && value <= 2, "roi_sweep in {0,1,2}"); g_roi_sweep = value; return TRK_OK; }
   if (!strcmp(key, "roi_vec")) { TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "roi_vec in {0,1,2,4}"); g_roi_vec = value; return TRK_OK; }
   trk::set_error("set_tuning: unknown key '%s'", key);
   return TRK_EINVAL;
@@ -509,6 +757,14 @@ extern "C" int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64
               "roi_align: output_size x sampling_ratio must be <= 128 per axis");
   const int iB = (int)B, iC = (int)C, iH = (int)H, iW = (int)W, iK = (int)K;
   const bool bf = out_dtype == TRK_BF16, nhwc_out = out_layout == TRK_NHWC;
+  if (nhwc_out && g_roi_sweep && iC % 4 == 0 && sampling_ratio == 2 && (PW == 10 || PW == 7) && iH < 4096 &&
+      iW < 4096 && (int64_t)iH * iW * iC < ((int64_t)1 << 29)) {
+    if (PW == 10)
+      return bf ? dispatch_sweep<true, 10>(nhwc, iC, iH, iW, rois, iK, spatial_scale, PH, aligned, out, st)
+                : dispatch_sweep<false, 10>(nhwc, iC, iH, iW, rois, iK, spatial_scale, PH, aligned, out, st);
+    return bf ? dispatch_sweep<true, 7>(nhwc, iC, iH, iW, rois, iK, spatial_scale, PH, aligned, out, st)
+              : dispatch_sweep<false, 7>(nhwc, iC, iH, iW, rois, iK, spatial_scale, PH, aligned, out, st);
+  }
   if (bf && nhwc_out) return dispatch_vec<true, true>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);
   if (bf && !nhwc_out) return dispatch_vec<true, false>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);
   if (!bf && nhwc_out) return dispatch_vec<false, true>(iC, nhwc, iB, iH, iW, rois, iK, spatial_scale, PH, PW, sampling_ratio, aligned, out, st);

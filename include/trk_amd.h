@@ -40,7 +40,8 @@ int trk_abi_version(void);
 const char* trk_last_error(void);
 /* Performance knobs (process-global; results are bit-identical for every value):
  *   "roi_window_kb"  LDS budget (KiB) for staging a ROI's source window; 0 = never stage
- *   "roi_vec"        channels per lane in roi_align (0 = auto, 1, 2, 4)            */
+ *   "roi_vec"        channels per lane in roi_align (0 = auto, 1, 2, 4)
+ *   "roi_sweep"      1 (default): NHWC output through the row-sweep kernel; 0: per-sample taps */
 int trk_set_tuning(const char* key, int value);
 
 /* ------------------------------------------------------------------------

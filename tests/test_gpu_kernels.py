@@ -80,6 +80,39 @@ def test_roi_align_batched_frames_and_edges(trk, oracle, gpu):
     assert np.array_equal(got3.cpu().numpy(), exp3)
 
 
+@pytest.mark.parametrize("sweep", [1, 2, 0])
+def test_roi_align_nhwc_out_paths(trk, oracle, gpu, sweep):
+    """NHWC output goes through the row-sweep kernel (register column cache);
+    roi_sweep=0 selects the per-sample-tap kernel.  Both bit-exact, including
+    edge ROIs, sampling ratios 1..4, aligned=False, non-square bins and a
+    channel count that leaves a partial chunk."""
+    L = trk.lib()
+    rng = np.random.default_rng(11)
+    B, N = 3, 96
+    feat = _feat(rng, B, C=516, H=23, W=31)
+    boxes = _boxes(rng, B * N, img=992, pad=100)
+    rois = np.concatenate([np.repeat(np.arange(B), N).astype(np.float32)[:, None], boxes], 1)
+    rois[0, 1:] = [2000, 2000, 2100, 2100]
+    rois[1, 1:] = [-300, -300, 100, 100]
+    rois[2, 1:] = [900, 700, 1400, 1500]
+    rois[3, 1:] = [500, 500, 500, 500]
+    rois[4, 1:] = [700, 700, 650, 640]
+    rois[5, 1:] = [-50, -50, 1330, 1330]
+    x = torch.from_numpy(feat).to(gpu)
+    r = torch.from_numpy(rois).to(gpu)
+    try:
+        L.trk_set_tuning(b"roi_sweep", sweep)
+        for (ph, pw), sr, al in (((10, 10), 2, True), ((7, 7), 2, True), ((7, 5), 3, False),
+                                 ((4, 6), 1, True), ((5, 3), 4, True)):
+            exp = oracle.roi_align(feat, rois, (ph, pw), 1 / 32, sr, al)
+            got = trk.roi_align(x, r, (ph, pw), 1 / 32, sr, al, channels_last=True)
+            assert np.array_equal(got.cpu().numpy(), exp), (ph, pw, sr, al)
+            bf = trk.roi_align(x, r, (ph, pw), 1 / 32, sr, al, out_dtype=torch.bfloat16, channels_last=True)
+            assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16()), (ph, pw, sr, al)
+    finally:
+        L.trk_set_tuning(b"roi_sweep", 1)
+
+
 def test_roi_align_odd_channels_and_empty(trk, oracle, gpu):
     rng = np.random.default_rng(4)
     feat = rng.standard_normal((2, 37, 13, 11)).astype(np.float32)

@@ -35,22 +35,24 @@ def main():
     K = B * N
     algo = B * C * H * H * 4 + K * C * S * S * 2 + K * 20
     res = {}
-    variants = [(0, 4), (0, 2), (32, 2), (64, 2), (96, 2), (48, 1), (64, 4)]
+    variants = [(1, 0, 0), (2, 0, 0), (0, 0, 4)]
     for rnd in range(3):
-        for wk, vec in variants:
-            L.set_tuning("roi_window_kb", wk); L.set_tuning("roi_vec", vec)
+        for sw, wk, vec in variants:
+            L.set_tuning("roi_sweep", sw); L.set_tuning("roi_window_kb", wk); L.set_tuning("roi_vec", vec)
             f = lambda: trk.roi_align(nhwc, rois, (S, S), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True)
             out = f()
             ok = torch.equal(out, ref)
             t = timeit(f)
-            res.setdefault((wk, vec), []).append(t)
+            res.setdefault((sw, wk, vec), []).append(t)
             if rnd == 2:
-                tm = float(np.median(res[(wk, vec)]))
-                print(json.dumps({"item": "roi_align_nhwc_in", "window_kb": wk, "vec": vec, "us": round(tm, 1),
+                tm = float(np.median(res[(sw, wk, vec)]))
+                print(json.dumps({"item": "roi_align_nhwc_in", "sweep": sw, "window_kb": wk, "vec": vec, "us": round(tm, 1),
                                   "GBps": round(algo / tm / 1e3, 1), "bitexact": ok}), flush=True)
-    L.set_tuning("roi_window_kb", 64); L.set_tuning("roi_vec", 0)
+    L.set_tuning("roi_sweep", 1); L.set_tuning("roi_window_kb", 0); L.set_tuning("roi_vec", 0)
     t = timeit(lambda: trk.roi_align(feat, rois, (S, S), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True))
     print(json.dumps({"item": "roi_align_nchw_in(default)", "us": round(t, 1)}), flush=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "roi":
+        return
     # encoder pieces
     y1t = torch.randn(K, S, S, 1024, device=dev).bfloat16()
     wdw = torch.randn(25, 1024, device=dev)
