@@ -145,8 +145,11 @@ def kernel_pass(pipe, f, reps=10):
         st.synchronize()
         out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
 
-    nhwc = torch.empty((sc["streams"], 40, 40, 512), device=sc["feat"].device)
-    timed("roi_align", lambda: pipe.stage_roi(f))
+    # roi_align kernel alone (map already NHWC) and the stage (NCHW map: + transpose)
+    nhwc = sc["feat"].contiguous(memory_format=torch.channels_last)
+    timed("roi_align", lambda: trk.roi_align(nhwc, sc["rois"][f], (pipe.S, pipe.S), 40 / 1280.0, 2, True,
+                                             out_dtype=torch.bfloat16, channels_last=True))
+    timed("roi_stage", lambda: pipe.stage_roi(f))
     roi = pipe.stage_roi(f)
     m = pipe.model
     W = m._fused_weights(torch.bfloat16, roi.device)
@@ -292,9 +295,21 @@ def main():
     # dominant hand-written kernel by measured time (LSAP is latency-bound: no roofline)
     mine = {k: kt[k] for k in ("roi_align", "dwconv5", "cost", "lsap")}
     dom = max(("roi_align", "dwconv5", "cost"), key=lambda k: mine[k])
+    # HBM traffic per launch from the committed rocprofv3 --pmc summary of this
+    # bench (tools/gpu_pmc.sh -> profiles/pmc_traffic.json); null if absent
+    traffic, tsrc = None, None
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as fh:
+            pm = json.load(fh)
+        e = pm["kernels"].get(dom)
+        if e is not None:
+            traffic = e["read_bytes"] + e["write_bytes"]
+            tsrc = pm.get("profile", "profiles/pmc_traffic.json")
+    except (OSError, KeyError, ValueError):
+        pass
     rf = {"kernel": dom, "bound": per[dom]["bound"], "achieved": per[dom]["achieved"],
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
-          "traffic": None, "kernel_us": {k: round(v, 2) for k, v in kt.items()},
+          "traffic": traffic, "traffic_source": tsrc, "algorithmic_work_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2)}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",

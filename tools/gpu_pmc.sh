@@ -14,5 +14,5 @@ for C in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "rc=$rc"; tail -n 3 "$OUT/pmc_${TAG}_$C.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
-cd "$ROOT" && python3 tools/pmc_summary.py "$OUT/pmc_${TAG}_FETCH_SIZE" "$OUT/pmc_${TAG}_WRITE_SIZE" > "$OUT/pmc_${TAG}_summary.txt"
+cd "$ROOT" && python3 tools/pmc_summary.py "$OUT/pmc_${TAG}_FETCH_SIZE" "$OUT/pmc_${TAG}_WRITE_SIZE" "$OUT/pmc_traffic_${TAG}.json" > "$OUT/pmc_${TAG}_summary.txt"
 cat "$OUT/pmc_${TAG}_summary.txt"

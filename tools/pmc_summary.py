@@ -37,6 +37,20 @@ def main():
     for k, v in short[:20]:
         print(f"{k[:90]:90s} n={v['launches']:4d} fetch={v['fetch_kib'] or 0:12.1f} KiB write={v['write_kib'] or 0:12.1f} KiB")
     print("JSON " + json.dumps(out))
+    if len(sys.argv) > 3:  # short-name traffic table for bench.py (profiles/pmc_traffic.json)
+        short_names = {"roi_sweep_kernel": "roi_align", "dwconv5_nhwc_kernel": "dwconv5", "cost_kernel": "cost",
+                       "lsap_kernel": "lsap", "act_mean_kernel": "act_mean", "scale_rows_kernel": "scale_rows",
+                       "nchw_to_nhwc_kernel": "nchw_to_nhwc", "track_update_kernel": "track_update"}
+        tab = {}
+        for k, v in out.items():
+            for pat, nm in short_names.items():
+                if pat in k and v["read_bytes_corrected"] is not None and v["write_bytes"] is not None:
+                    tab[nm] = dict(read_bytes=round(v["read_bytes_corrected"]), write_bytes=round(v["write_bytes"]),
+                                   launches=v["launches"], kernel=k[:120])
+        with open(sys.argv[3], "w") as f:
+            json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (separate runs); "
+                                 "read = 2 x FETCH_SIZE (gfx950 64-B tally of 128-B requests, MI355X_MICROARCH.md "
+                                 "§HBM), per launch averages", "kernels": tab}, f, indent=1)
 
 
 if __name__ == "__main__":
