@@ -217,6 +217,24 @@ def cpu_baseline(sc, sd, budget_s=20.0):
                        f"gate (C, 1 thread) + scipy linear_sum_assignment")
 
 
+def timed_region(step, steps, dist, sync, red_dev):
+    """Run `steps` steps between a barrier + device sync on both sides; return
+    the MAX elapsed time over ranks (one all_reduce) and the step outputs."""
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    out = [step(k) for k in range(steps)]
+    sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=red_dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        dist.barrier()
+    return el, out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,21 +272,9 @@ def main():
         pipe.step(f)
         f += 1
 
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    results = []
-    for _ in range(args.steps):
-        results.append(pipe.step(f))
-        f += 1
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        dist.barrier()
+    el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
+                               torch.cuda.synchronize, dev)
+    f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
     ident = float(np.mean([pipe.check_identity(PREROLL + args.warmup + k, r) for k, r in enumerate(results)]))

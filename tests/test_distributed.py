@@ -1,0 +1,98 @@
+"""Multi-rank path of bench.py on CPU (gloo, world size 2).
+
+The path shards by video stream with no data-path collective:
+each rank owns its own streams; the only communication is the barrier pair and
+one MAX all_reduce of the elapsed time around the timed region.  These tests
+run that exact code (`bench.timed_region`) in two gloo processes and check the
+aggregate bookkeeping, plus that ranks build disjoint synthetic workloads.
+"""
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, REPO)
+    import bench
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def step(k):  # rank r's steps take (r + 1) * 20 ms
+            time.sleep(0.02 * (rank + 1))
+            calls.append(k)
+            return rank * 100 + k
+
+        el, out = bench.timed_region(step, 3, tdist, lambda: None, torch.device("cpu"))
+        # per-rank workload: different seeds -> different boxes, same shapes
+        sc = bench.make_scenes(torch.device("cpu"), 2, 8, 3, seed=1000 + rank, C=4, H=8)
+        q.put((rank, el, out, calls, sc["np"]["rois"].copy()))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_timed_region_max_over_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, el, out, calls, rois = q.get(timeout=240)
+        res[r] = (el, out, calls, rois)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    # every rank ran exactly its own steps, in order
+    for r in (0, 1):
+        assert res[r][2] == [0, 1, 2]
+        assert res[r][1] == [r * 100 + k for k in range(3)]
+    # both ranks report the same elapsed time: the slowest rank's (3 x 40 ms)
+    assert res[0][0] == res[1][0]
+    assert res[0][0] >= 3 * 0.04 - 1e-3
+    # replicas: the ranks' workloads are independent (different boxes)
+    assert res[0][3].shape == res[1][3].shape
+    assert not np.array_equal(res[0][3], res[1][3])
+
+
+def test_timed_region_single_process():
+    sys.path.insert(0, REPO)
+    import bench
+    el, out = bench.timed_region(lambda k: k * k, 4, None, lambda: None, torch.device("cpu"))
+    assert out == [0, 1, 4, 9] and el >= 0.0
+
+
+def test_scene_shapes_and_bounds():
+    sys.path.insert(0, REPO)
+    import bench
+    sc = bench.make_scenes(torch.device("cpu"), 3, 16, 5, seed=7, C=4, H=8)
+    rois = sc["np"]["rois"]
+    assert rois.shape == (5, 48, 5)
+    assert set(np.unique(rois[..., 0]).astype(int)) == {0, 1, 2}
+    w = rois[..., 3] - rois[..., 1]
+    h = rois[..., 4] - rois[..., 2]
+    assert (w > 20).all() and (w < 340).all() and (h > 20).all() and (h < 340).all()
+    # every frame's detections are a permutation of the stream's objects
+    for f in range(5):
+        for s in range(3):
+            assert sorted(sc["obj"][f, s]) == list(range(16))
