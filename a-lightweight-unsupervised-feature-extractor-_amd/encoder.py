@@ -167,10 +167,10 @@ class Model(nn.Module):
         Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
         xr = torch.addmm(W["br"], Y2[:, :h2], W["w2r"]).view(N, ss, C)   # DSC reinforce (BN folded)
         xn = torch.addmm(W["bn"], Y2[:, h2:], W["w2n"]).view(N, ss, C)   # DSC normal (BN folded)
-        m_r = act_mean(xr, "silu")                                   # SiLU + SE squeeze
+        m_r = act_mean(xr, "silu", write=False)                      # SE squeeze of SiLU(xr), no write-back
         m_n = act_mean(xn, "hardswish")                              # Hardswish + its GAP
         s = self._se(m_r)
-        scale_rows(xr, s)                                            # x_f * s
+        scale_rows(xr, s, act="silu")                                # x_f * s = SiLU(xr) * s, one pass
         T = torch.addmm(W["bt"], xr.view(N * ss, C), W["wt1"])
         T.addmm_(xn.view(N * ss, C), W["wt2"])                       # transition over cat[x_f*s, x_n]
         m_cat = act_mean(T.view(N, ss, C), "silu", write=False)      # SiLU + GAP, no write-back

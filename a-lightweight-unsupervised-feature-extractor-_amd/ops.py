@@ -73,12 +73,16 @@ def act_mean(x: torch.Tensor, act: Optional[str], *, inplace: bool = True,
     return mean
 
 
-def scale_rows(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
-    """x [N, P, C] *= s[N, C] in place."""
+def scale_rows(x: torch.Tensor, s: torch.Tensor, act: Optional[str] = None) -> torch.Tensor:
+    """x [N, P, C] = act(x) * s[N, C] in place (act None: plain scale)."""
     _need_gpu(x, "scale_rows")
     N, P, C = x.shape
     s = s.to(torch.float32).contiguous()
-    check(lib().trk_scale_rows(_ptr(x), _ptr(s), N, P, C, _edt(x), _stream(x.device)), "scale_rows")
+    if act is None:
+        check(lib().trk_scale_rows(_ptr(x), _ptr(s), N, P, C, _edt(x), _stream(x.device)), "scale_rows")
+    else:
+        check(lib().trk_act_scale_rows(_ptr(x), _ptr(s), N, P, C, _ACT[act], _edt(x), _stream(x.device)),
+              "act_scale_rows")
     return x
 
 

@@ -41,7 +41,8 @@ const char* trk_last_error(void);
 /* Performance knobs (process-global; results are bit-identical for every value):
  *   "roi_window_kb"  LDS budget (KiB) for staging a ROI's source window; 0 = never stage
  *   "roi_vec"        channels per lane in roi_align (0 = auto, 1, 2, 4)
- *   "roi_sweep"      1 (default): NHWC output through the row-sweep kernel; 0: per-sample taps */
+ *   "roi_sweep"      1 (default): NHWC output through the row-sweep kernel; 0: per-sample taps
+ *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel */
 int trk_set_tuning(const char* key, int value);
 
 /* ------------------------------------------------------------------------
@@ -151,6 +152,11 @@ int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, in
                  int act, int dtype, void* stream);
 /* x[n, p, c] *= s[n, c] in place (SE excitation, card.py:78). */
 int trk_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int dtype, void* stream);
+/* x[n,p,c] = act(x[n,p,c]) * s[n,c] in place (act as trk_act_mean): the SE
+ * excitation applied to the activated DSC output without a separate
+ * activation write-back (card.py:53-56 + :78). */
+int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int act, int dtype,
+                       void* stream);
 
 /* ------------------------------------------------------------------------
  * Device-resident track state.  Track slots of all

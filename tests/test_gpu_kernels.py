@@ -340,6 +340,20 @@ def test_dwconv5_vs_torch_fp32(trk, gpu, S, dtype):
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w, padding=2, groups=1024).permute(0, 2, 3, 1)
     tol = 2e-5 if dtype == torch.float32 else 1e-2
     assert (got - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item())
+    # the fast row-pair kernel and the generic kernel accumulate in the same order: identical
+    L = trk.lib()
+    try:
+        L.trk_set_tuning(b"dw_fast", 0)
+        gen = ops.dwconv5_nhwc(x, w).float()
+    finally:
+        L.trk_set_tuning(b"dw_fast", 1)
+    assert torch.equal(got, gen)
+    # ragged / odd shapes take the generic kernel (C % 128 != 0, non-square)
+    x2 = torch.randn(5, 6, 9, 196, generator=g).to(gpu, dtype)
+    w2 = (torch.randn(196, 1, 5, 5, generator=g) / 5).to(gpu)
+    got2 = ops.dwconv5_nhwc(x2, w2).float()
+    ref2 = F.conv2d(x2.float().permute(0, 3, 1, 2), w2, padding=2, groups=196).permute(0, 2, 3, 1)
+    assert (got2 - ref2).abs().max().item() <= tol * max(1.0, ref2.abs().max().item())
 
 
 @pytest.mark.parametrize("act", ["silu", "hardswish", None])
@@ -359,3 +373,11 @@ def test_act_mean_and_scale_rows(trk, gpu, act):
     y0 = y.clone()
     ops.scale_rows(y, s)
     assert torch.equal(y, y0 * s[:, None, :])
+    # fused act + scale == act (as act_mean writes it) then scale, bit for bit
+    z = x.clone()
+    ops.scale_rows(z, s, act=act)
+    assert torch.equal(z, y)
+    # mean without write-back leaves x untouched and equals the written mean
+    x2 = x.clone()
+    m2 = ops.act_mean(x2, act, write=False)
+    assert torch.equal(x2, x) and torch.equal(m2, m)

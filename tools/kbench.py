@@ -25,6 +25,7 @@ def timeit(fn, reps=20, rounds=1):
 
 def main():
     rng = np.random.default_rng(0)
+    mode = sys.argv[1] if len(sys.argv) > 1 else "all"
     B, C, H, N, S = 8, 512, 40, 256, 10
     feat = torch.from_numpy((lambda x: x / (1 + np.exp(-x)))(rng.standard_normal((B, C, H, H)).astype(np.float32))).to(dev)
     w = rng.uniform(32, 320, B * N); h = rng.uniform(32, 320, B * N)
@@ -35,7 +36,7 @@ def main():
     K = B * N
     algo = B * C * H * H * 4 + K * C * S * S * 2 + K * 20
     res = {}
-    variants = [(1, 0, 0), (2, 0, 0), (0, 0, 4)]
+    variants = [(1, 0, 0), (2, 0, 0), (0, 0, 4)] if mode in ("all", "roi") else []
     for rnd in range(3):
         for sw, wk, vec in variants:
             L.set_tuning("roi_sweep", sw); L.set_tuning("roi_window_kb", wk); L.set_tuning("roi_vec", vec)
@@ -49,9 +50,10 @@ def main():
                 print(json.dumps({"item": "roi_align_nhwc_in", "sweep": sw, "window_kb": wk, "vec": vec, "us": round(tm, 1),
                                   "GBps": round(algo / tm / 1e3, 1), "bitexact": ok}), flush=True)
     L.set_tuning("roi_sweep", 1); L.set_tuning("roi_window_kb", 0); L.set_tuning("roi_vec", 0)
-    t = timeit(lambda: trk.roi_align(feat, rois, (S, S), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True))
-    print(json.dumps({"item": "roi_align_nchw_in(default)", "us": round(t, 1)}), flush=True)
-    if len(sys.argv) > 1 and sys.argv[1] == "roi":
+    if mode in ("all", "roi"):
+        t = timeit(lambda: trk.roi_align(feat, rois, (S, S), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True))
+        print(json.dumps({"item": "roi_align_nchw_in(default)", "us": round(t, 1)}), flush=True)
+    if mode == "roi":
         return
     # encoder pieces
     y1t = torch.randn(K, S, S, 1024, device=dev).bfloat16()
@@ -64,6 +66,19 @@ def main():
     s_ = torch.rand(K, 512, device=dev)
     t = timeit(lambda: ops.scale_rows(xr, s_))
     print(json.dumps({"item": "scale_rows_bf16", "us": round(t, 1), "GBps": round(2 * xr.numel() * 2 / t / 1e3, 1)}), flush=True)
+    # whole encoder forward at the bench shape (bf16, NHWC ROI input)
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import gen_common as G
+    model = trk.Model(512, 512, 10, 128).eval()
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}, strict=True)
+    model = model.to(dev)
+    roi = ref
+    with torch.no_grad():
+        t = timeit(lambda: model(roi), reps=10)
+    print(json.dumps({"item": "encoder_bf16_2048rois", "us": round(t, 1),
+                      "TFLOPs": round(K * 320.61e6 / t / 1e6, 1)}), flush=True)
+    if mode == "enc":
+        return
     # LSAP: tracking-like (near-identity, gated) and uniform random, 8 frames of 256x256
     F = 8
     Ct = np.full((F, 256, 256), 1e9, np.float32)
