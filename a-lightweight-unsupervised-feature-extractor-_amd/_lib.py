@@ -58,12 +58,16 @@ def _declare(L):
     L.trk_lsap.restype = i32
     L.trk_dwconv5_nhwc.argtypes = [P, P, P, i64, i64, i64, i64, i32, P]
     L.trk_dwconv5_nhwc.restype = i32
-    L.trk_act_mean.argtypes = [P, P, P, i64, i64, i64, i32, i32, P]
+    L.trk_act_mean.argtypes = [P, P, P, i64, i64, i64, i64, i32, i32, P]
     L.trk_act_mean.restype = i32
     L.trk_scale_rows.argtypes = [P, P, i64, i64, i64, i32, P]
     L.trk_scale_rows.restype = i32
-    L.trk_act_scale_rows.argtypes = [P, P, i64, i64, i64, i32, i32, P]
+    L.trk_act_scale_rows.argtypes = [P, P, i64, i64, i64, i64, i32, i32, P]
     L.trk_act_scale_rows.restype = i32
+    L.trk_enc_dsc_gemm.argtypes = [P, i64, i64, i64, P, P, i64, P, P, P]
+    L.trk_enc_dsc_gemm.restype = i32
+    L.trk_enc_transition_gemm.argtypes = [P, i64, i64, i64, P, i64, P, P, i64, P, P]
+    L.trk_enc_transition_gemm.restype = i32
     L.trk_kf_predict.argtypes = [i64, P, P, P, P, P, P, P]
     L.trk_kf_predict.restype = i32
     L.trk_track_update.argtypes = [i64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, i64, f32, f32,

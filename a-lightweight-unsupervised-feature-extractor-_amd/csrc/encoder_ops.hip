@@ -311,7 +311,8 @@ constexpr int kAmUnroll = 5;
 
 template <typename T>
 __global__ void __launch_bounds__(256)
-act_mean_kernel(const T* __restrict__ x, T* out, float* __restrict__ mean, int N, int P, int C, int act) {
+act_mean_kernel(const T* __restrict__ x, T* out, float* __restrict__ mean, int N, int P, int C, int ld,
+                int act) {
   using V = Vec16<T>;
   constexpr int E = V::kN;
   __shared__ float red[256 * 8];
@@ -323,14 +324,14 @@ act_mean_kernel(const T* __restrict__ x, T* out, float* __restrict__ mean, int N
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = 0.f;
   if (g < groups) {
-    const T* src = x + (int64_t)n * P * C + v * E;
-    T* dst = out ? out + (int64_t)n * P * C + v * E : nullptr;
+    const T* src = x + (int64_t)n * P * ld + v * E;
+    T* dst = out ? out + (int64_t)n * P * ld + v * E : nullptr;
     for (int p0 = g; p0 < P; p0 += groups * kAmUnroll) {
       uint4 raw[kAmUnroll];
 #pragma unroll
       for (int u = 0; u < kAmUnroll; ++u) {
         const int p = p0 + u * groups;
-        raw[u] = p < P ? *reinterpret_cast<const uint4*>(src + (int64_t)p * C) : make_uint4(0, 0, 0, 0);
+        raw[u] = p < P ? *reinterpret_cast<const uint4*>(src + (int64_t)p * ld) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < kAmUnroll; ++u) {
@@ -343,7 +344,7 @@ act_mean_kernel(const T* __restrict__ x, T* out, float* __restrict__ mean, int N
           f[e] = act_apply(f[e], act);
           acc[e] += f[e];
         }
-        if (dst) *reinterpret_cast<uint4*>(dst + (int64_t)p * C) = V::pack(f);
+        if (dst) *reinterpret_cast<uint4*>(dst + (int64_t)p * ld) = V::pack(f);
       }
     }
   }
@@ -364,15 +365,17 @@ act_mean_kernel(const T* __restrict__ x, T* out, float* __restrict__ mean, int N
 // one 16-B vector per thread (C % (16 / sizeof(T)) == 0), else channel pairs
 template <typename T>
 __global__ void __launch_bounds__(256)
-scale_rows_kernel(T* __restrict__ x, const float* __restrict__ s, int64_t total_vec, int P, int C, int act) {
+scale_rows_kernel(T* __restrict__ x, const float* __restrict__ s, int64_t total_vec, int P, int C, int ld,
+                  int act) {
   using V = Vec16<T>;
   constexpr int E = V::kN;
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= total_vec) return;
   const int64_t e0 = q * E;
   const int c = (int)(e0 % C);
-  const int64_t n = e0 / ((int64_t)P * C);
-  uint4* px = reinterpret_cast<uint4*>(x + e0);
+  const int64_t row = e0 / C;             // pixel row over all ROIs
+  const int64_t n = row / P;
+  uint4* px = reinterpret_cast<uint4*>(x + row * ld + c);
   float f[E];
   V::unpack(*px, f);
   const float4* sp = reinterpret_cast<const float4*>(s + n * C + c);  // 16-B aligned: c % E == 0
@@ -466,27 +469,30 @@ extern "C" int trk_dwconv5_nhwc(const void* in, const float* weight, void* out, 
   return trk::check_launch("dwconv5_nhwc_kernel");
 }
 
-extern "C" int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, int64_t C,
+extern "C" int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, int64_t C, int64_t ld,
                             int act, int dtype, void* stream) {
   TRK_REQUIRE(dtype == TRK_F32 || dtype == TRK_BF16, "act_mean: dtype must be f32 or bf16");
   const int E = dtype == TRK_F32 ? 4 : 8;
   TRK_REQUIRE(N >= 0 && P >= 1 && C >= E && C % E == 0 && C / E <= 256,
               "act_mean: C must be a multiple of %d and at most %d", E, 256 * E);
+  TRK_REQUIRE(ld >= C && ld % E == 0, "act_mean: row stride ld must be >= C and a multiple of %d", E);
   TRK_REQUIRE(act >= 0 && act <= 2, "act_mean: act must be 0 (none), 1 (SiLU) or 2 (Hardswish)");
   if (N == 0) return TRK_OK;
   TRK_REQUIRE(x && mean, "act_mean: null pointer");
+  TRK_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0),
+              "act_mean: x/out must be 16-B aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == TRK_F32)
     hipLaunchKernelGGL(act_mean_kernel<float>, dim3((unsigned)N), dim3(256), 0, st, (const float*)x, (float*)out,
-                       mean, (int)N, (int)P, (int)C, act);
+                       mean, (int)N, (int)P, (int)C, (int)ld, act);
   else
     hipLaunchKernelGGL(act_mean_kernel<uint16_t>, dim3((unsigned)N), dim3(256), 0, st, (const uint16_t*)x,
-                       (uint16_t*)out, mean, (int)N, (int)P, (int)C, act);
+                       (uint16_t*)out, mean, (int)N, (int)P, (int)C, (int)ld, act);
   return trk::check_launch("act_mean_kernel");
 }
 
-static int scale_rows_impl(void* x, const float* s, int64_t N, int64_t P, int64_t C, int act, int dtype,
-                           void* stream, const char* what) {
+static int scale_rows_impl(void* x, const float* s, int64_t N, int64_t P, int64_t C, int64_t ld, int act,
+                           int dtype, void* stream, const char* what) {
   TRK_REQUIRE(dtype == TRK_F32 || dtype == TRK_BF16, "%s: dtype must be f32 or bf16", what);
   TRK_REQUIRE(N >= 0 && P >= 1 && C >= 2 && C % 2 == 0, "%s: bad shape", what);
   TRK_REQUIRE(act >= 0 && act <= 2, "%s: act must be 0 (none), 1 (SiLU) or 2 (Hardswish)", what);
@@ -494,15 +500,19 @@ static int scale_rows_impl(void* x, const float* s, int64_t N, int64_t P, int64_
   TRK_REQUIRE(x && s, "%s: null pointer", what);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int E = dtype == TRK_F32 ? 4 : 8;
-  if (C % E == 0) {
+  TRK_REQUIRE(ld == C || (C % E == 0 && ld % E == 0 && ld > C), "%s: row stride ld must equal C or be a "
+              "multiple of %d", what, E);
+  if (C % E == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0) {
     const int64_t nv = N * P * C / E;
     const unsigned g = (unsigned)((nv + 255) / 256);
     if (dtype == TRK_F32)
-      hipLaunchKernelGGL(scale_rows_kernel<float>, dim3(g), dim3(256), 0, st, (float*)x, s, nv, (int)P, (int)C, act);
+      hipLaunchKernelGGL(scale_rows_kernel<float>, dim3(g), dim3(256), 0, st, (float*)x, s, nv, (int)P, (int)C,
+                         (int)ld, act);
     else
       hipLaunchKernelGGL(scale_rows_kernel<uint16_t>, dim3(g), dim3(256), 0, st, (uint16_t*)x, s, nv, (int)P,
-                         (int)C, act);
+                         (int)C, (int)ld, act);
   } else {
+    TRK_REQUIRE(ld == C, "%s: a row stride needs C %% %d == 0 and 16-B alignment", what, E);
     const int64_t pairs = N * P * C / 2;
     const unsigned g = (unsigned)((pairs + 255) / 256);
     if (dtype == TRK_F32)
@@ -517,10 +527,10 @@ static int scale_rows_impl(void* x, const float* s, int64_t N, int64_t P, int64_
 
 extern "C" int trk_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int dtype,
                               void* stream) {
-  return scale_rows_impl(x, s, N, P, C, 0, dtype, stream, "scale_rows");
+  return scale_rows_impl(x, s, N, P, C, C, 0, dtype, stream, "scale_rows");
 }
 
-extern "C" int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int act, int dtype,
-                                  void* stream) {
-  return scale_rows_impl(x, s, N, P, C, act, dtype, stream, "act_scale_rows");
+extern "C" int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int64_t ld, int act,
+                                  int dtype, void* stream) {
+  return scale_rows_impl(x, s, N, P, C, ld, act, dtype, stream, "act_scale_rows");
 }

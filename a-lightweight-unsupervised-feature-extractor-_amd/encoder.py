@@ -125,6 +125,18 @@ class Model(nn.Module):
             C = wt.shape[0]
             w["wt1"] = wt[:, :C].t().contiguous().to(device, dtype)
             w["wt2"] = wt[:, C:].t().contiguous().to(device, dtype)
+            w["wt"] = wt.t().contiguous().to(device, dtype)                          # [2C, C]: K = [x_f*s | x_n]
+            # fused bf16 GEMM operands ([N][K] = the conv weight's own [out, in] layout)
+            w2nk = []
+            for dsc in (dr, dn):
+                bn = dsc.bn
+                scale = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+                w2 = torch.cat([dsc.depth[2].weight.flatten(1), dsc.point[2].weight.flatten(1)], 1).float()
+                w2nk.append(w2 * scale[:, None])                                     # [C, 2h]
+            w["w2_nk"] = torch.stack(w2nk, 0).contiguous().to(device, torch.bfloat16)  # [2, C, 2h]
+            w["b2"] = torch.cat([w["br"].float(), w["bn"].float()]).to(device, torch.float32)
+            w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
+            w["bt_f"] = r.transition[0].bias.float().to(device)
             w["bt"] = r.transition[0].bias.to(device, dtype)
         self._fused, self._fused_key = w, key
         return w
@@ -153,9 +165,13 @@ class Model(nn.Module):
         return F.hardsigmoid(F.linear(F.relu(F.linear(m_r, se[0].weight.float(), se[0].bias.float())),
                                       se[2].weight.float(), se[2].bias.float()))
 
+    # bf16 inputs take the fused trk GEMMs (enc_gemm.hip) when the shapes allow;
+    # fp32 (the parity path) keeps hipBLASLt GEMMs + the separate act/mean passes
+    fused_gemm = True
+
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
-        """GEMMs on hipBLASLt (torch), everything else in trk HIP kernels."""
-        from .ops import act_mean, dwconv5_nhwc, scale_rows
+        """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
+        from .ops import act_mean, dwconv5_nhwc, scale_rows, enc_dsc_gemm, enc_transition_gemm
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -165,15 +181,28 @@ class Model(nn.Module):
         X = x.permute(0, 2, 3, 1).reshape(N * ss, C)                 # view when channels_last
         Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)                      # 4 first 1x1 convs, one GEMM
         Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
-        xr = torch.addmm(W["br"], Y2[:, :h2], W["w2r"]).view(N, ss, C)   # DSC reinforce (BN folded)
-        xn = torch.addmm(W["bn"], Y2[:, h2:], W["w2n"]).view(N, ss, C)   # DSC normal (BN folded)
+        Co = W["w2r"].shape[1]
+        if (self.fused_gemm and dt == torch.bfloat16 and ss >= 32 and h2 % 32 == 0 and Co % 128 == 0):
+            # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
+            # + SiLU + GAP in another: the [M, 512] intermediates are written once (x_r|x_n)
+            XRN, sum_r, sum_n = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"])
+            m_r, m_n = sum_r / ss, sum_n / ss
+            s = self._se(m_r)
+            m_cat = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"]) / ss
+            a = self._alpha()
+            g = 0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n)
+            return self._head(g)
+        XRN = torch.empty((N * ss, 2 * Co), device=dev, dtype=dt)    # [x_r | x_n] rows: the transition's K
+        torch.addmm(W["br"], Y2[:, :h2], W["w2r"], out=XRN[:, :Co])  # DSC reinforce (BN folded)
+        torch.addmm(W["bn"], Y2[:, h2:], W["w2n"], out=XRN[:, Co:])  # DSC normal (BN folded)
+        XR = XRN.view(N, ss, 2 * Co)
+        xr, xn = XR[:, :, :Co], XR[:, :, Co:]
         m_r = act_mean(xr, "silu", write=False)                      # SE squeeze of SiLU(xr), no write-back
-        m_n = act_mean(xn, "hardswish")                              # Hardswish + its GAP
+        m_n = act_mean(xn, "hardswish")                              # Hardswish + its GAP, in place
         s = self._se(m_r)
-        scale_rows(xr, s, act="silu")                                # x_f * s = SiLU(xr) * s, one pass
-        T = torch.addmm(W["bt"], xr.view(N * ss, C), W["wt1"])
-        T.addmm_(xn.view(N * ss, C), W["wt2"])                       # transition over cat[x_f*s, x_n]
-        m_cat = act_mean(T.view(N, ss, C), "silu", write=False)      # SiLU + GAP, no write-back
+        scale_rows(xr, s, act="silu")                                # x_f * s = SiLU(xr) * s, in place
+        T = torch.addmm(W["bt"], XRN, W["wt"])                       # transition over cat[x_f*s, x_n], K = 2C
+        m_cat = act_mean(T.view(N, ss, Co), "silu", write=False)     # SiLU + GAP, no write-back
         a = self._alpha()
         g = 0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n)     # Shake2 eval :94-96 + GAP
         return self._head(g)

@@ -61,29 +61,87 @@ def dwconv5_nhwc(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _rows_view(x: torch.Tensor, name: str):
+    """x [N, P, C] whose rows (dims 0-1 flattened) have unit channel stride and a
+    common row stride ld >= C (a column block of a wider buffer is allowed)."""
+    _need_gpu(x, name)
+    if x.dim() != 3 or x.stride(2) != 1 or x.stride(0) != x.shape[1] * x.stride(1):
+        raise ValueError(f"{name}: x must be [N, P, C] with unit channel stride and uniform row stride")
+    return x.shape[0], x.shape[1], x.shape[2], x.stride(1)
+
+
 def act_mean(x: torch.Tensor, act: Optional[str], *, inplace: bool = True,
              write: bool = True) -> torch.Tensor:
-    """x [N, P, C] contiguous: x <- act(x) (if write), returns mean over P (f32 [N, C])."""
-    _need_gpu(x, "act_mean")
-    N, P, C = x.shape
+    """x [N, P, C] (row stride may exceed C): x <- act(x) (if write), returns
+    mean over P (f32 [N, C])."""
+    N, P, C, ld = _rows_view(x, "act_mean")
     mean = torch.empty((N, C), device=x.device, dtype=torch.float32)
-    out = (x if inplace else torch.empty_like(x)) if write else None
-    check(lib().trk_act_mean(_ptr(x), _ptr(out), _ptr(mean), N, P, C, _ACT[act], _edt(x),
+    if write and not inplace:
+        out = torch.empty_like(x.contiguous())
+        if ld != C:
+            raise ValueError("act_mean: a strided x needs inplace=True")
+    else:
+        out = x if write else None
+    check(lib().trk_act_mean(_ptr(x), _ptr(out), _ptr(mean), N, P, C, ld, _ACT[act], _edt(x),
                              _stream(x.device)), "act_mean")
     return mean
 
 
 def scale_rows(x: torch.Tensor, s: torch.Tensor, act: Optional[str] = None) -> torch.Tensor:
-    """x [N, P, C] = act(x) * s[N, C] in place (act None: plain scale)."""
-    _need_gpu(x, "scale_rows")
-    N, P, C = x.shape
+    """x [N, P, C] = act(x) * s[N, C] in place (act None: plain scale; row stride may exceed C)."""
+    N, P, C, ld = _rows_view(x, "scale_rows")
     s = s.to(torch.float32).contiguous()
-    if act is None:
+    if act is None and ld == C:
         check(lib().trk_scale_rows(_ptr(x), _ptr(s), N, P, C, _edt(x), _stream(x.device)), "scale_rows")
     else:
-        check(lib().trk_act_scale_rows(_ptr(x), _ptr(s), N, P, C, _ACT[act], _edt(x), _stream(x.device)),
+        check(lib().trk_act_scale_rows(_ptr(x), _ptr(s), N, P, C, ld, _ACT[act], _edt(x), _stream(x.device)),
               "act_scale_rows")
     return x
+
+
+_FIX = 2.0 ** -24
+
+
+def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor):
+    """Both DSC 1x1 GEMMs (bf16): Y2 [M, 2*Kg], W2 [2, Ng, Kg], bias [2*Ng] f32 ->
+    (XRN [M, 2*Ng] = [x_r | Hardswish(x_n)], sum_silu_r [R, Ng] f32, sum_hsw_n [R, Ng] f32)
+    with R = ceil(M / P) ROIs (sums over each ROI's P rows)."""
+    _need_gpu(Y2, "enc_dsc_gemm")
+    if Y2.dtype != torch.bfloat16 or W2.dtype != torch.bfloat16:
+        raise TypeError("enc_dsc_gemm: bf16 operands required")
+    M, K2 = Y2.shape
+    G, Ng, Kg = W2.shape
+    if G != 2 or K2 != 2 * Kg or bias.numel() != 2 * Ng:
+        raise ValueError("enc_dsc_gemm: shape mismatch")
+    Y2, W2, bias = Y2.contiguous(), W2.contiguous(), bias.to(torch.float32).contiguous()
+    R = (M + P - 1) // P
+    XRN = torch.empty((M, 2 * Ng), device=Y2.device, dtype=torch.bfloat16)
+    sums = torch.empty((R, 2 * Ng), device=Y2.device, dtype=torch.int64)
+    check(lib().trk_enc_dsc_gemm(_ptr(Y2), M, P, Kg, _ptr(W2), _ptr(bias), Ng, _ptr(XRN), _ptr(sums),
+                                 _stream(Y2.device)), "enc_dsc_gemm")
+    f = (sums.double() * _FIX).float()
+    return XRN, f[:, :Ng], f[:, Ng:]
+
+
+def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
+                        bias: torch.Tensor) -> torch.Tensor:
+    """sum over each ROI's P rows of SiLU([SiLU(x_r) * s | x_n] . Wt^T + bias):
+    XRN [M, K] bf16 (x_r = first kscale = s.shape[1] columns), s [R, kscale]
+    f32, Wt [N, K] bf16 -> [R, N] f32."""
+    _need_gpu(XRN, "enc_transition_gemm")
+    if XRN.dtype != torch.bfloat16 or Wt.dtype != torch.bfloat16:
+        raise TypeError("enc_transition_gemm: bf16 operands required")
+    M, K = XRN.shape
+    N, K2 = Wt.shape
+    R = (M + P - 1) // P
+    if K2 != K or s.shape[0] != R or bias.numel() != N:
+        raise ValueError("enc_transition_gemm: shape mismatch")
+    XRN, Wt = XRN.contiguous(), Wt.contiguous()
+    s, bias = s.to(torch.float32).contiguous(), bias.to(torch.float32).contiguous()
+    sums = torch.empty((R, N), device=XRN.device, dtype=torch.int64)
+    check(lib().trk_enc_transition_gemm(_ptr(XRN), M, P, K, _ptr(s), s.shape[1], _ptr(Wt), _ptr(bias), N,
+                                        _ptr(sums), _stream(XRN.device)), "enc_transition_gemm")
+    return (sums.double() * _FIX).float()
 
 
 # ------------------------------------------------------------- ROI Align --

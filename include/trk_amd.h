@@ -147,16 +147,40 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
 int trk_dwconv5_nhwc(const void* in, const float* weight, void* out, int64_t N, int64_t H,
                      int64_t W, int64_t C, int dtype, void* stream);
 /* y = act(x) (act 0 none, 1 SiLU, 2 Hardswish), written to out (may equal x,
- * may be NULL); mean [N, C] f32 = mean over the P pixels of y. */
-int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, int64_t C,
+ * may be NULL); mean [N, C] f32 = mean over the P pixels of y.  x / out are
+ * [N*P] rows of C channels with row stride ld (>= C; a column block of a wider
+ * row-major buffer when ld > C). */
+int trk_act_mean(const void* x, void* out, float* mean, int64_t N, int64_t P, int64_t C, int64_t ld,
                  int act, int dtype, void* stream);
 /* x[n, p, c] *= s[n, c] in place (SE excitation, card.py:78). */
 int trk_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int dtype, void* stream);
 /* x[n,p,c] = act(x[n,p,c]) * s[n,c] in place (act as trk_act_mean): the SE
  * excitation applied to the activated DSC output without a separate
  * activation write-back (card.py:53-56 + :78). */
-int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int act, int dtype,
-                       void* stream);
+int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C, int64_t ld, int act,
+                       int dtype, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused bf16 encoder GEMMs (RMB of reference card.py:48-148).  A rows are
+ * bf16 [M, *] with M = ROIs x P pixels; weights bf16 [N][K] (conv [out, in]).
+ * Per-ROI column sums are int64 fixed point (value x 2^24), zeroed by the
+ * call and accumulated exactly (order-independent).  Requires P >= 32,
+ * K % 32 == 0, N % 128 == 0.
+ *
+ * trk_enc_dsc_gemm: both DSC 1x1 GEMMs (card.py:53-56, depth.2 + point.2 with
+ *   eval-BN folded): Y2 [M, 2*Kg] (reinforce half | normal half), W2
+ *   [2][Ng][Kg], bias [2*Ng] -> XRN [M, 2*Ng] = [x_r (pre-activation) |
+ *   Hardswish(x_n)], sums [ROIs][2*Ng] = per-ROI sums of SiLU(x_r) (SE squeeze,
+ *   card.py:75) and Hardswish(x_n) (GAP).
+ * trk_enc_transition_gemm: T = [SiLU(x_r) * s | x_n] . Wt^T + bias
+ *   (card.py:78 + :138-139), the SiLU(x_r) * s[roi] scaling applied to the
+ *   first kscale columns of XRN while staging; only the per-ROI sums of
+ *   SiLU(T) are produced (sums [ROIs][N]); T is never stored.
+ * ---------------------------------------------------------------------- */
+int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2, const float* bias,
+                     int64_t Ng, void* XRN, long long* sums, void* stream);
+int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
+                            const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
 
 /* ------------------------------------------------------------------------
  * Device-resident track state.  Track slots of all

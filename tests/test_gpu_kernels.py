@@ -323,6 +323,59 @@ def test_encoder_gpu_vs_reference_golden(trk, gpu, s):
     exp = d[f"z_s{s}"]
     assert np.max(np.abs(z - exp)) <= 1e-4
     assert (zb * exp).sum(1).min() >= 0.999
+    # bf16: fused trk GEMMs vs the hipBLASLt + separate-pass graph (same bf16 rounding points
+    # except the means, which the fused epilogues take in f32 before rounding)
+    try:
+        m.fused_gemm = False
+        with torch.no_grad():
+            zu = m(x.bfloat16().contiguous(memory_format=torch.channels_last)).float().cpu().numpy()
+    finally:
+        m.fused_gemm = True
+    assert (zb * zu).sum(1).min() >= 0.9999
+
+
+def _bf16_ref_rows(Y2, W2, b2):
+    """fp32 reference of the DSC pair on bf16 operands"""
+    Kg = W2.shape[2]
+    xr = Y2[:, :Kg].float() @ W2[0].float().t() + b2[:W2.shape[1]]
+    xn = Y2[:, Kg:].float() @ W2[1].float().t() + b2[W2.shape[1]:]
+    return xr, xn
+
+
+@pytest.mark.parametrize("P,R", [(100, 37), (49, 29)])
+def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
+    """trk_enc_dsc_gemm / trk_enc_transition_gemm vs a torch fp32 reference on the same
+    bf16 operands (tol: bf16 output rounding for stored values; 2e-3 relative for sums).
+    M = R*P is not a multiple of the 128-row tile and ROIs straddle tiles."""
+    import torch.nn.functional as F
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(P)
+    M, Kg, Ng = R * P, 512, 512
+    Y2 = torch.randn(M, 2 * Kg, generator=g).to(gpu).bfloat16()
+    W2 = (torch.randn(2, Ng, Kg, generator=g) / 24).to(gpu).bfloat16()
+    b2 = (torch.randn(2 * Ng, generator=g) / 4).to(gpu)
+    XRN, sr, sn = ops.enc_dsc_gemm(Y2, P, W2, b2)
+    xr, xn = _bf16_ref_rows(Y2, W2, b2)
+    hn = F.hardswish(xn)
+    assert (XRN[:, :Ng].float() - xr).abs().max().item() <= 1e-2 * max(1.0, xr.abs().max().item())
+    assert (XRN[:, Ng:].float() - hn).abs().max().item() <= 1e-2 * max(1.0, hn.abs().max().item())
+    ref_sr = F.silu(xr).view(R, P, Ng).sum(1)
+    ref_sn = hn.view(R, P, Ng).sum(1)
+    assert (sr - ref_sr).abs().max().item() <= 2e-3 * ref_sr.abs().max().item()
+    assert (sn - ref_sn).abs().max().item() <= 2e-3 * ref_sn.abs().max().item()
+    # deterministic: a second run gives the same bits
+    XRN2, sr2, sn2 = ops.enc_dsc_gemm(Y2, P, W2, b2)
+    assert torch.equal(XRN, XRN2) and torch.equal(sr, sr2) and torch.equal(sn, sn2)
+    # transition with the SE scale applied in the prologue
+    s = torch.rand(R, Ng, generator=g).to(gpu)
+    Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
+    bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
+    st = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+    xs = (F.silu(XRN[:, :Ng].float()).view(R, P, Ng) * s[:, None, :]).bfloat16().float().view(M, Ng)
+    A = torch.cat([xs, XRN[:, Ng:].float()], 1)
+    ref_t = F.silu(A @ Wt.float().t() + bt).view(R, P, Ng).sum(1)
+    assert (st - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item()
 
 
 # ----------------------------------------------------- encoder helpers ----
@@ -381,3 +434,13 @@ def test_act_mean_and_scale_rows(trk, gpu, act):
     x2 = x.clone()
     m2 = ops.act_mean(x2, act, write=False)
     assert torch.equal(x2, x) and torch.equal(m2, m)
+    # a column block of a wider buffer (row stride 1024): only that block changes
+    wide = torch.randn(19, 100, 1024, generator=g).to(gpu)
+    wide[:, :, 256:768] = x
+    w0 = wide.clone()
+    blk = wide[:, :, 256:768]
+    m3 = ops.act_mean(blk, act)
+    assert torch.equal(m3, m) and torch.equal(blk, y0)
+    ops.scale_rows(blk, s, act=None)
+    assert torch.equal(blk, y) and torch.equal(wide[:, :, :256], w0[:, :, :256])
+    assert torch.equal(wide[:, :, 768:], w0[:, :, 768:])
