@@ -196,7 +196,11 @@ class MultiStreamTracker:
     # --------------------------------------------------------------- step --
     def step(self, det_emb: torch.Tensor, dbox: torch.Tensor, dconf: torch.Tensor,
              N: Sequence[int], confs_host: Sequence[Sequence[float]],
-             frame_ids: Optional[Sequence[int]] = None) -> List[FrameResult]:
+             frame_ids: Optional[Sequence[int]] = None,
+             after_launch: Optional[Any] = None) -> List[FrameResult]:
+        """after_launch: optional callable run once the stage-1 LSAP is enqueued and
+        before the host waits for its indices -- e.g. to enqueue the next frame's
+        ROI Align + encoder on another stream while the solver runs."""
         cfg = self.cfg
         S = self.n_streams
         if det_emb.dim() != 3 or det_emb.shape[0] != S or det_emb.shape[2] != D:
@@ -245,6 +249,9 @@ class MultiStreamTracker:
                             params=self.params, gmean=t.gmean, gsinv=t.gsinv, gate_on=t.gate_on,
                             row_slot=self._i32(row_slot))["C_total"]
             lres = lsap_batched(C1, Ms, Ns, cost_max=float(cfg["cost_max"]))
+            if after_launch is not None:
+                after_launch()
+                after_launch = None
             st_h = lres["status"].cpu().numpy()
             assign = lres["assign"].cpu().numpy()  # the host sync of mainTracking.py:503
             for s in active:
@@ -260,6 +267,9 @@ class MultiStreamTracker:
                 taken = np.zeros(int(N[s]), bool)
                 taken[a[rows]] = True
                 unmatched_dets[s] = np.flatnonzero(~taken)
+
+        if after_launch is not None:  # no stage-1 rows this frame
+            after_launch()
 
         # stage-1 state updates (:520-538)
         up_slots, up_dets, up_ci = [], [], []
