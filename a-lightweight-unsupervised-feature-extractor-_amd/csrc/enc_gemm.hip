@@ -1,47 +1,80 @@
-// Fused bf16 GEMMs of the encoder's RMB (reference model/utils/modules/card.py:
-// DSC :48-57, SEBlock :73-78, RMB.forward :128-148) for gfx950.
+// bf16 GEMMs of the encoder (reference model/utils/modules/card.py: DSC :48-57,
+// SEBlock :73-78, RMB.forward :128-148) for gfx950, with the elementwise work
+// of the eval graph fused into their prologues / epilogues.
 //
-// C = A . B^T on MFMA 32x32x16 bf16 (f32 accumulate), A = activation rows
-// [M, K] (row stride lda), B = weights [N, K] (the conv weight's natural
-// [out, in] layout, K contiguous).  Workgroup tile 128 x 128 (kBM x kBN), BK = 32,
-// 8 waves as 2 (M) x 4 (N), each wave 64 x 32 (two 32x32 accumulators; 256 x
-// 256 tiles measured slower: the accumulators spill at 2 waves/SIMD); A and B tiles
-// are register-staged into a double-buffered, row-padded LDS image (80-B rows:
-// the 16-B fragment reads of the 32 rows of a tile spread over all banks).
+// C = A . B^T on MFMA 32x32x16 bf16 (f32 accumulate): A = activation rows
+// [M, K] (row stride lda), B = weights [N, K] (the conv weight's [out, in]
+// layout, K contiguous).  Workgroup tile 256 x 256, BK = 32, 8 waves as
+// 2 (M) x 4 (N), each wave 128 x 64 (4 x 2 accumulators): 0.75 KB of LDS
+// fragment reads per MFMA, inside the ~1 KB / 32-cycle MFMA the CU's LDS
+// delivers (64 x 32 wave tiles were LDS-bound at 1.5 KB).
 //
-// Epilogues replace the elementwise passes of the unfused graph:
-//   DSC pair  (EPI 0): both DSC 1x1 GEMMs of the RMB in one launch (group 0 =
-//       reinforce, 1 = normal); + BN-folded bias; stores x_r (pre-activation,
-//       SiLU is applied by the transition's prologue) / Hardswish(x_n) into the
-//       [x_r | x_n] rows; accumulates per-ROI column sums of SiLU(x_r) (SE
-//       squeeze) and Hardswish(x_n) (GAP).
-//   transition (EPI 1): A prologue applies SiLU(x_r) * s[roi] (SE excitation)
-//       to the first kscale columns while staging; epilogue + bias, SiLU,
-//       per-ROI column sums only (the GAP is all the head needs; T is never
-//       written).
-// Per-ROI sums are int64 fixed point (2^-24) updated with 64-bit atomics:
-// exact integer addition, so the result does not depend on the order in
-// which tiles finish (deterministic run to run).
+// K loop: operands are staged with LDS-DMA (global_load_lds, 16 B per lane)
+// into a three-stage LDS ring; the wave writes its 1 KB lane-linearly and the XOR
+// swizzle of the image is applied to the per-lane SOURCE address (chunk c of
+// row r at position r*4 + (c ^ ((r >> 2) & 3))), so the 16-B fragment reads of
+// 16 consecutive rows hit 16 distinct bank groups.  Two K steps stay in flight
+// (counted vmcnt + raw s_barrier); no staging registers.
+//
+// Epilogue:
+//   * per-ROI column sums of the activation straight from the accumulators
+//     (lane = column, registers = rows; a 32-row tile spans <= 2 ROIs since
+//     P >= 32), as int64 fixed point (x 2^24) in LDS, then one 64-bit global
+//     atomic per (ROI, column): integer adds, so the sums are identical
+//     whatever order tiles finish in;
+//   * stores through an f32 LDS block [64][264] (row stride chosen so the two
+//     lane halves of a write hit disjoint banks) as 16-B bf16 vectors.
+// Variants:
+//   EPI_DSC   both DSC 1x1 GEMMs (group 0 = reinforce, 1 = normal) + BN-folded
+//             bias; stores SiLU(x_r) / Hardswish(x_n) into the [x_r | x_n]
+//             rows; sums SiLU(x_r) (SE squeeze) / Hardswish(x_n) (GAP).
+//   EPI_TRANS transition: the SE excitation (x_r * s[roi]) is applied in LDS to
+//             the staged A tiles of the first kscale columns; + bias, sums
+//             SiLU(T); T is never stored.
+//   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
 #include "trk_common.h"
 
 namespace {
 
 typedef __bf16 bf8_t __attribute__((ext_vector_type(8)));
 typedef float f16_t __attribute__((ext_vector_type(16)));
+#define GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-constexpr int BK = 32, LDK = BK + 8;  // padded LDS row: 80 B
-constexpr float kFix = 16777216.0f;  // 2^24
+enum { EPI_DSC = 0, EPI_TRANS = 1, EPI_PLAIN = 2 };
+
+constexpr int BK = 32;
+constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
+constexpr int NSTAGE = 3;                   // LDS-DMA ring: two K steps in flight
+constexpr int EROWS = 64;                   // rows per epilogue store block
+
+// Tile configuration: workgroup BM x BN, 8 waves as 2 (M) x 4 (N).  256 x 256
+// (wave 128 x 64: 0.75 KB of LDS fragment reads per MFMA) for the plain GEMM;
+// 128 x 128 (wave 64 x 32) where the epilogue's registers would not fit next
+// to 128 accumulators (the DSC pair and the transition).
+template <int BM_, int BN_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_;
+  static constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 32, TN = WN / 32;
+  static constexpr int AI = BM * CPR / 512, BI = BN * CPR / 512;  // DMA ops per thread per stage
+  static constexpr int TLD = BN + 8;                               // epilogue block row stride (floats)
+  static constexpr int kSlots = BM / 32 + 1;                       // ROIs a tile can touch (P >= 32)
+  static constexpr size_t kStageBytes = NSTAGE * (size_t)(BM + BN) * CPR * 16;
+  static constexpr size_t kEpiBytes = (size_t)EROWS * TLD * 4 + (size_t)kSlots * BN * 8;
+  static constexpr size_t kLds = kStageBytes > kEpiBytes ? kStageBytes : kEpiBytes;
+};
+constexpr float kFix = 16777216.0f;         // 2^24
 
 struct EncGemmArgs {
   const uint16_t* A;
   int64_t lda;
   const uint16_t* B;       // [groups][N][K]
-  const float* bias;       // [groups * N]
-  uint16_t* C;             // EPI 0 output, row stride ldc, group g at column g * N
+  const float* bias;       // [groups * N] or null
+  uint16_t* C;             // output rows, stride ldc; group g at column g * N
   int64_t ldc;
-  long long* sums;         // [nroi][ld_sums]: group g's columns at g * N
+  long long* sums;         // [nroi][ld_sums]; group g at column g * N
   int ld_sums;
-  const float* scale;      // EPI 1: s [nroi][kscale]
+  const float* scale;      // EPI_TRANS: s [nroi][kscale]
   int M, N, K, P, groups, kscale;
 };
 
@@ -62,30 +95,23 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
   return base + bid / nx;
 }
 
+// chunk c (of CPR = 4) of row r lives at r*4 + (c ^ ((r >> 2) & 3)): 16 consecutive
+// rows of one chunk land in 16 distinct 16-B bank groups
+__device__ __forceinline__ int swz(int r, int c) { return r * CPR + (c ^ ((r >> 2) & 3)); }
+__device__ __forceinline__ int unswz_c(int p) { return (p % CPR) ^ (((p / CPR) >> 2) & 3); }
+
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return (uint32_t)trk::f32_to_bf16(a) | ((uint32_t)trk::f32_to_bf16(b) << 16);
 }
 
-// EPI 1 prologue on one staged 16-B piece (8 consecutive k of one row)
-__device__ __forceinline__ uint4 silu_scale_piece(uint4 v, const float* s8) {
-  const float4 s0 = *reinterpret_cast<const float4*>(s8);
-  const float4 s1 = *reinterpret_cast<const float4*>(s8 + 4);
-  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float a = __uint_as_float(w[q] << 16), b = __uint_as_float(w[q] & 0xffff0000u);
-    w[q] = pack_bf16x2(silu_f(a) * sv[2 * q], silu_f(b) * sv[2 * q + 1]);
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-template <int EPI, int BM, int BN>
+template <int EPI, int BM_, int BN_>
 __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
-  constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 32, TN = WN / 32;  // 8 waves: 2 (M) x 4 (N)
-  constexpr int APT = BM / 128, BPT = BN / 128;                          // 16-B pieces per thread
-  __shared__ __align__(16) uint16_t As[2][BM * LDK];
-  __shared__ __align__(16) uint16_t Bs[2][BN * LDK];
+  using T = Tile<BM_, BN_>;
+  constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, TM = T::TM, TN = T::TN;
+  constexpr int AI = T::AI, BI = T::BI, TLD = T::TLD, kSlots = T::kSlots;
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* As = reinterpret_cast<uint4*>(smem);  // [NSTAGE][BM * CPR]
+  uint4* Bs = As + NSTAGE * BM * CPR;           // [NSTAGE][BN * CPR]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -98,32 +124,62 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
   const uint16_t* Ag = a.A + (int64_t)g * a.K;  // group g's K columns of the A rows
   const uint16_t* Bg = a.B + (int64_t)g * a.N * a.K;
 
-  // staging: APT 16-B A pieces and BPT B pieces per thread per K step
-  const int sr = tid >> 2, sk = (tid & 3) * 8;
-  const uint16_t* ap[APT];
-  const float* srow[APT];
+  // LDS-DMA sources: the lane writes LDS position (wave*AI + q)*64 + lane, which
+  // holds (row, chunk) = inverse swizzle of that position
+  const uint16_t* asrc[AI];
+  const uint16_t* bsrc[BI];
 #pragma unroll
-  for (int q = 0; q < APT; ++q) {
-    const int64_t arow = min(m0 + sr + 128 * q, (int64_t)a.M - 1);  // clamp: rows >= M are never stored
-    ap[q] = Ag + arow * a.lda + sk;
-    srow[q] = EPI == 1 ? a.scale + (int64_t)(arow / a.P) * a.kscale + sk : nullptr;
+  for (int q = 0; q < AI; ++q) {
+    const int p = (wave * AI + q) * 64 + lane, r = p / CPR, c = unswz_c(p);
+    const int64_t row = min(m0 + r, (int64_t)a.M - 1);  // clamp: rows >= M are never stored
+    asrc[q] = Ag + row * a.lda + c * 8;
   }
-  const uint16_t* bp = Bg + (int64_t)(n0 + sr) * a.K + sk;
-  uint4 ra[APT], rb[BPT];
-  auto gload = [&](int k0) {
 #pragma unroll
-    for (int q = 0; q < APT; ++q) ra[q] = *reinterpret_cast<const uint4*>(ap[q] + k0);
+  for (int q = 0; q < BI; ++q) {
+    const int p = (wave * BI + q) * 64 + lane, r = p / CPR, c = unswz_c(p);
+    bsrc[q] = Bg + (int64_t)(n0 + r) * a.K + c * 8;
+  }
+  auto issue = [&](int stage, int k0) {
 #pragma unroll
-    for (int q = 0; q < BPT; ++q) rb[q] = *reinterpret_cast<const uint4*>(bp + (int64_t)128 * q * a.K + k0);
+    for (int q = 0; q < AI; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + k0), LPTR(As + stage * BM * CPR + (wave * AI + q) * 64), 16,
+                                       0, 0);
+#pragma unroll
+    for (int q = 0; q < BI; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + k0), LPTR(Bs + stage * BN * CPR + (wave * BI + q) * 64), 16,
+                                       0, 0);
   };
-  auto swrite = [&](int buf, int k0) {
+  // EPI_TRANS: x_r * s[roi] on a staged A tile whose K range is < kscale.  The
+  // thread's s values for step k are loaded during step k-1 (sv registers), so
+  // the transform never waits on a global load.
+  constexpr int TPT = BM * CPR / 512;  // A pieces per thread per step
+  float4 sv[TPT][2];
+  auto sload = [&](int k0) {
 #pragma unroll
-    for (int q = 0; q < APT; ++q) {
-      if (EPI == 1 && k0 + sk < a.kscale) ra[q] = silu_scale_piece(ra[q], srow[q] + k0);
-      *reinterpret_cast<uint4*>(&As[buf][(sr + 128 * q) * LDK + sk]) = ra[q];
+    for (int q = 0; q < TPT; ++q) {
+      const int p = tid + 512 * q, r = p / CPR, c = unswz_c(p);
+      const int64_t row = min(m0 + r, (int64_t)a.M - 1);
+      const float* sp = a.scale + (row / a.P) * a.kscale + k0 + c * 8;
+      sv[q][0] = *reinterpret_cast<const float4*>(sp);
+      sv[q][1] = *reinterpret_cast<const float4*>(sp + 4);
     }
+  };
+  auto transform = [&](int stage) {
+    uint4* as = As + stage * BM * CPR;
 #pragma unroll
-    for (int q = 0; q < BPT; ++q) *reinterpret_cast<uint4*>(&Bs[buf][(sr + 128 * q) * LDK + sk]) = rb[q];
+    for (int q = 0; q < TPT; ++q) {
+      const int p = tid + 512 * q;
+      const float s8[8] = {sv[q][0].x, sv[q][0].y, sv[q][0].z, sv[q][0].w,
+                           sv[q][1].x, sv[q][1].y, sv[q][1].z, sv[q][1].w};
+      uint4 v = as[p];
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x0 = __uint_as_float(w[e] << 16), x1 = __uint_as_float(w[e] & 0xffff0000u);
+        w[e] = pack_bf16x2(x0 * s8[2 * e], x1 * s8[2 * e + 1]);
+      }
+      as[p] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
   };
 
   f16_t acc[TM][TN];
@@ -134,114 +190,198 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  gload(0);
-  swrite(0, 0);
-  __syncthreads();
+  // K loop over an NSTAGE ring.  Each stage is 2 LDS-DMA ops per thread
+  // (AI + BI); waiting for stage kt while stage kt+1 stays in flight is a
+  // counted vmcnt(AI + BI), and the barrier is a raw s_barrier (__syncthreads would
+  // drain every DMA in flight with vmcnt(0), MI355X guide "glds ... across a
+  // barrier").  Stage (kt+2) % 3 is refilled right after the barrier of step
+  // kt: every wave has finished reading it (step kt-1) by then.
+  static_assert(AI + BI == 2 || AI + BI == 4, "vmcnt immediates below assume 2 or 4 DMA ops per stage");
   const int nk = a.K / BK;
+  issue(0, 0);
+  if (nk > 1) issue(1, BK);
+  if (EPI == EPI_TRANS && a.kscale > 0) sload(0);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    const int st = kt % NSTAGE;
+    if (kt + 1 < nk) {
+      if constexpr (AI + BI == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (EPI == EPI_TRANS && kt * BK < a.kscale) {
+      transform(st);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (kt + 2 < nk) issue((kt + 2) % NSTAGE, (kt + 2) * BK);
+    if (EPI == EPI_TRANS && (kt + 1) * BK < a.kscale) sload((kt + 1) * BK);
+    const uint4* as = As + st * BM * CPR;
+    const uint4* bs = Bs + st * BN * CPR;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
-      const int kk = ks * 16 + 8 * (lane >> 5);
+      const int c = ks * 2 + (lane >> 5);
       bf8_t bfr[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf8_t*>(&Bs[buf][(wn * WN + j * 32 + (lane & 31)) * LDK + kk]);
+        bfr[j] = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * WN + j * 32 + (lane & 31), c)]);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const bf8_t af = *reinterpret_cast<const bf8_t*>(&As[buf][(wm * WM + i * 32 + (lane & 31)) * LDK + kk]);
+        const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(wm * WM + i * 32 + (lane & 31), c)]);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) swrite(buf ^ 1, (kt + 1) * BK);
-    __syncthreads();
   }
+  __syncthreads();  // all LDS reads of the ring done before the epilogue reuses it
 
-  // epilogue: lane = column, registers = rows (row = (r&3) + 8(r>>2) + 4(lane>>5)).
-  // Per-ROI column sums: each 32-row tile splits into <= 2 ROI segments (P >= 32);
-  // segments are accumulated in LDS as int64 fixed point per (ROI slot, column)
-  // -- the workgroup's 128 rows touch at most kSlots ROIs -- then one 64-bit
-  // global atomic per touched (ROI, column).  Integer adds: order-independent.
-  constexpr int kSlots = BM / 32 + 1;
-  static_assert(kSlots * BN * 8 <= 2 * BM * LDK * 2, "ROI sums must fit the A operand LDS");
-  __syncthreads();  // operand LDS is reused for the sums
-  unsigned long long* red = reinterpret_cast<unsigned long long*>(&As[0][0]);  // [kSlots][BN]
-  for (int q = tid; q < kSlots * BN; q += 512) red[q] = 0ull;
-  __syncthreads();
-  const int64_t roi_base = m0 / a.P;
+  // ---- epilogue
+  float* tile = reinterpret_cast<float*>(smem);                                                  // [EROWS][TLD]
+  unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + (size_t)EROWS * TLD * 4);  // [kSlots][BN]
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col_l = wn * WN + j * 32 + (lane & 31);
-    const int col = n0 + col_l;
-    const float bv = a.bias[g * a.N + col];
+    const int cl = wn * WN + j * 32 + (lane & 31);
+    const float bv = a.bias ? a.bias[g * a.N + n0 + cl] : 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int64_t r0 = m0 + wm * WM + i * 32;  // first row of this 32-row tile
-      const int64_t roi0 = r0 / a.P;
-      const int64_t split = (roi0 + 1) * a.P;    // first row of the next ROI
-      float s_lo = 0.f, s_hi = 0.f;
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = r0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= a.M) continue;
-        const float v = acc[i][j][r] + bv;
-        float act;
-        if (EPI == 0) {
-          if (g == 0) {
-            act = silu_f(v);
-            a.C[row * a.ldc + col] = trk::f32_to_bf16(v);
-          } else {
-            act = hswish_f(v);
-            a.C[row * a.ldc + (int64_t)a.N + col] = trk::f32_to_bf16(act);
+      for (int r = 0; r < 16; ++r) acc[i][j][r] += bv;
+  }
+
+  if (EPI != EPI_PLAIN) {
+    // per-ROI column sums of the activation from the registers (lane = column,
+    // registers = 16 rows of a 32-row tile; <= 2 ROI segments per tile)
+    for (int q = tid; q < kSlots * BN; q += 512) red[q] = 0ull;
+    __syncthreads();
+    const int64_t roi_base = m0 / a.P;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = wn * WN + j * 32 + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int64_t r0 = m0 + wm * WM + i * 32;
+        const int64_t roi0 = r0 / a.P;
+        const int64_t split = (roi0 + 1) * a.P;
+        float s_lo = 0.f, s_hi = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = r0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const float v = acc[i][j][r];
+          const float act = (EPI == EPI_DSC && g == 1) ? hswish_f(v) : silu_f(v);
+          if (row < a.M) {
+            if (row < split) s_lo += act;
+            else s_hi += act;
           }
-        } else {
-          act = silu_f(v);
         }
-        if (row < split) s_lo += act;
-        else s_hi += act;
-      }
-      s_lo += __shfl_xor(s_lo, 32);
-      s_hi += __shfl_xor(s_hi, 32);
-      if (lane < 32 && r0 < a.M) {
-        const int slot = (int)(roi0 - roi_base);
-        atomicAdd(&red[slot * BN + col_l], (unsigned long long)llrintf(s_lo * kFix));
-        if (split < r0 + 32 && split < a.M)
-          atomicAdd(&red[(slot + 1) * BN + col_l], (unsigned long long)llrintf(s_hi * kFix));
+        s_lo += __shfl_xor(s_lo, 32);
+        s_hi += __shfl_xor(s_hi, 32);
+        if (lane < 32 && r0 < a.M) {
+          const int slot = (int)(roi0 - roi_base);
+          atomicAdd(&red[slot * BN + cl], (unsigned long long)llrintf(s_lo * kFix));
+          if (split < r0 + 32 && split < a.M)
+            atomicAdd(&red[(slot + 1) * BN + cl], (unsigned long long)llrintf(s_hi * kFix));
+        }
       }
     }
+    __syncthreads();
+    const int64_t last_row = min(m0 + BM, (int64_t)a.M) - 1;
+    const int nslot = (int)(last_row / a.P - roi_base) + 1;
+    for (int q = tid; q < nslot * BN; q += 512) {
+      const int slot = q / BN, c = q % BN;
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + (roi_base + slot) * a.ld_sums + g * a.N + n0 + c),
+                red[q]);
+    }
   }
-  __syncthreads();
-  const int64_t last_row = min(m0 + BM, (int64_t)a.M) - 1;
-  const int nslot = (int)(last_row / a.P - roi_base) + 1;
-  for (int q = tid; q < nslot * BN; q += 512) {
-    const int slot = q / BN, c = q % BN;
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + (roi_base + slot) * a.ld_sums + g * a.N + n0 + c),
-              red[q]);
+  if (EPI == EPI_TRANS) return;
+
+  // stores: 64-row blocks through the f32 LDS tile, then 16-B bf16 vectors per
+  // thread (coalesced rows).  Block h holds rows [64h, 64h + 64): wave row-group
+  // wm = h / (WM / 64), its accumulator tiles i = 2 (h % (WM / 64)) .. + 1.
+  constexpr int HPW = WM / EROWS;  // store blocks per wave row-group
+  const int64_t cbase = (int64_t)(EPI == EPI_DSC ? g * a.N : 0) + n0;
+#pragma unroll
+  for (int h = 0; h < BM / EROWS; ++h) {
+    if (wm == h / HPW) {
+#pragma unroll
+      for (int i2 = 0; i2 < 2; ++i2) {
+        const int i = 2 * (h % HPW) + i2;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int cl = wn * WN + j * 32 + (lane & 31);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = i2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            float v = acc[i][j][r];
+            if (EPI == EPI_DSC) v = g == 1 ? hswish_f(v) : silu_f(v);
+            tile[rl * TLD + cl] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < EROWS * BN / 8 / 512; ++q) {
+      const int p = tid + 512 * q, rl = p / (BN / 8), c8 = (p % (BN / 8)) * 8;
+      const int64_t row = m0 + h * EROWS + rl;
+      if (row < a.M) {
+        const float4 v0 = *reinterpret_cast<const float4*>(&tile[rl * TLD + c8]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&tile[rl * TLD + c8 + 4]);
+        *reinterpret_cast<uint4*>(a.C + row * a.ldc + cbase + c8) =
+            make_uint4(pack_bf16x2(v0.x, v0.y), pack_bf16x2(v0.z, v0.w), pack_bf16x2(v1.x, v1.y),
+                       pack_bf16x2(v1.z, v1.w));
+      }
+    }
+    __syncthreads();
   }
 }
 
-constexpr int kBM = 128, kBN = 128;
-
-int launch(const EncGemmArgs& a, int epi, hipStream_t st) {
-  const int64_t mt = ((int64_t)a.M + kBM - 1) / kBM;
-  const int64_t nwg = mt * (a.N / kBN) * a.groups;
+template <int EPI, int BM, int BN>
+int launch(const EncGemmArgs& a, hipStream_t st) {
+  using T = Tile<BM, BN>;
+  const int64_t mt = ((int64_t)a.M + BM - 1) / BM;
+  const int64_t nwg = mt * (a.N / BN) * a.groups;
+  TRK_REQUIRE(a.N % BN == 0, "enc_gemm: N must be a multiple of %d", BN);
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm: too many workgroups");
-  if (epi == 0) hipLaunchKernelGGL((enc_gemm_kernel<0, kBM, kBN>), dim3((unsigned)nwg), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL((enc_gemm_kernel<1, kBM, kBN>), dim3((unsigned)nwg), dim3(512), 0, st, a);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_gemm_kernel<EPI, BM, BN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((enc_gemm_kernel<EPI, BM, BN>), dim3((unsigned)nwg), dim3(512), T::kLds, st, a);
   return trk::check_launch("enc_gemm_kernel");
 }
 
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 }  // namespace
+
+extern "C" int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
+                            int64_t ldc, void* stream) {
+  TRK_REQUIRE(M >= 0 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 && lda >= K && ldc >= N && lda % 8 == 0 &&
+                  ldc % 8 == 0,
+              "enc_gemm: need K %% 32 == 0, N %% 256 == 0, lda/ldc multiples of 8");
+  if (M == 0) return TRK_OK;
+  TRK_REQUIRE(A && B && C && aligned16(A) && aligned16(B) && aligned16(C), "enc_gemm: null or unaligned pointer");
+  EncGemmArgs a{};
+  a.A = (const uint16_t*)A; a.lda = lda;
+  a.B = (const uint16_t*)B; a.bias = nullptr;
+  a.C = (uint16_t*)C; a.ldc = ldc;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = 1; a.groups = 1;
+  return launch<EPI_PLAIN, 256, 256>(a, reinterpret_cast<hipStream_t>(stream));
+}
 
 extern "C" int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2,
                                 const float* bias, int64_t Ng, void* XRN, long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && Kg % BK == 0 && Kg > 0 && Ng % kBN == 0 && Ng > 0,
+  TRK_REQUIRE(M >= 0 && P >= 32 && Kg % BK == 0 && Kg > 0 && Ng % 128 == 0 && Ng > 0,
               "enc_dsc_gemm: need P >= 32, K %% 32 == 0, N %% 128 == 0");
   if (M == 0) return TRK_OK;
-  TRK_REQUIRE(Y2 && W2 && bias && XRN && sums, "enc_dsc_gemm: null pointer");
+  TRK_REQUIRE(Y2 && W2 && bias && XRN && sums && aligned16(Y2) && aligned16(W2) && aligned16(XRN),
+              "enc_dsc_gemm: null or unaligned pointer");
   const int64_t nroi = (M + P - 1) / P;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(sums, 0, sizeof(long long) * nroi * 2 * Ng, st) != hipSuccess) {
@@ -254,17 +394,18 @@ extern "C" int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg
   a.C = (uint16_t*)XRN; a.ldc = 2 * Ng;
   a.sums = sums; a.ld_sums = (int)(2 * Ng);
   a.M = (int)M; a.N = (int)Ng; a.K = (int)Kg; a.P = (int)P; a.groups = 2; a.kscale = 0;
-  return launch(a, 0, st);
+  return launch<EPI_DSC, 128, 128>(a, st);
 }
 
 extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
                                        int64_t kscale, const void* Wt, const float* bias, int64_t N,
                                        long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && K % BK == 0 && K > 0 && N % kBN == 0 && N > 0 && kscale % 8 == 0 &&
+  TRK_REQUIRE(M >= 0 && P >= 32 && K % BK == 0 && K > 0 && N % 128 == 0 && N > 0 && kscale % BK == 0 &&
                   kscale <= K,
-              "enc_transition_gemm: need P >= 32, K %% 32 == 0, N %% 128 == 0, kscale %% 8 == 0");
+              "enc_transition_gemm: need P >= 32, K %% 32 == 0, N %% 128 == 0, kscale %% 32 == 0");
   if (M == 0) return TRK_OK;
-  TRK_REQUIRE(XRN && s && Wt && bias && sums, "enc_transition_gemm: null pointer");
+  TRK_REQUIRE(XRN && s && Wt && bias && sums && aligned16(XRN) && aligned16(Wt) && aligned16(s),
+              "enc_transition_gemm: null or unaligned pointer");
   const int64_t nroi = (M + P - 1) / P;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(sums, 0, sizeof(long long) * nroi * N, st) != hipSuccess) {
@@ -274,9 +415,8 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   EncGemmArgs a{};
   a.A = (const uint16_t*)XRN; a.lda = K;
   a.B = (const uint16_t*)Wt; a.bias = bias;
-  a.C = nullptr; a.ldc = 0;
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  return launch(a, 1, st);
+  return launch<EPI_TRANS, 128, 128>(a, st);
 }

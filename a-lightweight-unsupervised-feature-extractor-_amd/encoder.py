@@ -134,6 +134,7 @@ class Model(nn.Module):
                 w2 = torch.cat([dsc.depth[2].weight.flatten(1), dsc.point[2].weight.flatten(1)], 1).float()
                 w2nk.append(w2 * scale[:, None])                                     # [C, 2h]
             w["w2_nk"] = torch.stack(w2nk, 0).contiguous().to(device, torch.bfloat16)  # [2, C, 2h]
+            w["w1_nk"] = w1.contiguous().to(device, torch.bfloat16)                  # [4h, C]
             w["b2"] = torch.cat([w["br"].float(), w["bn"].float()]).to(device, torch.float32)
             w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
             w["bt_f"] = r.transition[0].bias.float().to(device)
@@ -171,7 +172,7 @@ class Model(nn.Module):
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
-        from .ops import act_mean, dwconv5_nhwc, scale_rows, enc_dsc_gemm, enc_transition_gemm
+        from .ops import act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_dsc_gemm, enc_transition_gemm
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -179,10 +180,15 @@ class Model(nn.Module):
         h2 = h4 // 2
         ss = S1 * S2
         X = x.permute(0, 2, 3, 1).reshape(N * ss, C)                 # view when channels_last
-        Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)                      # 4 first 1x1 convs, one GEMM
-        Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
         Co = W["w2r"].shape[1]
-        if (self.fused_gemm and dt == torch.bfloat16 and ss >= 32 and h2 % 32 == 0 and Co % 128 == 0):
+        fused = (self.fused_gemm and dt == torch.bfloat16 and ss >= 32 and C % 32 == 0 and h4 % 256 == 0 and
+                 h2 % 32 == 0 and Co % 256 == 0)
+        if fused:
+            Y1 = enc_gemm(X, W["w1_nk"]).view(N, S1, S2, h4)         # 4 first 1x1 convs, one GEMM
+        else:
+            Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)
+        Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
+        if fused:
             # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
             # + SiLU + GAP in another: the [M, 512] intermediates are written once (x_r|x_n)
             XRN, sum_r, sum_n = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"])

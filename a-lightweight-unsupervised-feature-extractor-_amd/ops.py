@@ -102,9 +102,26 @@ def scale_rows(x: torch.Tensor, s: torch.Tensor, act: Optional[str] = None) -> t
 _FIX = 2.0 ** -24
 
 
+def enc_gemm(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """bf16 C[M, N] = A[M, K] . B[N, K]^T (A rows may be strided; B = [out, in] weights)."""
+    _need_gpu(A, "enc_gemm")
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16:
+        raise TypeError("enc_gemm: bf16 operands required")
+    if A.dim() != 2 or A.stride(1) != 1:
+        raise ValueError("enc_gemm: A must be [M, K] with unit column stride")
+    M, K = A.shape
+    N, K2 = B.shape
+    if K2 != K:
+        raise ValueError("enc_gemm: shape mismatch")
+    B = B.contiguous()
+    C = torch.empty((M, N), device=A.device, dtype=torch.bfloat16)
+    check(lib().trk_enc_gemm(_ptr(A), M, K, A.stride(0), _ptr(B), N, _ptr(C), N, _stream(A.device)), "enc_gemm")
+    return C
+
+
 def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor):
     """Both DSC 1x1 GEMMs (bf16): Y2 [M, 2*Kg], W2 [2, Ng, Kg], bias [2*Ng] f32 ->
-    (XRN [M, 2*Ng] = [x_r | Hardswish(x_n)], sum_silu_r [R, Ng] f32, sum_hsw_n [R, Ng] f32)
+    (XRN [M, 2*Ng] = [SiLU(x_r) | Hardswish(x_n)], sum_silu_r [R, Ng] f32, sum_hsw_n [R, Ng] f32)
     with R = ceil(M / P) ROIs (sums over each ROI's P rows)."""
     _need_gpu(Y2, "enc_dsc_gemm")
     if Y2.dtype != torch.bfloat16 or W2.dtype != torch.bfloat16:
@@ -125,8 +142,8 @@ def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor)
 
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
                         bias: torch.Tensor) -> torch.Tensor:
-    """sum over each ROI's P rows of SiLU([SiLU(x_r) * s | x_n] . Wt^T + bias):
-    XRN [M, K] bf16 (x_r = first kscale = s.shape[1] columns), s [R, kscale]
+    """sum over each ROI's P rows of SiLU([x_f * s | x_n] . Wt^T + bias):
+    XRN [M, K] bf16 (x_f = first kscale = s.shape[1] columns), s [R, kscale]
     f32, Wt [N, K] bf16 -> [R, N] f32."""
     _need_gpu(XRN, "enc_transition_gemm")
     if XRN.dtype != torch.bfloat16 or Wt.dtype != torch.bfloat16:

@@ -165,18 +165,23 @@ int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C,
  * bf16 [M, *] with M = ROIs x P pixels; weights bf16 [N][K] (conv [out, in]).
  * Per-ROI column sums are int64 fixed point (value x 2^24), zeroed by the
  * call and accumulated exactly (order-independent).  Requires P >= 32,
- * K % 32 == 0, N % 128 == 0.
+ * K % 32 == 0, N % 256 == 0, 16-B aligned operands.
+ *
+ * trk_enc_gemm: plain C[M, N] = A[M, K] . B[N, K]^T in bf16 (row strides lda,
+ *   ldc): the four first 1x1 convs of the RMB as one GEMM (card.py:28,38). 
  *
  * trk_enc_dsc_gemm: both DSC 1x1 GEMMs (card.py:53-56, depth.2 + point.2 with
  *   eval-BN folded): Y2 [M, 2*Kg] (reinforce half | normal half), W2
- *   [2][Ng][Kg], bias [2*Ng] -> XRN [M, 2*Ng] = [x_r (pre-activation) |
- *   Hardswish(x_n)], sums [ROIs][2*Ng] = per-ROI sums of SiLU(x_r) (SE squeeze,
- *   card.py:75) and Hardswish(x_n) (GAP).
- * trk_enc_transition_gemm: T = [SiLU(x_r) * s | x_n] . Wt^T + bias
- *   (card.py:78 + :138-139), the SiLU(x_r) * s[roi] scaling applied to the
- *   first kscale columns of XRN while staging; only the per-ROI sums of
- *   SiLU(T) are produced (sums [ROIs][N]); T is never stored.
+ *   [2][Ng][Kg], bias [2*Ng] -> XRN [M, 2*Ng] = [SiLU(x_r) | Hardswish(x_n)],
+ *   sums [ROIs][2*Ng] = per-ROI sums of SiLU(x_r) (SE squeeze, card.py:75)
+ *   and Hardswish(x_n) (GAP).
+ * trk_enc_transition_gemm: T = [x_f * s | x_n] . Wt^T + bias (card.py:78 +
+ *   :138-139) with XRN = [x_f | x_n], the SE scale s[roi] applied to the first
+ *   kscale columns while staging; only the per-ROI sums of SiLU(T) are
+ *   produced (sums [ROIs][N]); T is never stored.
  * ---------------------------------------------------------------------- */
+int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
+                 int64_t ldc, void* stream);
 int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2, const float* bias,
                      int64_t Ng, void* XRN, long long* sums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,

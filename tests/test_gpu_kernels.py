@@ -358,7 +358,8 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     XRN, sr, sn = ops.enc_dsc_gemm(Y2, P, W2, b2)
     xr, xn = _bf16_ref_rows(Y2, W2, b2)
     hn = F.hardswish(xn)
-    assert (XRN[:, :Ng].float() - xr).abs().max().item() <= 1e-2 * max(1.0, xr.abs().max().item())
+    sr_ = F.silu(xr)
+    assert (XRN[:, :Ng].float() - sr_).abs().max().item() <= 1e-2 * max(1.0, sr_.abs().max().item())
     assert (XRN[:, Ng:].float() - hn).abs().max().item() <= 1e-2 * max(1.0, hn.abs().max().item())
     ref_sr = F.silu(xr).view(R, P, Ng).sum(1)
     ref_sn = hn.view(R, P, Ng).sum(1)
@@ -372,10 +373,16 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
     bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
     st = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
-    xs = (F.silu(XRN[:, :Ng].float()).view(R, P, Ng) * s[:, None, :]).bfloat16().float().view(M, Ng)
+    xs = (XRN[:, :Ng].float().view(R, P, Ng) * s[:, None, :]).bfloat16().float().view(M, Ng)
     A = torch.cat([xs, XRN[:, Ng:].float()], 1)
     ref_t = F.silu(A @ Wt.float().t() + bt).view(R, P, Ng).sum(1)
     assert (st - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item()
+    # plain GEMM (the first 1x1 convs), strided A rows
+    W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
+    A = Y2[:, :512]
+    Y1 = ops.enc_gemm(A, W1)
+    ref1 = A.float() @ W1.float().t()
+    assert (Y1.float() - ref1).abs().max().item() <= 1e-2 * max(1.0, ref1.abs().max().item())
 
 
 # ----------------------------------------------------- encoder helpers ----
