@@ -209,8 +209,16 @@ def kernel_pass(pipe, f, reps=10):
     m = pipe.model
     W = m._fused_weights(torch.bfloat16, roi.device)
     K = roi.shape[0]
-    Y1 = (roi.permute(0, 2, 3, 1).reshape(K * 100, 512) @ W["w1t"]).view(K, 10, 10, -1)
+    X = roi.permute(0, 2, 3, 1).reshape(K * 100, 512)
+    timed("enc_gemm_plain", lambda: ops.enc_gemm(X, W["w1_nk"]))
+    Y1 = ops.enc_gemm(X, W["w1_nk"]).view(K, 10, 10, -1)
     timed("dwconv5", lambda: ops.dwconv5_nhwc(Y1, W["dw_t"]))
+    Y2 = ops.dwconv5_nhwc(Y1, W["dw_t"]).view(K * 100, -1)
+    timed("enc_gemm_dsc", lambda: ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"]))
+    XRN, sum_r, _ = ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"])
+    with torch.no_grad():
+        s_se = m._se(sum_r / 100)
+    timed("enc_gemm_trans", lambda: ops.enc_transition_gemm(XRN, 100, s_se, W["wt_nk"], W["bt_f"]))
     timed("encoder", lambda: pipe.stage_embed(roi))
     emb = pipe.stage_embed(roi)
     # tracker kernels on the current track table (rows = all live tracks)
@@ -349,20 +357,36 @@ def main():
     Fs, N, S = sc["streams"], sc["N"], 10
     K = Fs * N
     # algorithmic work per launch; DESIGN.md §Roofline
-    algo = {
-        "roi_align": ("hbm", Fs * 512 * 40 * 40 * 4 + K * 512 * S * S * 2 + K * 20, HBM_PEAK_GBS, "GB/s"),
-        "dwconv5": ("hbm", 2 * K * S * S * 1024 * 2 + 25 * 1024 * 4, HBM_PEAK_GBS, "GB/s"),
-        "encoder": ("mfma", K * ENC_FLOP_PER_ROI[S], BF16_PEAK_TFLOPS, "TFLOP/s"),
-        "cost": ("mfma", 2.0 * Fs * M * 32 * N * 128, F32_MFMA_PEAK_TFLOPS, "TFLOP/s"),
+    # algorithmic work per launch: bytes that
+    # must cross HBM and flops on the kernel's matrix core; the binding roof is
+    # the larger of bytes / HBM peak and flops / MFMA peak
+    R = K * S * S  # encoder rows
+    algo = {  # name: (bytes, flops, mfma peak TFLOP/s)
+        "roi_align": (Fs * 512 * 40 * 40 * 4 + K * 512 * S * S * 2 + K * 20, 0.0, BF16_PEAK_TFLOPS),
+        "enc_gemm_plain": (R * 512 * 2 + R * 1024 * 2 + 1024 * 512 * 2, 2.0 * R * 1024 * 512, BF16_PEAK_TFLOPS),
+        "dwconv5": (2 * R * 1024 * 2 + 25 * 1024 * 4, 2.0 * R * 1024 * 25, BF16_PEAK_TFLOPS),
+        "enc_gemm_dsc": (R * 1024 * 2 * 2 + 2 * 512 * 512 * 2 + K * 1024 * 8, 2.0 * R * 1024 * 512,
+                         BF16_PEAK_TFLOPS),
+        "enc_gemm_trans": (R * 1024 * 2 + 512 * 1024 * 2 + K * 512 * 12, 2.0 * R * 512 * 1024, BF16_PEAK_TFLOPS),
+        "cost": (Fs * (M * 30 * 128 * 4 + N * 128 * 4 + M * N * 4), 2.0 * Fs * M * 30 * N * 128,
+                 F32_MFMA_PEAK_TFLOPS),
     }
     per = {}
-    for k, (bound, work, peak, unit) in algo.items():
-        ach = work / (kt[k] * 1e-6) / (1e9 if unit == "GB/s" else 1e12)
-        per[k] = dict(bound=bound, us=round(kt[k], 2), achieved=round(ach, 2), peak=peak, unit=unit,
-                      frac=round(ach / peak, 4))
+    for k, (byt, fl, mpeak) in algo.items():
+        t = kt[k] * 1e-6
+        t_hbm, t_mfma = byt / (HBM_PEAK_GBS * 1e9), fl / (mpeak * 1e12)
+        if t_hbm >= t_mfma:
+            per[k] = dict(bound="hbm", us=round(kt[k], 2), achieved=round(byt / t / 1e9, 2), peak=HBM_PEAK_GBS,
+                          unit="GB/s", frac=round(t_hbm / t, 4), work=byt)
+        else:
+            per[k] = dict(bound="mfma", us=round(kt[k], 2), achieved=round(fl / t / 1e12, 2), peak=mpeak,
+                          unit="TFLOP/s", frac=round(t_mfma / t, 4), work=fl)
+    per["encoder_stage"] = dict(bound="mfma", us=round(kt["encoder"], 2),
+                                achieved=round(K * ENC_FLOP_PER_ROI[S] / (kt["encoder"] * 1e-6) / 1e12, 2),
+                                peak=BF16_PEAK_TFLOPS, unit="TFLOP/s",
+                                frac=round(K * ENC_FLOP_PER_ROI[S] / (BF16_PEAK_TFLOPS * 1e12) / (kt["encoder"] * 1e-6), 4))
     # dominant hand-written kernel by measured time (LSAP is latency-bound: no roofline)
-    mine = {k: kt[k] for k in ("roi_align", "dwconv5", "cost", "lsap")}
-    dom = max(("roi_align", "dwconv5", "cost"), key=lambda k: mine[k])
+    dom = max(algo, key=lambda k: kt[k])
     # HBM traffic per launch from the committed rocprofv3 --pmc summary of this
     # bench (tools/gpu_pmc.sh -> profiles/pmc_traffic.json); null if absent
     traffic, tsrc = None, None
@@ -377,7 +401,8 @@ def main():
         pass
     rf = {"kernel": dom, "bound": per[dom]["bound"], "achieved": per[dom]["achieved"],
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
-          "traffic": traffic, "traffic_source": tsrc, "algorithmic_work_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
+          "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": algo[dom][0],
+          "algorithmic_flops_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2)}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",

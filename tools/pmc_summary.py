@@ -38,7 +38,10 @@ def main():
         print(f"{k[:90]:90s} n={v['launches']:4d} fetch={v['fetch_kib'] or 0:12.1f} KiB write={v['write_kib'] or 0:12.1f} KiB")
     print("JSON " + json.dumps(out))
     if len(sys.argv) > 3:  # short-name traffic table for bench.py (profiles/pmc_traffic.json)
-        short_names = {"roi_sweep_kernel": "roi_align", "dwconv5_nhwc_kernel": "dwconv5", "cost_kernel": "cost",
+        short_names = {"roi_sweep_kernel": "roi_align", "dwconv5_rows2_kernel": "dwconv5",
+                       "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost",
+                       "enc_gemm_kernel<0": "enc_gemm_dsc", "enc_gemm_kernel<1": "enc_gemm_trans",
+                       "enc_gemm_kernel<2": "enc_gemm_plain",
                        "lsap_kernel": "lsap", "act_mean_kernel": "act_mean", "scale_rows_kernel": "scale_rows",
                        "nchw_to_nhwc_kernel": "nchw_to_nhwc", "track_update_kernel": "track_update"}
         tab = {}
