@@ -89,11 +89,11 @@ class Pipeline:
     """The per-frame hot path over a batch of streams.
 
     Software-pipelined across frames: frame f+1's ROI Align + encoder (which do
-    not depend on tracking state) are enqueued on a side stream as soon as
-    frame f's stage-1 LSAP is launched, so they run while the solver (one
-    workgroup per video stream) and the host bookkeeping proceed; frame f+1's
-    cost build waits for them with a stream event.  Every frame still does the
-    full work once."""
+    not depend on tracking state) are enqueued on a side stream at the start of
+    frame f's step, so they run while frame f's cost build, solver (one
+    workgroup per video stream) and host bookkeeping proceed; frame f+1's cost
+    build waits for them with a stream event.  Every frame still does the full
+    work once, inside the timed region."""
 
     def __init__(self, sc, model, S=10):
         self.sc, self.model, self.S = sc, model, S
@@ -102,6 +102,11 @@ class Pipeline:
         self.side = torch.cuda.Stream(device=sc["feat"].device)
         self.pending = {}  # frame -> (embeddings, ready event)
         self.graphs = None
+        # enqueue frame f+1's embedding at the start of step f (measured 1.13M vs
+        # 0.94M ROIs/s against enqueueing it after step f's LSAP launch): the
+        # cost build and solver of f then share the GPU with it instead of
+        # serialising between consecutive encoder runs
+        self.prefetch_early = os.environ.get("TRK_PREFETCH_EARLY", "1") == "1"
 
     def capture(self):
         """Capture roi_align + encoder as two hipGraphs (static ROI / embedding
@@ -158,9 +163,13 @@ class Pipeline:
         self.embed_async(f)
         emb, ev = self.pending.pop(f)
         torch.cuda.current_stream().wait_event(ev)
+        if self.prefetch_early:  # next frame's embedding before this frame's cost build
+            self.embed_async(f + 1)
+            hook = None
+        else:
+            hook = lambda: self.embed_async(f + 1)
         return self.tracker.step(emb, sc["dbox"][f], sc["dconf"][f], [sc["N"]] * sc["streams"],
-                                 sc["confs_host"][f], [f] * sc["streams"],
-                                 after_launch=lambda: self.embed_async(f + 1))
+                                 sc["confs_host"][f], [f] * sc["streams"], after_launch=hook)
 
     def check_identity(self, f, res):
         """fraction of detections matched to the track that has followed the
