@@ -249,7 +249,11 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] += bv;
+      for (int r = 0; r < 16; ++r) {
+        // the activation, once: both the ROI sums and the stores use it
+        const float v = acc[i][j][r] + bv;
+        acc[i][j][r] = EPI == EPI_PLAIN ? v : (EPI == EPI_DSC && g == 1) ? hswish_f(v) : silu_f(v);
+      }
   }
 
   if (EPI != EPI_PLAIN) {
@@ -270,8 +274,7 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int64_t row = r0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const float v = acc[i][j][r];
-          const float act = (EPI == EPI_DSC && g == 1) ? hswish_f(v) : silu_f(v);
+          const float act = acc[i][j][r];
           if (row < a.M) {
             if (row < split) s_lo += act;
             else s_hi += act;
@@ -315,9 +318,7 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rl = i2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            float v = acc[i][j][r];
-            if (EPI == EPI_DSC) v = g == 1 ? hswish_f(v) : silu_f(v);
-            tile[rl * TLD + cl] = v;
+            tile[rl * TLD + cl] = acc[i][j][r];
           }
         }
       }
