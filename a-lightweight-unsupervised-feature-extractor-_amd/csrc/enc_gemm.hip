@@ -48,10 +48,11 @@ constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
 constexpr int NSTAGE = 3;                   // LDS-DMA ring: two K steps in flight
 constexpr int EROWS = 64;                   // rows per epilogue store block
 
-// Tile configuration: workgroup BM x BN, 8 waves as 2 (M) x 4 (N).  256 x 256
-// (wave 128 x 64: 0.75 KB of LDS fragment reads per MFMA) for the plain GEMM;
-// 128 x 128 (wave 64 x 32) where the epilogue's registers would not fit next
-// to 128 accumulators (the DSC pair and the transition).
+// Tile configuration: workgroup BM x BN, 8 waves as 2 (M) x 4 (N).  Measured
+// per variant (M = 204800, K = 512 / 1024): 256 x 256 (wave 128 x 64, 0.75 KB of
+// LDS fragment reads per MFMA) for the plain GEMM; 128 x 256 (wave 64 x 64) for
+// the transition; 128 x 128 (wave 64 x 32) for the DSC pair, whose store +
+// activation epilogue overlaps best with 3 workgroups per CU.
 template <int BM_, int BN_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_;
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
   // drain every DMA in flight with vmcnt(0), MI355X guide "glds ... across a
   // barrier").  Stage (kt+2) % 3 is refilled right after the barrier of step
   // kt: every wave has finished reading it (step kt-1) by then.
-  static_assert(AI + BI == 2 || AI + BI == 4, "vmcnt immediates below assume 2 or 4 DMA ops per stage");
+  static_assert(AI + BI >= 2 && AI + BI <= 4, "vmcnt immediates below assume 2..4 DMA ops per stage");
   const int nk = a.K / BK;
   issue(0, 0);
   if (nk > 1) issue(1, BK);
@@ -205,6 +206,7 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
     const int st = kt % NSTAGE;
     if (kt + 1 < nk) {
       if constexpr (AI + BI == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (AI + BI == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -401,9 +403,9 @@ extern "C" int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg
 extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
                                        int64_t kscale, const void* Wt, const float* bias, int64_t N,
                                        long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && K % BK == 0 && K > 0 && N % 128 == 0 && N > 0 && kscale % BK == 0 &&
+  TRK_REQUIRE(M >= 0 && P >= 32 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 && kscale % BK == 0 &&
                   kscale <= K,
-              "enc_transition_gemm: need P >= 32, K %% 32 == 0, N %% 128 == 0, kscale %% 32 == 0");
+              "enc_transition_gemm: need P >= 32, K %% 32 == 0, N %% 256 == 0, kscale %% 32 == 0");
   if (M == 0) return TRK_OK;
   TRK_REQUIRE(XRN && s && Wt && bias && sums && aligned16(XRN) && aligned16(Wt) && aligned16(s),
               "enc_transition_gemm: null or unaligned pointer");
@@ -419,5 +421,5 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  return launch<EPI_TRANS, 128, 128>(a, st);
+  return launch<EPI_TRANS, 128, 256>(a, st);
 }
