@@ -66,6 +66,8 @@ def _declare(L):
     L.trk_act_scale_rows.restype = i32
     L.trk_enc_gemm.argtypes = [P, i64, i64, i64, P, i64, P, i64, P]
     L.trk_enc_gemm.restype = i32
+    L.trk_enc_g1_dwconv.argtypes = [P, i64, P, i64, P, P, P]
+    L.trk_enc_g1_dwconv.restype = i32
     L.trk_enc_dsc_gemm.argtypes = [P, i64, i64, i64, P, P, i64, P, P, P]
     L.trk_enc_dsc_gemm.restype = i32
     L.trk_enc_transition_gemm.argtypes = [P, i64, i64, i64, P, i64, P, P, i64, P, P]

@@ -98,6 +98,8 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 
 // chunk c (of CPR = 4) of row r lives at r*4 + (c ^ ((r >> 2) & 3)): 16 consecutive
 // rows of one chunk land in 16 distinct 16-B bank groups
+typedef float dw_pair_t __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ int swz(int r, int c) { return r * CPR + (c ^ ((r >> 2) & 3)); }
 __device__ __forceinline__ int unswz_c(int p) { return (p % CPR) ^ (((p / CPR) >> 2) & 3); }
 
@@ -361,6 +363,176 @@ int launch(const EncGemmArgs& a, hipStream_t st) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// ---------------------------------------------------------------------------
+// First 1x1 convs + the four depthwise 5x5 convs in one kernel (10x10 ROIs).
+//
+// The M tile is two whole ROIs (200 rows, computed as 7 MFMA row tiles of 32;
+// rows 200..223 belong to the next tile and are discarded), so the 5x5
+// neighbourhood of every output pixel is inside the tile: Y1 = X . W1^T is
+// rounded to bf16 into LDS (exactly what the plain GEMM would store) and the
+// depthwise conv runs from there with the same f32 FMA order as
+// dwconv5_rows2_kernel, writing only Y2.  Y1 never reaches HBM.  N tile = 128
+// channels; 8 waves: wave w owns column tile w & 3 and row tiles
+// (w >> 2) + 2t.  K loop as enc_gemm_kernel (LDS-DMA ring, NSTAGE = 3).
+constexpr int G1_ROWS = 224, G1_RT = 7, G1_BN = 128, G1_S = 10, G1_P = 100;
+constexpr int G1_AP = G1_ROWS * CPR;               // A 16-B pieces per stage (896)
+constexpr size_t G1_STAGE = (size_t)(G1_ROWS + G1_BN) * CPR * 16;
+constexpr size_t G1_TILE = (size_t)2 * G1_P * (G1_BN / 2) * 4;   // bf16 pairs [200][64]
+constexpr size_t G1_W = (size_t)25 * (G1_BN / 2) * 8;            // f32 pairs [25][64]
+constexpr size_t G1_LDS = NSTAGE * G1_STAGE > G1_TILE + G1_W ? NSTAGE * G1_STAGE : G1_TILE + G1_W;
+
+__global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
+                                                   const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
+                                                   int M, int N) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* As = reinterpret_cast<uint4*>(smem);       // [NSTAGE][224 * CPR]
+  uint4* Bs = As + NSTAGE * G1_AP;                   // [NSTAGE][128 * CPR]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3, wr = wave >> 2;
+  const int ntile_n = N / G1_BN;
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(lb % ntile_n) * G1_BN;
+  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);   // two ROIs per tile
+  constexpr int K = 512;
+
+  // DMA sources: A pieces p = q*512 + tid (q = 0: all waves; q = 1: waves 0..5)
+  const uint16_t* asrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = min(q * 512 + tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
+    const int64_t row = min(m0 + r, (int64_t)M - 1);
+    asrc[q] = X + row * K + c * 8;
+  }
+  const uint16_t* bsrc;
+  {
+    const int p = tid, r = p / CPR, c = unswz_c(p);
+    bsrc = W1 + (int64_t)(n0 + r) * K + c * 8;
+  }
+  auto issue = [&](int stage, int k0) {
+    __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
+    if (wave < (G1_AP - 512) / 64)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
+  };
+  // row tiles of this wave: wr, wr + 2, wr + 4 (+ wr + 6 for wr == 0)
+  constexpr int TMX = 4;
+  const int ntm = wr == 0 ? 4 : 3;
+  f16_t acc[TMX];
+#pragma unroll
+  for (int i = 0; i < TMX; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  // waves 0..5 issue 3 DMA ops per stage, waves 6..7 issue 2
+  const int nk = K / BK;
+  issue(0, 0);
+  issue(1, BK);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt % NSTAGE;
+    if (kt + 1 < nk) {
+      if (wave < (G1_AP - 512) / 64) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) issue((kt + 2) % NSTAGE, (kt + 2) * BK);
+    const uint4* as = As + st * G1_AP;
+    const uint4* bs = Bs + st * G1_BN * CPR;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int c = ks * 2 + (lane >> 5);
+      const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
+#pragma unroll
+      for (int i = 0; i < TMX; ++i) {
+        if (i < ntm) {
+          const int rt = wr + 2 * i;
+          const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // Y1 (bf16-rounded, rows < 200 of the tile) -> LDS [200][64 channel pairs]
+  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
+  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G1_TILE);
+  {
+    const int cl = wn * 32 + (lane & 31);  // channel within the tile
+#pragma unroll
+    for (int i = 0; i < TMX; ++i) {
+      if (i < ntm) {
+        const int rt = wr + 2 * i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
+        }
+      }
+    }
+  }
+  for (int q = tid; q < 25 * (G1_BN / 2); q += 512) {
+    const int k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
+    wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
+  }
+  __syncthreads();
+
+  // depthwise 5x5: task = (ROI, output row pair), lane = channel pair
+  const int cp = lane;
+  for (int task = wave; task < 2 * (G1_S / 2); task += 8) {
+    const int roi = task / (G1_S / 2), y0 = 2 * (task % (G1_S / 2));
+    const int64_t rbase = m0 + roi * G1_P;
+    if (rbase >= M) continue;
+    const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2);
+    dw_pair_t a0[G1_S], a1[G1_S];
+#pragma unroll
+    for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int yy = y0 - 2 + r;
+      if (yy < 0 || yy >= G1_S) continue;
+      dw_pair_t rr[G1_S + 4];
+#pragma unroll
+      for (int x = 0; x < G1_S + 4; ++x) {
+        const int xx = x - 2;
+        if (xx >= 0 && xx < G1_S) {
+          const uint32_t v = src[(yy * G1_S + xx) * (G1_BN / 2) + cp];
+          rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+        } else {
+          rr[x] = dw_pair_t{0.f, 0.f};
+        }
+      }
+      if (r <= 4) {
+        dw_pair_t wv[5];
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G1_BN / 2) + cp];
+#pragma unroll
+        for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx], a0[x]);
+      }
+      if (r >= 1) {
+        dw_pair_t wv[5];
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G1_BN / 2) + cp];
+#pragma unroll
+        for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx], a1[x]);
+      }
+    }
+    uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
+#pragma unroll
+    for (int x = 0; x < G1_S; ++x) {
+      dst[(y0 * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a0[x].x, a0[x].y);
+      dst[((y0 + 1) * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a1[x].x, a1[x].y);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
@@ -422,4 +594,25 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
   return launch<EPI_TRANS, 128, 256>(a, st);
+}
+
+extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64_t N, const float* wdw, void* Y2,
+                                 void* stream) {
+  TRK_REQUIRE(M >= 0 && M % 100 == 0 && N % 128 == 0 && N > 0,
+              "enc_g1_dwconv: 10x10 ROIs (M %% 100 == 0), K = 512, N %% 128 == 0");
+  if (M == 0) return TRK_OK;
+  TRK_REQUIRE(X && W1 && wdw && Y2 && aligned16(X) && aligned16(W1) && aligned16(Y2) && aligned16(wdw),
+              "enc_g1_dwconv: null or unaligned pointer");
+  const int64_t nwg = (M / 200 + (M % 200 ? 1 : 0)) * (N / 128);
+  TRK_REQUIRE(nwg < 0x7fffffff, "enc_g1_dwconv: too many workgroups");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)G1_LDS);
+    attr = true;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(g1dw_kernel, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
+                     (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+  return trk::check_launch("g1dw_kernel");
 }

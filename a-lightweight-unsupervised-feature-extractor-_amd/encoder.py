@@ -169,10 +169,12 @@ class Model(nn.Module):
     # bf16 inputs take the fused trk GEMMs (enc_gemm.hip) when the shapes allow;
     # fp32 (the parity path) keeps hipBLASLt GEMMs + the separate act/mean passes
     fused_gemm = True
+    fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
-        from .ops import act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_dsc_gemm, enc_transition_gemm
+        from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
+                          enc_transition_gemm)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -183,11 +185,14 @@ class Model(nn.Module):
         Co = W["w2r"].shape[1]
         fused = (self.fused_gemm and dt == torch.bfloat16 and ss >= 32 and C % 32 == 0 and h4 % 256 == 0 and
                  h2 % 32 == 0 and Co % 256 == 0)
-        if fused:
-            Y1 = enc_gemm(X, W["w1_nk"]).view(N, S1, S2, h4)         # 4 first 1x1 convs, one GEMM
+        if fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_dwconv:
+            Y2 = enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])               # first 1x1 convs + depthwise 5x5, one kernel
         else:
-            Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)
-        Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)             # 4 depthwise 5x5, one kernel
+            if fused:
+                Y1 = enc_gemm(X, W["w1_nk"]).view(N, S1, S2, h4)     # 4 first 1x1 convs, one GEMM
+            else:
+                Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)
+            Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)         # 4 depthwise 5x5, one kernel
         if fused:
             # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
             # + SiLU + GAP in another: the [M, 512] intermediates are written once (x_r|x_n)

@@ -119,6 +119,24 @@ def enc_gemm(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     return C
 
 
+def enc_g1_dwconv(X: torch.Tensor, W1: torch.Tensor, wdw: torch.Tensor) -> torch.Tensor:
+    """bf16: dwconv5(X . W1^T) for 10x10 ROIs: X [R*100, 512] rows, W1 [N, 512],
+    wdw tap-major [25, N] f32 -> Y2 [R*100, N] (== enc_gemm then dwconv5_nhwc)."""
+    _need_gpu(X, "enc_g1_dwconv")
+    if X.dtype != torch.bfloat16 or W1.dtype != torch.bfloat16:
+        raise TypeError("enc_g1_dwconv: bf16 operands required")
+    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or W1.shape[1] != 512:
+        raise ValueError("enc_g1_dwconv: X must be contiguous [M, 512] and W1 [N, 512]")
+    M = X.shape[0]
+    N = W1.shape[0]
+    if wdw.shape != (25, N) or wdw.dtype != torch.float32:
+        raise ValueError("enc_g1_dwconv: wdw must be [25, N] f32")
+    Y2 = torch.empty((M, N), device=X.device, dtype=torch.bfloat16)
+    check(lib().trk_enc_g1_dwconv(_ptr(X), M, _ptr(W1.contiguous()), N, _ptr(wdw.contiguous()), _ptr(Y2),
+                                  _stream(X.device)), "enc_g1_dwconv")
+    return Y2
+
+
 def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor):
     """Both DSC 1x1 GEMMs (bf16): Y2 [M, 2*Kg], W2 [2, Ng, Kg], bias [2*Ng] f32 ->
     (XRN [M, 2*Ng] = [SiLU(x_r) | Hardswish(x_n)], sum_silu_r [R, Ng] f32, sum_hsw_n [R, Ng] f32)

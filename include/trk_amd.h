@@ -182,6 +182,12 @@ int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C,
  * ---------------------------------------------------------------------- */
 int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
                  int64_t ldc, void* stream);
+/* trk_enc_g1_dwconv: trk_enc_gemm (K = 512) followed by the 1024-channel
+ *   depthwise 5x5 (card.py:29,39) in one kernel for 10x10 ROIs (M = ROIs x 100):
+ *   Y2 = dwconv5(bf16(X . W1^T)) with weights tap-major [25][N] f32; Y1 never
+ *   reaches HBM.  Bit-identical to trk_enc_gemm + trk_dwconv5_nhwc. */
+int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64_t N, const float* wdw, void* Y2,
+                      void* stream);
 int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2, const float* bias,
                      int64_t Ng, void* XRN, long long* sums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,

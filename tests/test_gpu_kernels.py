@@ -383,6 +383,14 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     Y1 = ops.enc_gemm(A, W1)
     ref1 = A.float() @ W1.float().t()
     assert (Y1.float() - ref1).abs().max().item() <= 1e-2 * max(1.0, ref1.abs().max().item())
+    if P == 100:
+        # first GEMM + depthwise 5x5 fused == the two kernels, bit for bit (odd ROI count: a
+        # half-filled last tile)
+        X = A.contiguous()
+        wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
+        Yf = ops.enc_g1_dwconv(X, W1, wdw)
+        Yu = ops.dwconv5_nhwc(ops.enc_gemm(X, W1).view(R, 10, 10, 1024), wdw).view(M, 1024)
+        assert torch.equal(Yf, Yu)
 
 
 # ----------------------------------------------------- encoder helpers ----
