@@ -219,10 +219,8 @@ def kernel_pass(pipe, f, reps=10):
     W = m._fused_weights(torch.bfloat16, roi.device)
     K = roi.shape[0]
     X = roi.permute(0, 2, 3, 1).reshape(K * 100, 512)
-    timed("enc_gemm_plain", lambda: ops.enc_gemm(X, W["w1_nk"]))
-    Y1 = ops.enc_gemm(X, W["w1_nk"]).view(K, 10, 10, -1)
-    timed("dwconv5", lambda: ops.dwconv5_nhwc(Y1, W["dw_t"]))
-    Y2 = ops.dwconv5_nhwc(Y1, W["dw_t"]).view(K * 100, -1)
+    timed("enc_g1_dwconv", lambda: ops.enc_g1_dwconv(X, W["w1_nk"], W["dw_t"]))
+    Y2 = ops.enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])
     timed("enc_gemm_dsc", lambda: ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"]))
     XRN, sum_r, _ = ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"])
     with torch.no_grad():
@@ -372,8 +370,8 @@ def main():
     R = K * S * S  # encoder rows
     algo = {  # name: (bytes, flops, mfma peak TFLOP/s)
         "roi_align": (Fs * 512 * 40 * 40 * 4 + K * 512 * S * S * 2 + K * 20, 0.0, BF16_PEAK_TFLOPS),
-        "enc_gemm_plain": (R * 512 * 2 + R * 1024 * 2 + 1024 * 512 * 2, 2.0 * R * 1024 * 512, BF16_PEAK_TFLOPS),
-        "dwconv5": (2 * R * 1024 * 2 + 25 * 1024 * 4, 2.0 * R * 1024 * 25, BF16_PEAK_TFLOPS),
+        "enc_g1_dwconv": (R * 512 * 2 + R * 1024 * 2 + 1024 * 512 * 2 + 25 * 1024 * 4,
+                          2.0 * R * 1024 * 512 + 2.0 * R * 1024 * 25, BF16_PEAK_TFLOPS),
         "enc_gemm_dsc": (R * 1024 * 2 * 2 + 2 * 512 * 512 * 2 + K * 1024 * 8, 2.0 * R * 1024 * 512,
                          BF16_PEAK_TFLOPS),
         "enc_gemm_trans": (R * 1024 * 2 + 512 * 1024 * 2 + K * 512 * 12, 2.0 * R * 512 * 1024, BF16_PEAK_TFLOPS),

@@ -41,7 +41,7 @@ def main():
         short_names = {"roi_sweep_kernel": "roi_align", "dwconv5_rows2_kernel": "dwconv5",
                        "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost",
                        "enc_gemm_kernel<0": "enc_gemm_dsc", "enc_gemm_kernel<1": "enc_gemm_trans",
-                       "enc_gemm_kernel<2": "enc_gemm_plain",
+                       "enc_gemm_kernel<2": "enc_gemm_plain", "g1dw_kernel": "enc_g1_dwconv",
                        "lsap_kernel": "lsap", "act_mean_kernel": "act_mean", "scale_rows_kernel": "scale_rows",
                        "nchw_to_nhwc_kernel": "nchw_to_nhwc", "track_update_kernel": "track_update"}
         tab = {}
