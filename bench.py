@@ -192,6 +192,48 @@ def _ev():
     return torch.cuda.Event(enable_timing=True)
 
 
+class LiveProbe:
+    """HIP-event pairs around the library calls of the hot path INSIDE the timed
+    region, recorded on the stream each call launches on (the side stream for
+    roi_align + encoder).  Wraps ops' handle to libtrk_amd; inactive outside
+    the timed region.  Each bracketed call is one kernel launch, except
+    trk_roi_align_fwd (NCHW->NHWC transpose + sweep = the roi stage) and the
+    two summing GEMMs (a 4-8 MB hipMemsetAsync of the sums precedes the GEMM)."""
+
+    NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_enc_g1_dwconv": "enc_g1_dwconv",
+             "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans"}
+
+    def __init__(self):
+        self.on = False
+        self.ev = {v: [] for v in self.NAMES.values()}
+        self._orig = ops.lib
+        probe = self
+
+        class _Proxy:
+            def __getattr__(self, name):
+                fn = getattr(probe._orig(), name)
+                key = probe.NAMES.get(name)
+                if not probe.on or key is None:
+                    return fn
+
+                def call(*a):
+                    st = torch.cuda.current_stream()
+                    e0, e1 = _ev(), _ev()
+                    e0.record(st)
+                    rc = fn(*a)
+                    e1.record(st)
+                    probe.ev[key].append((e0, e1))
+                    return rc
+                return call
+
+        self._proxy = _Proxy()
+        ops.lib = lambda: self._proxy
+
+    def means_us(self):
+        torch.cuda.synchronize()
+        return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e3 for k, v in self.ev.items() if v}
+
+
 def kernel_pass(pipe, f, reps=10):
     """Average device time of each hand-written kernel on the real step inputs,
     HIP events on the stream the kernel is launched on (the current stream)."""
@@ -349,14 +391,21 @@ def main():
         pipe.step(f)
         f += 1
 
+    probe = LiveProbe()
+    probe.on = True
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
                                torch.cuda.synchronize, dev)
+    probe.on = False
+    live = probe.means_us()
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
     ident = float(np.mean([pipe.check_identity(PREROLL + args.warmup + k, r) for k, r in enumerate(results)]))
 
-    kt, M = kernel_pass(pipe, f - 1)
+    iso, M = kernel_pass(pipe, f - 1)
+    # per-launch device time: live (timed region) where probed, else isolated
+    kt = dict(iso)
+    kt.update(live)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -410,6 +459,9 @@ def main():
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
           "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": algo[dom][0],
           "algorithmic_flops_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
+          "kernel_us_source": {k: ("live: HIP events around each launch in the timed region" if k in live
+                                   else "isolated: back-to-back launches after the timed region") for k in kt},
+          "isolated_us": {k: round(v, 2) for k, v in iso.items()},
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2)}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",
