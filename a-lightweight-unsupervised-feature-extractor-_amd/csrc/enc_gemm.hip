@@ -374,7 +374,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 // dwconv5_rows2_kernel, writing only Y2.  Y1 never reaches HBM.  N tile = 128
 // channels; 8 waves: wave w owns column tile w & 3 and row tiles
 // (w >> 2) + 2t.  K loop as enc_gemm_kernel (LDS-DMA ring, NSTAGE = 3).
-constexpr int G1_ROWS = 224, G1_RT = 7, G1_BN = 128, G1_S = 10, G1_P = 100;
+constexpr int G1_ROWS = 224, G1_BN = 128, G1_S = 10, G1_P = 100;
 constexpr int G1_AP = G1_ROWS * CPR;               // A 16-B pieces per stage (896)
 constexpr size_t G1_STAGE = (size_t)(G1_ROWS + G1_BN) * CPR * 16;
 constexpr size_t G1_TILE = (size_t)2 * G1_P * (G1_BN / 2) * 4;   // bf16 pairs [200][64]

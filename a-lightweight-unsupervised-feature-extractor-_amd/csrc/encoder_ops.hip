@@ -44,14 +44,12 @@ typedef float dw_f2 __attribute__((ext_vector_type(2)));
 // 16-B global piece -> f32 channel pairs in LDS
 template <typename T> struct Piece;
 template <> struct Piece<float> {  // 4 channels
-  static constexpr int kPairs = 2;
   static __device__ __forceinline__ void put(dw_f2* d, uint4 v) {
     d[0] = dw_f2{__uint_as_float(v.x), __uint_as_float(v.y)};
     d[1] = dw_f2{__uint_as_float(v.z), __uint_as_float(v.w)};
   }
 };
 template <> struct Piece<uint16_t> {  // 8 channels
-  static constexpr int kPairs = 4;
   static __device__ __forceinline__ void put(dw_f2* d, uint4 v) {
     d[0] = dw_f2{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u)};
     d[1] = dw_f2{__uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};

@@ -139,6 +139,13 @@ class Model(nn.Module):
             w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
             w["bt_f"] = r.transition[0].bias.float().to(device)
             w["bt"] = r.transition[0].bias.to(device, dtype)
+            # f32 operands of the per-ROI tail kernels (enc_se / enc_head)
+            se, hd = r.se.excitation, self.head.net
+            f32 = lambda t: t.detach().float().contiguous().to(device)
+            w["se_w1"], w["se_b1"], w["se_w2"], w["se_b2"] = f32(se[0].weight), f32(se[0].bias), \
+                f32(se[2].weight), f32(se[2].bias)
+            w["h0"], w["ln_w"], w["ln_b"] = f32(hd[0].weight), f32(hd[1].weight), f32(hd[1].bias)
+            w["h4"], w["h4b"] = f32(hd[4].weight), f32(hd[4].bias)
         self._fused, self._fused_key = w, key
         return w
 
@@ -170,11 +177,12 @@ class Model(nn.Module):
     # fp32 (the parity path) keeps hipBLASLt GEMMs + the separate act/mean passes
     fused_gemm = True
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
+    fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_transition_gemm)
+                          enc_transition_gemm, enc_se, enc_head)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -196,8 +204,15 @@ class Model(nn.Module):
         if fused:
             # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
             # + SiLU + GAP in another: the [M, 512] intermediates are written once (x_r|x_n)
-            XRN, sum_r, sum_n = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"])
-            m_r, m_n = sum_r / ss, sum_n / ss
+            XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
+            if self.fused_tail:
+                # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
+                m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+                tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
+                return enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
+                                self.head.net[1].eps, W["h4"], W["h4b"])
+            f = (sums.double() * 2.0 ** -24).float()
+            m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
             s = self._se(m_r)
             m_cat = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"]) / ss
             a = self._alpha()

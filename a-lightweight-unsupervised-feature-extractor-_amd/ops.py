@@ -137,10 +137,11 @@ def enc_g1_dwconv(X: torch.Tensor, W1: torch.Tensor, wdw: torch.Tensor) -> torch
     return Y2
 
 
-def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor):
+def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor, raw: bool = False):
     """Both DSC 1x1 GEMMs (bf16): Y2 [M, 2*Kg], W2 [2, Ng, Kg], bias [2*Ng] f32 ->
     (XRN [M, 2*Ng] = [SiLU(x_r) | Hardswish(x_n)], sum_silu_r [R, Ng] f32, sum_hsw_n [R, Ng] f32)
-    with R = ceil(M / P) ROIs (sums over each ROI's P rows)."""
+    with R = ceil(M / P) ROIs (sums over each ROI's P rows).  raw=True returns
+    (XRN, sums [R, 2*Ng] int64 fixed point x 2^24) for enc_se."""
     _need_gpu(Y2, "enc_dsc_gemm")
     if Y2.dtype != torch.bfloat16 or W2.dtype != torch.bfloat16:
         raise TypeError("enc_dsc_gemm: bf16 operands required")
@@ -154,15 +155,17 @@ def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor)
     sums = torch.empty((R, 2 * Ng), device=Y2.device, dtype=torch.int64)
     check(lib().trk_enc_dsc_gemm(_ptr(Y2), M, P, Kg, _ptr(W2), _ptr(bias), Ng, _ptr(XRN), _ptr(sums),
                                  _stream(Y2.device)), "enc_dsc_gemm")
+    if raw:
+        return XRN, sums
     f = (sums.double() * _FIX).float()
     return XRN, f[:, :Ng], f[:, Ng:]
 
 
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
-                        bias: torch.Tensor) -> torch.Tensor:
+                        bias: torch.Tensor, raw: bool = False) -> torch.Tensor:
     """sum over each ROI's P rows of SiLU([x_f * s | x_n] . Wt^T + bias):
     XRN [M, K] bf16 (x_f = first kscale = s.shape[1] columns), s [R, kscale]
-    f32, Wt [N, K] bf16 -> [R, N] f32."""
+    f32, Wt [N, K] bf16 -> [R, N] f32 (raw=True: the int64 x 2^24 sums, for enc_head)."""
     _need_gpu(XRN, "enc_transition_gemm")
     if XRN.dtype != torch.bfloat16 or Wt.dtype != torch.bfloat16:
         raise TypeError("enc_transition_gemm: bf16 operands required")
@@ -176,7 +179,55 @@ def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Te
     sums = torch.empty((R, N), device=XRN.device, dtype=torch.int64)
     check(lib().trk_enc_transition_gemm(_ptr(XRN), M, P, K, _ptr(s), s.shape[1], _ptr(Wt), _ptr(bias), N,
                                         _ptr(sums), _stream(XRN.device)), "enc_transition_gemm")
+    if raw:
+        return sums
     return (sums.double() * _FIX).float()
+
+
+def _f32c(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.float32).contiguous()
+
+
+def enc_se(sums: torch.Tensor, P: int, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+           b2: torch.Tensor):
+    """SE squeeze + excitation from enc_dsc_gemm's raw sums [R, 2C] int64:
+    returns (m_r, m_n, s) [R, C] f32 with m = (float)(sum * 2^-24) / P and
+    s = hardsigmoid(w2 . relu(w1 . m_r + b1) + b2) (card.py:59-78)."""
+    _need_gpu(sums, "enc_se")
+    if sums.dtype != torch.int64 or sums.dim() != 2:
+        raise TypeError("enc_se: sums must be [R, 2C] int64")
+    H, C = w1.shape
+    R = sums.shape[0]
+    if sums.shape[1] < 2 * C or w2.shape != (C, H) or b1.numel() != H or b2.numel() != C:
+        raise ValueError("enc_se: shape mismatch")
+    sums = sums.contiguous()
+    out = torch.empty((3, R, C), device=sums.device, dtype=torch.float32)
+    w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
+    check(lib().trk_enc_se(_ptr(sums), R, sums.stride(0), P, C, _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2),
+                           _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _stream(sums.device)), "enc_se")
+    return out[0], out[1], out[2]
+
+
+def enc_head(tsums: torch.Tensor, P: int, s: torch.Tensor, m_r: torch.Tensor, m_n: torch.Tensor, alpha: float,
+             w0: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, ln_eps: float, w4: torch.Tensor,
+             b4: torch.Tensor) -> torch.Tensor:
+    """Shake2 eval mix + ProjectionHead from enc_transition_gemm's raw sums
+    [R, C] int64 (card.py:83-96, :151-169): [R, D] f32 unit rows."""
+    _need_gpu(tsums, "enc_head")
+    if tsums.dtype != torch.int64 or tsums.dim() != 2:
+        raise TypeError("enc_head: tsums must be [R, C] int64")
+    R, C = tsums.shape
+    D = w4.shape[0]
+    if (s.shape != (R, C) or m_r.shape != (R, C) or m_n.shape != (R, C) or w0.shape != (C, C) or
+            w4.shape[1] != C or b4.numel() != D or ln_w.numel() != C or ln_b.numel() != C):
+        raise ValueError("enc_head: shape mismatch")
+    out = torch.empty((R, D), device=tsums.device, dtype=torch.float32)
+    tsums, s, m_r, m_n = tsums.contiguous(), _f32c(s), _f32c(m_r), _f32c(m_n)
+    w0, ln_w, ln_b, w4, b4 = _f32c(w0), _f32c(ln_w), _f32c(ln_b), _f32c(w4), _f32c(b4)
+    check(lib().trk_enc_head(_ptr(tsums), R, P, C, _ptr(s), _ptr(m_r), _ptr(m_n), float(alpha), _ptr(w0),
+                             _ptr(ln_w), _ptr(ln_b), float(ln_eps), _ptr(w4), _ptr(b4), D, _ptr(out),
+                             _stream(tsums.device)), "enc_head")
+    return out
 
 
 # ------------------------------------------------------------- ROI Align --

@@ -193,6 +193,24 @@ int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const voi
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
 
+/* Per-ROI tail of the encoder (f32, 16 ROIs per workgroup, f32-input MFMA).
+ * trk_enc_se: squeeze means and SE excitation (card.py:59-78) from the sums of
+ *   trk_enc_dsc_gemm ([R][ld_sums], ld_sums >= 2C: C sums of SiLU(x_r), then C of
+ *   Hardswish(x_n)): m_r, m_n [R][C] = (float)(sum * 2^-24) / P;
+ *   s [R][C] = hardsigmoid(w2 . relu(w1 . m_r + b1) + b2), w1 [H][C], w2 [C][H].
+ * trk_enc_head: g = 0.5 m_cat + 0.5 (alpha (s m_r) + (1 - alpha) m_n) (Shake2
+ *   eval + GAP, card.py:83-96, :128-148; m_cat from the trk_enc_transition_gemm
+ *   sums [R][C]) -> ProjectionHead (card.py:151-169): out [R][D] =
+ *   normalize(w4 . silu(LayerNorm(w0 . g; ln_w, ln_b, ln_eps)) + b4), w0 [C][C],
+ *   w4 [D][C].  Replaces ~25 small torch launches between and after the GEMMs.
+ * C, H, D multiples of 16, <= 1024. */
+int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int64_t P, int64_t C, const float* w1,
+               const float* b1, int64_t H, const float* w2, const float* b2, float* m_r, float* m_n, float* s,
+               void* stream);
+int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_t C, const float* s, const float* m_r,
+                 const float* m_n, double alpha, const float* w0, const float* ln_w, const float* ln_b,
+                 float ln_eps, const float* w4, const float* b4, int64_t D, float* out, void* stream);
+
 /* ------------------------------------------------------------------------
  * Device-resident track state.  Track slots of all
  * streams share one set of slot arrays:

@@ -393,6 +393,62 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         assert torch.equal(Yf, Yu)
 
 
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_se_head_vs_torch_fp32(trk, gpu, R):
+    """trk_enc_se / trk_enc_head vs the same math in torch fp32 (the encoder's own
+    _se / _head on the reference weights).  Means: bit-identical (same ops);
+    s: 2e-6; embeddings (unit rows): 2e-5 -- the f32 MFMA sums in another order.
+    R = 1 / 37: partial 16-ROI workgroups."""
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()})
+    m = m.to(gpu)
+    W = m._fused_weights(torch.bfloat16, gpu)
+    g = torch.Generator().manual_seed(R)
+    P = 100
+    sums = (torch.randn(R, 1024, generator=g) * 40 * 2 ** 24).to(torch.int64).to(gpu)
+    m_r, m_n, s = ops.enc_se(sums, P, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+    f = (sums.double() * 2.0 ** -24).float()
+    # correctly rounded f32 division by P (torch's GPU tensor / scalar multiplies by 1/P: <= 1 ulp apart)
+    assert torch.allclose(m_r, f[:, :512] / P, rtol=1.2e-7, atol=0)
+    assert torch.allclose(m_n, f[:, 512:] / P, rtol=1.2e-7, atol=0)
+    with torch.no_grad():
+        s_ref = m._se(m_r)
+    assert (s - s_ref).abs().max().item() <= 2e-6
+    tsums = (torch.randn(R, 512, generator=g) * 30 * 2 ** 24).to(torch.int64).to(gpu)
+    for a in (0.5, 0.3141592653589793):
+        z = ops.enc_head(tsums, P, s, m_r, m_n, a, W["h0"], W["ln_w"], W["ln_b"], m.head.net[1].eps,
+                         W["h4"], W["h4b"])
+        m_cat = (tsums.double() * 2.0 ** -24).float() / P
+        with torch.no_grad():
+            z_ref = m._head(0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n))
+        assert z.shape == (R, 128)
+        assert (z - z_ref).abs().max().item() <= 2e-5, a
+    # deterministic
+    z2 = ops.enc_head(tsums, P, s, m_r, m_n, a, W["h0"], W["ln_w"], W["ln_b"], m.head.net[1].eps,
+                      W["h4"], W["h4b"])
+    assert torch.equal(z, z2)
+
+
+def test_encoder_fused_tail_matches_torch_tail(trk, gpu):
+    """bf16 encoder with the two tail kernels vs the same graph with the torch
+    SE / mix / head ops: identical up to f32 summation order (2e-5)."""
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()})
+    m = m.to(gpu)
+    x = torch.from_numpy(G.encoder_input(5, 64, 10)).to(gpu).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        z = m(x)
+        try:
+            m.fused_tail = False
+            zt = m(x)
+        finally:
+            m.fused_tail = True
+    assert (z - zt).abs().max().item() <= 2e-5
+
+
 # ----------------------------------------------------- encoder helpers ----
 @pytest.mark.parametrize("S", [7, 10])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
