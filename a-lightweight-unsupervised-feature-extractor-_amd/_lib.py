@@ -17,6 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "trk_amd.h")
 TRK_F32, TRK_BF16, TRK_F64 = 0, 1, 2
 TRK_NCHW, TRK_NHWC = 0, 1
 TRK_LSAP_MAX_DIM = 2048
+TRK_ENC_PARTS = 3  # per-ROI partial sums of the encoder GEMMs (trk_amd.h)
 
 _lock = threading.Lock()
 _lib = None
@@ -72,6 +73,8 @@ def _declare(L):
     L.trk_enc_dsc_gemm.restype = i32
     L.trk_enc_transition_gemm.argtypes = [P, i64, i64, i64, P, i64, P, P, i64, P, P]
     L.trk_enc_transition_gemm.restype = i32
+    L.trk_enc_sums_reduce.argtypes = [P, i64, i64, i64, P, P]
+    L.trk_enc_sums_reduce.restype = i32
     L.trk_enc_se.argtypes = [P, i64, i64, i64, i64, P, P, i64, P, P, P, P, P, P]
     L.trk_enc_se.restype = i32
     L.trk_enc_head.argtypes = [P, i64, i64, i64, P, P, P, ctypes.c_double, P, P, P, f32, P, P, i64, P, P]

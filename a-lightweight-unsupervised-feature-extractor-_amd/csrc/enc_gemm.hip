@@ -34,6 +34,9 @@
 //   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
 #include "trk_common.h"
 
+int g_enc_gemm = 1;      // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
+int g_enc_gemm_dbg = 0;  // trk_set_tuning("enc_gemm_dbg"): gemm4 experiments (1 skip epilogue, 2 stores, 4 sums, 8 sum writes)
+
 namespace {
 
 typedef __bf16 bf8_t __attribute__((ext_vector_type(8)));
@@ -65,6 +68,12 @@ struct Tile {
   static constexpr size_t kLds = kStageBytes > kEpiBytes ? kStageBytes : kEpiBytes;
 };
 constexpr float kFix = 16777216.0f;         // 2^24
+// per-ROI sums leave the GEMMs as int64 partials, one per 128-row M tile that
+// covers the ROI (<= 3 for P <= 256), written with plain stores (no atomics,
+// no memset); consumers add the 1..3 partials of a ROI (trk_enc_sums_reduce,
+// trk_enc_se, trk_enc_head) -- integer adds, so the totals do not depend on
+// tile order
+constexpr int kPart = TRK_ENC_PARTS, kPartRows = 128;
 
 struct EncGemmArgs {
   const uint16_t* A;
@@ -73,10 +82,11 @@ struct EncGemmArgs {
   const float* bias;       // [groups * N] or null
   uint16_t* C;             // output rows, stride ldc; group g at column g * N
   int64_t ldc;
-  long long* sums;         // [nroi][ld_sums]; group g at column g * N
-  int ld_sums;
+  long long* sums;         // per-ROI partial sums [nroi][kPart][ld_sums] (one per 128-row tile
+  int ld_sums;             // covering the ROI); group g at column g * N
   const float* scale;      // EPI_TRANS: s [nroi][kscale]
   int M, N, K, P, groups, kscale;
+  int dbg;                 // g_enc_gemm_dbg
 };
 
 // bf16-path activations: hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32), a
@@ -299,8 +309,9 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
     const int nslot = (int)(last_row / a.P - roi_base) + 1;
     for (int q = tid; q < nslot * BN; q += 512) {
       const int slot = q / BN, c = q % BN;
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.sums + (roi_base + slot) * a.ld_sums + g * a.N + n0 + c),
-                red[q]);
+      const int64_t roi = roi_base + slot;
+      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);  // this tile among the ROI's tiles
+      a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] = (long long)red[q];
     }
   }
   if (EPI == EPI_TRANS) return;
@@ -533,7 +544,359 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
   }
 }
 
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(const T* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)p);
+}
+__device__ __forceinline__ u32x4 lds_read128(uint32_t addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_write128(uint32_t addr, u32x4 v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v silu2(f2v v) {
+  const f2v e = v * f2v{-1.44269504088896341f, -1.44269504088896341f};
+  const f2v d = f2v{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)} + f2v{1.0f, 1.0f};
+  return v * f2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+__device__ __forceinline__ f2v hswish2(f2v v) {
+  const f2v c = v + f2v{3.0f, 3.0f};
+  const f2v r = f2v{fminf(fmaxf(c.x, 0.0f), 6.0f), fminf(fmaxf(c.y, 0.0f), 6.0f)};
+  return (v * r) * f2v{1.0f / 6.0f, 1.0f / 6.0f};
+}
+
+__device__ __forceinline__ void g4_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// gemm4: 128 x 256 tiles on 4-wave workgroups, two workgroups per CU, so one
+// workgroup's epilogue (activation, ROI sums, the bf16 stores) runs under the
+// other's MFMA loop.  Waves 2 (M) x 2 (N), wave tile 64 x 128 = 4 x 8 MFMA
+// 16x16x32 tiles (0.375 KB of fragment reads per MFMA).  BK = 32 in a
+// 3-buffer LDS-DMA ring, tile kt + 2 issued at the top of step kt (its buffer
+// was last read in step kt - 1, before the barrier that ends it); the counted
+// vmcnt(6) at the end of step kt retires tile kt + 1 and leaves kt + 2 in
+// flight; one raw s_barrier per K step.  LDS 80 KiB per workgroup.
+constexpr int G4_SLD = 132;                 // stage row stride (u32): conflict-free pair writes
+constexpr int G4_BUF = 1536;                // uint4 per buffer: A 512 (128 rows) | B 1024 (256 rows)
+constexpr size_t G4_RING = (size_t)3 * G4_BUF * 16;     // 72 KiB
+constexpr int G4_SLOTS = 4;                 // ROIs a 128-row tile spans (P >= 43)
+constexpr int G4_WSLOTS = 3;                // ROIs a wave's 64 rows span (P >= 43)
+constexpr int G4_SQ = 2;                    // s-tile DMA per thread (8 KiB)
+constexpr size_t G4_STILE = (size_t)G4_SQ * 256 * 16;
+constexpr size_t G4_STAGE = (size_t)128 * G4_SLD * 4;   // 66 KiB
+constexpr size_t G4_RED = (size_t)G4_SLOTS * 256 * 8;   // 8 KiB
+constexpr size_t G4_LDS = (G4_RING + G4_STILE) > (G4_STAGE + G4_RED) ? (G4_RING + G4_STILE) : (G4_STAGE + G4_RED);
+static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* ring = reinterpret_cast<uint4*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntile_n = a.N / 256;
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntl = (int)(lb % (ntile_n * a.groups));
+  const int64_t mt = lb / (ntile_n * a.groups);
+  const int g = ntl / ntile_n, n0 = (ntl % ntile_n) * 256;
+  const int64_t m0 = mt * 128;
+  const uint16_t* Ag = a.A + (int64_t)g * a.K;
+  const uint16_t* Bg = a.B + (int64_t)g * a.N * a.K;
+  const int nk = a.K / BK;
+  const int64_t roi_base = m0 / a.P;
+
+  const uint16_t* asrc[2];
+  const uint16_t* bsrc[4];
+  int arow[2], achk[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ ((r >> 2) & 3);
+    arow[q] = r;
+    achk[q] = c;
+    asrc[q] = Ag + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ ((r >> 2) & 3);
+    bsrc[q] = Bg + (int64_t)(n0 + r) * a.K + c * 8;
+  }
+  auto issue = [&](int kt) {
+    uint4* d = ring + (kt % 3) * G4_BUF + wave * 64;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + kt * BK), LPTR(d + 512 + q * 256), 16, 0, 0);
+  };
+
+  const float* stile = reinterpret_cast<const float*>(smem + G4_RING);
+  const float* srow[2] = {stile, stile};
+  if constexpr (EPI == EPI_TRANS) {
+    const int per = a.kscale / 4;
+    const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
+#pragma unroll
+    for (int q = 0; q < G4_SQ; ++q) {
+      const int p = q * 256 + tid;
+      const int slot = min(p / per, G4_SLOTS - 1);
+      const int64_t roi = min(roi_base + slot, nroi - 1);
+      const float* src = a.scale + roi * a.kscale + (p % per) * 4;
+      __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(reinterpret_cast<uint4*>(smem + G4_RING) + q * 256 + wave * 64),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t row = min(m0 + arow[q], (int64_t)a.M - 1);
+      srow[q] = stile + (int)(row / a.P - roi_base) * a.kscale + achk[q] * 8;
+    }
+  }
+  auto transform = [&](int kt) {
+    if constexpr (EPI == EPI_TRANS) {
+      if (kt * BK < a.kscale) {
+        const uint32_t d = lds_addr(ring + (kt % 3) * G4_BUF + tid);
+        u32x4 v[2], s4[2][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          v[q] = lds_read128(d + q * 256 * 16);
+          const uint32_t sa = lds_addr(srow[q] + kt * BK);
+          s4[q][0] = lds_read128(sa);
+          s4[q][1] = lds_read128(sa + 16);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(s4[0][0]), "+v"(s4[0][1]),
+                     "+v"(s4[1][0]), "+v"(s4[1][1])::"memory");
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float s_lo = __uint_as_float(s4[q][e >> 1][(2 * e) & 3]);
+            const float s_hi = __uint_as_float(s4[q][e >> 1][(2 * e + 1) & 3]);
+            o[e] = pack_bf16x2(__uint_as_float(v[q][e] << 16) * s_lo, __uint_as_float(v[q][e] & 0xffff0000u) * s_hi);
+          }
+          lds_write128(d + q * 256 * 16, o);
+        }
+      }
+    }
+  };
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int lterm = fr * 4 + (fc ^ ((fr >> 2) & 3));
+  const int aoff = (wr * 64) * 4 + lterm;            // + mt * 64
+  const int boff = 512 + (wc * 128) * 4 + lterm;     // + nt * 64
+
+  f4v acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nk > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  transform(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g4_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 2 < nk) issue(kt + 2);
+    const uint4* buf = ring + (kt % 3) * G4_BUF;
+    bf8v bfr[8], afr[4];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) bfr[t] = *reinterpret_cast<const bf8v*>(buf + boff + t * 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + aoff + i * 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[t], acc[i][t], 0, 0, 0);
+    if (kt + 1 < nk) {
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      transform(kt + 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    g4_barrier();
+  }
+
+  if (a.dbg & 1) {
+    if (tid == 0 && acc[0][0][0] == 12345.f) a.sums[0] = 1;
+    return;
+  }
+  // ---- epilogue (the ring is free: every DMA retired, all reads done at the last barrier)
+  const int colq = wc * 128 + fr;  // + t * 16
+  const bool hsw = EPI == EPI_DSC && g == 1;
+  float bias8[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) bias8[t] = a.bias[g * a.N + n0 + colq + t * 16];  // one batch of loads
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const f2v b2 = {bias8[t], bias8[t]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + b2;
+        v = hsw ? hswish2(v) : silu2(v);
+        acc[i][t][2 * h] = v.x;
+        acc[i][t][2 * h + 1] = v.y;
+      }
+  }
+  unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));
+  for (int q = tid; q < G4_SLOTS * 256; q += 256) red[q] = 0ull;
+  __syncthreads();
+  if (!(a.dbg & 4)) {
+    const int64_t r0w = m0 + wr * 64;
+    const int64_t roiw = r0w / a.P;
+    const int wslot0 = (int)(roiw - roi_base);
+    const int P = a.P;
+    const int nxt0 = P - (int)(r0w - roiw * P);
+    const bool full = r0w + 64 <= (int64_t)a.M;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float ssum[G4_WSLOTS] = {0.f, 0.f, 0.f};
+      int slot = 0, nxt = nxt0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f4v v = acc[k][t];
+        if (full && nxt >= 16 * k + 16) {
+          const float x = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+          for (int q = 0; q < G4_WSLOTS; ++q)
+            if (q == slot) ssum[q] += x;
+        } else {
+          float lo = 0.f, hi = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 16 * k + fc * 4 + e;
+            const float x = (r0w + row < a.M) ? v[e] : 0.f;
+            if (row < nxt) lo += x;
+            else hi += x;
+          }
+#pragma unroll
+          for (int q = 0; q < G4_WSLOTS; ++q) {
+            if (q == slot) ssum[q] += lo;
+            if (q == slot + 1) ssum[q] += hi;
+          }
+        }
+        if (nxt <= 16 * k + 16) {
+          ++slot;
+          nxt += P;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < G4_WSLOTS; ++q) {
+        ssum[q] += __shfl_xor(ssum[q], 16);
+        ssum[q] += __shfl_xor(ssum[q], 32);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int q = 0; q < G4_WSLOTS; ++q)
+          if (q <= slot && wslot0 + q < G4_SLOTS && ssum[q] != 0.f)
+            atomicAdd(&red[(wslot0 + q) * 256 + colq + t * 16], (unsigned long long)llrintf(ssum[q] * kFix));
+      }
+    }
+  }
+  if (EPI == EPI_DSC && !(a.dbg & 2)) {
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
+    const bool odd = fr & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const f4v v = acc[i][t];
+        const float x0 = __shfl_xor(odd ? v[0] : v[2], 1);
+        const float x1 = __shfl_xor(odd ? v[1] : v[3], 1);
+        const int rb = wr * 64 + i * 16 + fc * 4 + (odd ? 2 : 0);
+        const int cp = (wc * 128 + t * 16 + fr) >> 1;
+        stage[rb * G4_SLD + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
+        stage[(rb + 1) * G4_SLD + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+      }
+  }
+  __syncthreads();
+  {
+    const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
+    const int nslot = (int)(last_row / a.P - roi_base) + 1;
+    if (!(a.dbg & 8))
+      for (int q = tid; q < nslot * 256; q += 256) {
+        const int slot = q >> 8, c = q & 255;
+        const int64_t roi = roi_base + slot;
+        const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
+        a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] = (long long)red[q];
+      }
+  }
+  if (EPI == EPI_DSC && !(a.dbg & 2)) {
+    const uint32_t* stage = reinterpret_cast<const uint32_t*>(smem);
+    const int64_t cbase = (int64_t)g * a.N + n0;
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      const int p = q * 256 + tid, rl = p >> 5, c8 = (p & 31) * 8;
+      const int64_t row = m0 + rl;
+      if (row < a.M)
+        *reinterpret_cast<uint4*>(a.C + row * a.ldc + cbase + c8) =
+            *reinterpret_cast<const uint4*>(stage + rl * G4_SLD + c8 / 2);
+    }
+  }
+}
+
+template <int EPI>
+int launch4(const EncGemmArgs& a, hipStream_t st) {
+  const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
+  TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm4: too many workgroups");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
+    attr = true;
+  }
+  EncGemmArgs b = a;
+  b.dbg = g_enc_gemm_dbg;
+  hipLaunchKernelGGL((gemm4_kernel<EPI>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b);
+  return trk::check_launch("gemm4_kernel");
+}
+
+
+// out[roi][c] = (float)(sum_j part[roi][j][c] * 2^-24) over the 1..3 partials
+__global__ void __launch_bounds__(256) sums_reduce_kernel(const long long* __restrict__ part, int64_t R, int P,
+                                                          int ld, float* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= R * ld) return;
+  const int64_t roi = q / ld;
+  const int c = (int)(q % ld);
+  const int cnt = (int)((roi * P + P - 1) / kPartRows - roi * P / kPartRows) + 1;
+  long long v = 0;
+  for (int j = 0; j < cnt; ++j) v += part[(roi * kPart + j) * ld + c];
+  out[q] = (float)((double)v * (1.0 / 16777216.0));
+}
+
 }  // namespace
+
+extern "C" int trk_enc_sums_reduce(const long long* part, int64_t R, int64_t P, int64_t ld, float* out,
+                                   void* stream) {
+  TRK_REQUIRE(R >= 0 && P >= 1 && P <= 256 && ld > 0, "enc_sums_reduce: need R >= 0, 1 <= P <= 256, ld > 0");
+  if (R == 0) return TRK_OK;
+  TRK_REQUIRE(part && out, "enc_sums_reduce: null pointer");
+  hipLaunchKernelGGL(sums_reduce_kernel, dim3((unsigned)((R * ld + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), part, R, (int)P, (int)ld, out);
+  return trk::check_launch("sums_reduce_kernel");
+}
 
 extern "C" int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
                             int64_t ldc, void* stream) {
@@ -552,47 +915,39 @@ extern "C" int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, co
 
 extern "C" int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2,
                                 const float* bias, int64_t Ng, void* XRN, long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && Kg % BK == 0 && Kg > 0 && Ng % 128 == 0 && Ng > 0,
-              "enc_dsc_gemm: need P >= 32, K %% 32 == 0, N %% 128 == 0");
+  TRK_REQUIRE(M >= 0 && P >= 32 && P <= 256 && Kg % BK == 0 && Kg > 0 && Ng % 128 == 0 && Ng > 0,
+              "enc_dsc_gemm: need 32 <= P <= 256, K %% 32 == 0, N %% 128 == 0");
   if (M == 0) return TRK_OK;
   TRK_REQUIRE(Y2 && W2 && bias && XRN && sums && aligned16(Y2) && aligned16(W2) && aligned16(XRN),
               "enc_dsc_gemm: null or unaligned pointer");
-  const int64_t nroi = (M + P - 1) / P;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(sums, 0, sizeof(long long) * nroi * 2 * Ng, st) != hipSuccess) {
-    trk::set_error("enc_dsc_gemm: memset failed");
-    return TRK_ELAUNCH;
-  }
   EncGemmArgs a{};
   a.A = (const uint16_t*)Y2; a.lda = 2 * Kg;
   a.B = (const uint16_t*)W2; a.bias = bias;
   a.C = (uint16_t*)XRN; a.ldc = 2 * Ng;
   a.sums = sums; a.ld_sums = (int)(2 * Ng);
   a.M = (int)M; a.N = (int)Ng; a.K = (int)Kg; a.P = (int)P; a.groups = 2; a.kscale = 0;
+  if (g_enc_gemm == 1 && P >= 43 && Ng % 256 == 0) return launch4<EPI_DSC>(a, st);
   return launch<EPI_DSC, 128, 128>(a, st);
 }
 
 extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
                                        int64_t kscale, const void* Wt, const float* bias, int64_t N,
                                        long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 && kscale % BK == 0 &&
-                  kscale <= K,
-              "enc_transition_gemm: need P >= 32, K %% 32 == 0, N %% 256 == 0, kscale %% 32 == 0");
+  TRK_REQUIRE(M >= 0 && P >= 32 && P <= 256 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 &&
+                  kscale % BK == 0 && kscale <= K,
+              "enc_transition_gemm: need 32 <= P <= 256, K %% 32 == 0, N %% 256 == 0, kscale %% 32 == 0");
   if (M == 0) return TRK_OK;
   TRK_REQUIRE(XRN && s && Wt && bias && sums && aligned16(XRN) && aligned16(Wt) && aligned16(s),
               "enc_transition_gemm: null or unaligned pointer");
-  const int64_t nroi = (M + P - 1) / P;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(sums, 0, sizeof(long long) * nroi * N, st) != hipSuccess) {
-    trk::set_error("enc_transition_gemm: memset failed");
-    return TRK_ELAUNCH;
-  }
   EncGemmArgs a{};
   a.A = (const uint16_t*)XRN; a.lda = K;
   a.B = (const uint16_t*)Wt; a.bias = bias;
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
+  if (g_enc_gemm == 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
   return launch<EPI_TRANS, 128, 256>(a, st);
 }
 

@@ -26,60 +26,82 @@ constexpr int RB = 16;        // ROIs per workgroup
 constexpr int NWAVE = 8;
 constexpr int MAXC = 1024;    // channel bound (LDS sizing)
 
-// acc[t] (t < nt) += X[16][K] . W[n0 + 16 t .. + 15][K]^T
-__device__ __forceinline__ void rb_gemm4(const float* __restrict__ Xs, int ldx, const float* __restrict__ W,
-                                         int64_t ldw, int n0, int nt, int K, f4_t (&acc)[4]) {
-  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const float* wp[4];
+// acc[t] (t < NT) += X[16][K] . W[n0 + 16 t .. + 15][K]^T.  K is walked in
+// chunks of U blocks of 16 whose weight loads (NT x U 16-B loads per lane) are
+// all issued before the chunk's first MFMA: one L2 round trip per chunk
+// instead of one per block (the loop is latency-bound otherwise).  NT and U are
+// compile-time so the loads / MFMAs are straight-line code.
+template <int NT, int U>
+__device__ __forceinline__ void rb_chunk(const float* xp, const float* const (&wp)[NT], int kb0, f4_t (&acc)[NT]) {
+  float4 a[U], b[U][NT];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) wp[t] = W + (int64_t)(n0 + 16 * min(t, nt - 1) + r) * ldw + 4 * g;
-  const float* xp = Xs + r * ldx + 4 * g;
-#pragma unroll 2
-  for (int kb = 0; kb < K; kb += 16) {
-    const float4 a = *reinterpret_cast<const float4*>(xp + kb);
-    float4 b[4];
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) b[t] = *reinterpret_cast<const float4*>(wp[t] + kb);
+    for (int t = 0; t < NT; ++t) b[u][t] = *reinterpret_cast<const float4*>(wp[t] + kb0 + 16 * u);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < nt) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[t].x, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[t].y, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[t].z, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[t].w, acc[t], 0, 0, 0);
-      }
+  for (int u = 0; u < U; ++u) a[u] = *reinterpret_cast<const float4*>(xp + kb0 + 16 * u);
+  // keep every load of the chunk ahead of its MFMAs (the scheduler would otherwise
+  // interleave them to save registers and re-serialise the round trips)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, b[u][t].x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, b[u][t].y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, b[u][t].z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, b[u][t].w, acc[t], 0, 0, 0);
     }
+}
+
+template <int NT>
+__device__ __forceinline__ void rb_gemm(const float* __restrict__ Xs, int ldx, const float* __restrict__ W,
+                                        int64_t ldw, int n0, int K, f4_t (&acc)[NT]) {
+  constexpr int U = NT >= 4 ? 8 : 16;  // <= 32 weight loads in flight per lane
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const float* wp[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) wp[t] = W + (int64_t)(n0 + 16 * t + r) * ldw + 4 * g;
+  const float* xp = Xs + r * ldx + 4 * g;
+  int kb = 0;
+  for (; kb + 16 * U <= K; kb += 16 * U) rb_chunk<NT, U>(xp, wp, kb, acc);
+  for (; kb < K; kb += 16) rb_chunk<NT, 1>(xp, wp, kb, acc);
+}
+
+// Y[16][N] = epi(col, X[16][K] . W[N][K]^T + bias) -> per-element store
+// callback, column tiles of 16 spread over the 8 waves (runs of 4, then singles).
+template <int NT, class Store>
+__device__ __forceinline__ void rb_tiles(const float* Xs, int ldx, const float* W, const float* bias, int K,
+                                         int t0, Store store) {
+  const int lane = threadIdx.x & 63;
+  f4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_t{0.f, 0.f, 0.f, 0.f};
+  rb_gemm<NT>(Xs, ldx, W, K, t0 * 16, K, acc);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = (t0 + t) * 16 + (lane & 15);
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) store(4 * (lane >> 4) + i, col, acc[t][i] + bv);
   }
 }
 
-// Y[16][N] = epi(X[16][K] . W[N][K]^T + bias) into LDS (ldy), tiles spread over
-// the 8 waves in runs of <= 4.  epi(col, v) is applied per element.
-template <class Epi>
+template <class Store>
 __device__ __forceinline__ void rb_linear(const float* Xs, int ldx, const float* W, const float* bias, int N,
-                                          int K, float* Ys, int ldy, Epi epi) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                          int K, Store store) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntile = N / 16;
   const int per = (ntile + NWAVE - 1) / NWAVE;
   const int t_begin = wave * per, t_end = min(ntile, t_begin + per);
-  for (int t0 = t_begin; t0 < t_end; t0 += 4) {
-    const int nt = min(4, t_end - t0);
-    f4_t acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f4_t{0.f, 0.f, 0.f, 0.f};
-    rb_gemm4(Xs, ldx, W, K, t0 * 16, nt, K, acc);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < nt) {
-        const int col = (t0 + t) * 16 + (lane & 15);
-        const float bv = bias ? bias[col] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 4 * (lane >> 4) + i;
-          Ys[row * ldy + col] = epi(col, acc[t][i] + bv);
-        }
-      }
-    }
-  }
+  int t0 = t_begin;
+  for (; t0 + 4 <= t_end; t0 += 4) rb_tiles<4>(Xs, ldx, W, bias, K, t0, store);
+  for (; t0 < t_end; ++t0) rb_tiles<1>(Xs, ldx, W, bias, K, t0, store);
+}
+
+// number of 128-row GEMM tiles covering ROI roi (its partial sums, trk_amd.h)
+__device__ __forceinline__ int part_count(int64_t roi, int P) {
+  return (int)((roi * P + P - 1) / 128 - roi * P / 128) + 1;
 }
 
 __device__ __forceinline__ float fix_mean(long long v, float P) {
@@ -92,7 +114,7 @@ struct SeArgs {
   int64_t ld_sums;
   const float *w1, *b1, *w2, *b2;
   float *m_r, *m_n, *s;
-  int R, C, H;
+  int R, C, H, Pi;
   float P;
 };
 
@@ -103,43 +125,41 @@ __global__ void __launch_bounds__(512) enc_se_kernel(const SeArgs a) {
   float* Hs = lds + RB * ldx;      // [16][H + 4] relu(W1 m_r + b1)
   const int64_t r0 = (int64_t)blockIdx.x * RB;
   const int nrow = (int)min<int64_t>(RB, a.R - r0);
-  for (int q = threadIdx.x; q < RB * C; q += blockDim.x) {
-    const int rr = q / C, c = q % C;
-    float mr = 0.f;
+  // 4 channels per item, all of a thread's loads in flight together
+  const int C4 = C / 4;
+#pragma unroll 4
+  for (int q = threadIdx.x; q < RB * C4; q += blockDim.x) {
+    const int rr = q / C4, c = (q % C4) * 4;
+    float4 mr = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rr < nrow) {
-      const long long* sp = a.sums + (r0 + rr) * a.ld_sums;
-      mr = fix_mean(sp[c], a.P);
-      a.m_r[(r0 + rr) * C + c] = mr;
-      a.m_n[(r0 + rr) * C + c] = fix_mean(sp[C + c], a.P);
+      // the ROI's 1..3 partial sums (one per 128-row tile of the DSC GEMM)
+      const int64_t roi = r0 + rr;
+      const int cnt = part_count(roi, a.Pi);
+      longlong2 r01 = {0, 0}, r23 = {0, 0}, n01 = {0, 0}, n23 = {0, 0};
+      for (int j = 0; j < cnt; ++j) {
+        const long long* __restrict__ sp = a.sums + (roi * TRK_ENC_PARTS + j) * a.ld_sums + c;
+        const longlong2 x0 = *reinterpret_cast<const longlong2*>(sp);
+        const longlong2 x1 = *reinterpret_cast<const longlong2*>(sp + 2);
+        const longlong2 y0 = *reinterpret_cast<const longlong2*>(sp + C);
+        const longlong2 y1 = *reinterpret_cast<const longlong2*>(sp + C + 2);
+        r01.x += x0.x; r01.y += x0.y; r23.x += x1.x; r23.y += x1.y;
+        n01.x += y0.x; n01.y += y0.y; n23.x += y1.x; n23.y += y1.y;
+      }
+      mr = make_float4(fix_mean(r01.x, a.P), fix_mean(r01.y, a.P), fix_mean(r23.x, a.P), fix_mean(r23.y, a.P));
+      *reinterpret_cast<float4*>(a.m_r + (r0 + rr) * C + c) = mr;
+      *reinterpret_cast<float4*>(a.m_n + (r0 + rr) * C + c) =
+          make_float4(fix_mean(n01.x, a.P), fix_mean(n01.y, a.P), fix_mean(n23.x, a.P), fix_mean(n23.y, a.P));
     }
-    Xs[rr * ldx + c] = mr;
+    *reinterpret_cast<float4*>(Xs + rr * ldx + c) = mr;
   }
   __syncthreads();
-  rb_linear(Xs, ldx, a.w1, a.b1, H, C, Hs, ldh, [](int, float v) { return fmaxf(v, 0.f); });
+  rb_linear(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[row * ldh + col] = fmaxf(v, 0.f); });
   __syncthreads();
   // hardsigmoid (torch: min(max(x + 3, 0), 6) / 6), straight to global
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ntile = C / 16, per = (ntile + NWAVE - 1) / NWAVE;
-  const int t_begin = wave * per, t_end = min(ntile, t_begin + per);
-  for (int t0 = t_begin; t0 < t_end; t0 += 4) {
-    const int nt = min(4, t_end - t0);
-    f4_t acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f4_t{0.f, 0.f, 0.f, 0.f};
-    rb_gemm4(Hs, ldh, a.w2, H, t0 * 16, nt, H, acc);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < nt) {
-        const int col = (t0 + t) * 16 + (lane & 15);
-        const float bv = a.b2[col];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 4 * (lane >> 4) + i;
-          if (row < nrow) a.s[(r0 + row) * C + col] = fminf(fmaxf(acc[t][i] + bv + 3.0f, 0.f), 6.0f) / 6.0f;
-        }
-      }
-    }
-  }
+  float* __restrict__ sout = a.s;
+  rb_linear(Hs, ldh, a.w2, a.b2, C, H, [&](int row, int col, float v) {
+    if (row < nrow) sout[(r0 + row) * C + col] = fminf(fmaxf(v + 3.0f, 0.f), 6.0f) / 6.0f;
+  });
 }
 
 struct HeadArgs {
@@ -147,7 +167,7 @@ struct HeadArgs {
   const float *s, *m_r, *m_n;
   const float *w0, *ln_w, *ln_b, *w4, *b4;
   float* out;
-  int R, C, D;
+  int R, C, D, Pi;
   float P, eps;
   double alpha;
 };
@@ -160,21 +180,40 @@ __global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
   float* Ys = Zs + RB * ldx;        // [16][D + 4] W4 . + b4
   const int64_t r0 = (int64_t)blockIdx.x * RB;
   const int nrow = (int)min<int64_t>(RB, a.R - r0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float al = (float)a.alpha, bl = (float)(1.0 - a.alpha);  // torch: a * (.), (1 - a) * (.)
-  for (int q = threadIdx.x; q < RB * C; q += blockDim.x) {
-    const int rr = q / C, c = q % C;
-    float gv = 0.f;
+  const int C4 = C / 4;
+#pragma unroll 4
+  for (int q = threadIdx.x; q < RB * C4; q += blockDim.x) {
+    const int rr = q / C4, c = (q % C4) * 4;
+    float gv[4] = {0.f, 0.f, 0.f, 0.f};
     if (rr < nrow) {
       const int64_t o = (r0 + rr) * C + c;
-      const float mcat = fix_mean(a.tsums[o], a.P);
-      const float x2 = al * (a.s[o] * a.m_r[o]) + bl * a.m_n[o];
-      gv = 0.5f * mcat + 0.5f * x2;
+      const int cnt = part_count(r0 + rr, a.Pi);
+      longlong2 t01 = {0, 0}, t23 = {0, 0};
+      for (int j = 0; j < cnt; ++j) {
+        const long long* __restrict__ tp = a.tsums + ((r0 + rr) * TRK_ENC_PARTS + j) * C + c;
+        const longlong2 x0 = *reinterpret_cast<const longlong2*>(tp);
+        const longlong2 x1 = *reinterpret_cast<const longlong2*>(tp + 2);
+        t01.x += x0.x; t01.y += x0.y; t23.x += x1.x; t23.y += x1.y;
+      }
+      const float4 sv = *reinterpret_cast<const float4*>(a.s + o);
+      const float4 rv = *reinterpret_cast<const float4*>(a.m_r + o);
+      const float4 nv = *reinterpret_cast<const float4*>(a.m_n + o);
+      const long long tv[4] = {t01.x, t01.y, t23.x, t23.y};
+      const float s4[4] = {sv.x, sv.y, sv.z, sv.w}, r4[4] = {rv.x, rv.y, rv.z, rv.w};
+      const float n4[4] = {nv.x, nv.y, nv.z, nv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float mcat = fix_mean(tv[e], a.P);
+        const float x2 = al * (s4[e] * r4[e]) + bl * n4[e];
+        gv[e] = 0.5f * mcat + 0.5f * x2;
+      }
     }
-    Gs[rr * ldx + c] = gv;
+    *reinterpret_cast<float4*>(Gs + rr * ldx + c) = make_float4(gv[0], gv[1], gv[2], gv[3]);
   }
   __syncthreads();
-  rb_linear(Gs, ldx, a.w0, nullptr, C, C, Zs, ldx, [](int, float v) { return v; });
+  rb_linear(Gs, ldx, a.w0, nullptr, C, C, [&](int row, int col, float v) { Zs[row * ldx + col] = v; });
   __syncthreads();
   // LayerNorm over C (biased variance, eps inside the sqrt) + SiLU: wave w owns rows 2w, 2w + 1
   for (int rr = 2 * wave; rr < 2 * wave + 2; ++rr) {
@@ -198,7 +237,7 @@ __global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
     }
   }
   __syncthreads();
-  rb_linear(Gs, ldx, a.w4, a.b4, D, C, Ys, ldd, [](int, float v) { return v; });
+  rb_linear(Gs, ldx, a.w4, a.b4, D, C, [&](int row, int col, float v) { Ys[row * ldd + col] = v; });
   __syncthreads();
   // F.normalize(dim=1): y / max(||y||, 1e-12)
   for (int rr = 2 * wave; rr < 2 * wave + 2; ++rr) {
@@ -213,17 +252,21 @@ __global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
   }
 }
 
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 }  // namespace
 
 extern "C" int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int64_t P, int64_t C,
                           const float* w1, const float* b1, int64_t H, const float* w2, const float* b2,
                           float* m_r, float* m_n, float* s, void* stream) {
-  TRK_REQUIRE(R >= 0 && P > 0 && C > 0 && C % 16 == 0 && C <= MAXC && H > 0 && H % 16 == 0 && H <= MAXC &&
-                  ld_sums >= 2 * C,
-              "enc_se: need C, H multiples of 16 in [16, %d], ld_sums >= 2C", MAXC);
+  TRK_REQUIRE(R >= 0 && P > 0 && P <= 256 && C > 0 && C % 16 == 0 && C <= MAXC && H > 0 && H % 16 == 0 && H <= MAXC &&
+                  ld_sums >= 2 * C && ld_sums % 2 == 0,
+              "enc_se: need C, H multiples of 16 in [16, %d], ld_sums >= 2C and even", MAXC);
   if (R == 0) return TRK_OK;
   TRK_REQUIRE(sums && w1 && b1 && w2 && b2 && m_r && m_n && s, "enc_se: null pointer");
-  SeArgs a{sums, ld_sums, w1, b1, w2, b2, m_r, m_n, s, (int)R, (int)C, (int)H, (float)P};
+  TRK_REQUIRE(al16(sums) && al16(w1) && al16(w2) && al16(m_r) && al16(m_n) && al16(s),
+              "enc_se: operands must be 16-byte aligned");
+  SeArgs a{sums, ld_sums, w1, b1, w2, b2, m_r, m_n, s, (int)R, (int)C, (int)H, (int)P, (float)P};
   const size_t lds = (size_t)RB * ((C + 4) + (H + 4)) * 4;
   static bool attr = false;
   if (!attr) {
@@ -240,11 +283,14 @@ extern "C" int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_
                             const float* m_r, const float* m_n, double alpha, const float* w0, const float* ln_w,
                             const float* ln_b, float ln_eps, const float* w4, const float* b4, int64_t D,
                             float* out, void* stream) {
-  TRK_REQUIRE(R >= 0 && P > 0 && C > 0 && C % 16 == 0 && C <= MAXC && D > 0 && D % 16 == 0 && D <= MAXC,
-              "enc_head: need C, D multiples of 16 in [16, %d]", MAXC);
+  TRK_REQUIRE(R >= 0 && P > 0 && P <= 256 && C > 0 && C % 16 == 0 && C <= MAXC && D > 0 && D % 16 == 0 &&
+                  D <= MAXC,
+              "enc_head: need P <= 256, C, D multiples of 16 in [16, %d]", MAXC);
   if (R == 0) return TRK_OK;
   TRK_REQUIRE(tsums && s && m_r && m_n && w0 && ln_w && ln_b && w4 && b4 && out, "enc_head: null pointer");
-  HeadArgs a{tsums, s, m_r, m_n, w0, ln_w, ln_b, w4, b4, out, (int)R, (int)C, (int)D, (float)P, ln_eps, alpha};
+  TRK_REQUIRE(al16(tsums) && al16(s) && al16(m_r) && al16(m_n) && al16(w0) && al16(w4),
+              "enc_head: operands must be 16-byte aligned");
+  HeadArgs a{tsums, s, m_r, m_n, w0, ln_w, ln_b, w4, b4, out, (int)R, (int)C, (int)D, (int)P, (float)P, ln_eps, alpha};
   const size_t lds = (size_t)RB * (2 * (C + 4) + (D + 4)) * 4;
   static bool attr = false;
   if (!attr) {

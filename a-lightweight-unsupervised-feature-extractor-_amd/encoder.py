@@ -182,7 +182,7 @@ class Model(nn.Module):
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_transition_gemm, enc_se, enc_head)
+                          enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -211,7 +211,7 @@ class Model(nn.Module):
                 tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
                 return enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                 self.head.net[1].eps, W["h4"], W["h4b"])
-            f = (sums.double() * 2.0 ** -24).float()
+            f = enc_sums_reduce(sums, ss)
             m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
             s = self._se(m_r)
             m_cat = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"]) / ss

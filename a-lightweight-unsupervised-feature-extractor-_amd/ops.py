@@ -152,12 +152,12 @@ def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor,
     Y2, W2, bias = Y2.contiguous(), W2.contiguous(), bias.to(torch.float32).contiguous()
     R = (M + P - 1) // P
     XRN = torch.empty((M, 2 * Ng), device=Y2.device, dtype=torch.bfloat16)
-    sums = torch.empty((R, 2 * Ng), device=Y2.device, dtype=torch.int64)
+    sums = torch.empty((R, _lib.TRK_ENC_PARTS, 2 * Ng), device=Y2.device, dtype=torch.int64)  # partials
     check(lib().trk_enc_dsc_gemm(_ptr(Y2), M, P, Kg, _ptr(W2), _ptr(bias), Ng, _ptr(XRN), _ptr(sums),
                                  _stream(Y2.device)), "enc_dsc_gemm")
     if raw:
         return XRN, sums
-    f = (sums.double() * _FIX).float()
+    f = enc_sums_reduce(sums, P)
     return XRN, f[:, :Ng], f[:, Ng:]
 
 
@@ -176,12 +176,25 @@ def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Te
         raise ValueError("enc_transition_gemm: shape mismatch")
     XRN, Wt = XRN.contiguous(), Wt.contiguous()
     s, bias = s.to(torch.float32).contiguous(), bias.to(torch.float32).contiguous()
-    sums = torch.empty((R, N), device=XRN.device, dtype=torch.int64)
+    sums = torch.empty((R, _lib.TRK_ENC_PARTS, N), device=XRN.device, dtype=torch.int64)  # partials
     check(lib().trk_enc_transition_gemm(_ptr(XRN), M, P, K, _ptr(s), s.shape[1], _ptr(Wt), _ptr(bias), N,
                                         _ptr(sums), _stream(XRN.device)), "enc_transition_gemm")
     if raw:
         return sums
-    return (sums.double() * _FIX).float()
+    return enc_sums_reduce(sums, P)
+
+
+def enc_sums_reduce(part: torch.Tensor, P: int) -> torch.Tensor:
+    """Total per-ROI sums from the GEMMs' int64 partials [R, TRK_ENC_PARTS, ld]
+    (one per 128-row tile covering the ROI): [R, ld] f32 = (sum * 2^-24)."""
+    _need_gpu(part, "enc_sums_reduce")
+    if part.dtype != torch.int64 or part.dim() != 3 or part.shape[1] != _lib.TRK_ENC_PARTS:
+        raise TypeError("enc_sums_reduce: part must be [R, TRK_ENC_PARTS, ld] int64")
+    part = part.contiguous()
+    R, _, ld = part.shape
+    out = torch.empty((R, ld), device=part.device, dtype=torch.float32)
+    check(lib().trk_enc_sums_reduce(_ptr(part), R, P, ld, _ptr(out), _stream(part.device)), "enc_sums_reduce")
+    return out
 
 
 def _f32c(t: torch.Tensor) -> torch.Tensor:
@@ -190,20 +203,21 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
 
 def enc_se(sums: torch.Tensor, P: int, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
            b2: torch.Tensor):
-    """SE squeeze + excitation from enc_dsc_gemm's raw sums [R, 2C] int64:
-    returns (m_r, m_n, s) [R, C] f32 with m = (float)(sum * 2^-24) / P and
-    s = hardsigmoid(w2 . relu(w1 . m_r + b1) + b2) (card.py:59-78)."""
+    """SE squeeze + excitation from enc_dsc_gemm's raw partial sums
+    [R, TRK_ENC_PARTS, 2C] int64: returns (m_r, m_n, s) [R, C] f32 with
+    m = (float)(sum * 2^-24) / P and s = hardsigmoid(w2 . relu(w1 . m_r + b1) + b2)
+    (card.py:59-78)."""
     _need_gpu(sums, "enc_se")
-    if sums.dtype != torch.int64 or sums.dim() != 2:
-        raise TypeError("enc_se: sums must be [R, 2C] int64")
+    if sums.dtype != torch.int64 or sums.dim() != 3 or sums.shape[1] != _lib.TRK_ENC_PARTS:
+        raise TypeError("enc_se: sums must be [R, TRK_ENC_PARTS, 2C] int64 partials")
     H, C = w1.shape
     R = sums.shape[0]
-    if sums.shape[1] < 2 * C or w2.shape != (C, H) or b1.numel() != H or b2.numel() != C:
+    if sums.shape[2] < 2 * C or w2.shape != (C, H) or b1.numel() != H or b2.numel() != C:
         raise ValueError("enc_se: shape mismatch")
     sums = sums.contiguous()
     out = torch.empty((3, R, C), device=sums.device, dtype=torch.float32)
     w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
-    check(lib().trk_enc_se(_ptr(sums), R, sums.stride(0), P, C, _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2),
+    check(lib().trk_enc_se(_ptr(sums), R, sums.stride(1), P, C, _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2),
                            _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _stream(sums.device)), "enc_se")
     return out[0], out[1], out[2]
 
@@ -211,12 +225,12 @@ def enc_se(sums: torch.Tensor, P: int, w1: torch.Tensor, b1: torch.Tensor, w2: t
 def enc_head(tsums: torch.Tensor, P: int, s: torch.Tensor, m_r: torch.Tensor, m_n: torch.Tensor, alpha: float,
              w0: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, ln_eps: float, w4: torch.Tensor,
              b4: torch.Tensor) -> torch.Tensor:
-    """Shake2 eval mix + ProjectionHead from enc_transition_gemm's raw sums
-    [R, C] int64 (card.py:83-96, :151-169): [R, D] f32 unit rows."""
+    """Shake2 eval mix + ProjectionHead from enc_transition_gemm's raw partial
+    sums [R, TRK_ENC_PARTS, C] int64 (card.py:83-96, :151-169): [R, D] f32 unit rows."""
     _need_gpu(tsums, "enc_head")
-    if tsums.dtype != torch.int64 or tsums.dim() != 2:
-        raise TypeError("enc_head: tsums must be [R, C] int64")
-    R, C = tsums.shape
+    if tsums.dtype != torch.int64 or tsums.dim() != 3 or tsums.shape[1] != _lib.TRK_ENC_PARTS:
+        raise TypeError("enc_head: tsums must be [R, TRK_ENC_PARTS, C] int64 partials")
+    R, _, C = tsums.shape
     D = w4.shape[0]
     if (s.shape != (R, C) or m_r.shape != (R, C) or m_n.shape != (R, C) or w0.shape != (C, C) or
             w4.shape[1] != C or b4.numel() != D or ln_w.numel() != C or ln_b.numel() != C):

@@ -201,7 +201,8 @@ class LiveProbe:
     two summing GEMMs (a 4-8 MB hipMemsetAsync of the sums precedes the GEMM)."""
 
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_enc_g1_dwconv": "enc_g1_dwconv",
-             "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans"}
+             "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
+             "trk_enc_se": "enc_se", "trk_enc_head": "enc_head"}
 
     def __init__(self):
         self.on = False
@@ -232,6 +233,14 @@ class LiveProbe:
     def means_us(self):
         torch.cuda.synchronize()
         return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e3 for k, v in self.ev.items() if v}
+
+    def embed_gaps_us(self):
+        """mean time between one frame's last encoder launch ending (enc_head)
+        and the next frame's roi stage starting, on the side stream: the side
+        stream's idle time per frame"""
+        ends, starts = self.ev["enc_head"], self.ev["roi_stage"]
+        gaps = [e1.elapsed_time(s0) * 1e3 for (_, e1), (s0, _) in zip(ends, starts[1:])]
+        return float(np.mean(gaps)) if gaps else None
 
 
 def kernel_pass(pipe, f, reps=10):
@@ -397,6 +406,7 @@ def main():
                                torch.cuda.synchronize, dev)
     probe.on = False
     live = probe.means_us()
+    side_gap = probe.embed_gaps_us()
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
@@ -462,7 +472,8 @@ def main():
           "kernel_us_source": {k: ("live: HIP events around each launch in the timed region" if k in live
                                    else "isolated: back-to-back launches after the timed region") for k in kt},
           "isolated_us": {k: round(v, 2) for k, v in iso.items()},
-          "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2)}
+          "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2),
+          "embed_stream_idle_us_per_step": None if side_gap is None else round(side_gap, 2)}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",
         "value": round(value, 1), "unit": "ROIs/s", "n_gpus": world, "steps": args.steps,

@@ -163,9 +163,13 @@ int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C,
 /* ------------------------------------------------------------------------
  * Fused bf16 encoder GEMMs (RMB of reference card.py:48-148).  A rows are
  * bf16 [M, *] with M = ROIs x P pixels; weights bf16 [N][K] (conv [out, in]).
- * Per-ROI column sums are int64 fixed point (value x 2^24), zeroed by the
- * call and accumulated exactly (order-independent).  Requires P >= 32,
- * K % 32 == 0, N % 256 == 0, 16-B aligned operands.
+ * Per-ROI column sums are int64 fixed point (value x 2^24) PARTIALS
+ * [ROIs][TRK_ENC_PARTS][ld]: entry j holds the sum over the rows of the ROI's
+ * j-th 128-row M tile (j < 1 + (roi*P + P - 1)/128 - roi*P/128); entries past
+ * that count are not written.  The total of a ROI is the integer sum of its
+ * partials (trk_enc_sums_reduce, or inside trk_enc_se / trk_enc_head), so it
+ * does not depend on tile order.  Requires 32 <= P <= 256, K % 32 == 0,
+ * N % 256 == 0, 16-B aligned operands.
  *
  * trk_enc_gemm: plain C[M, N] = A[M, K] . B[N, K]^T in bf16 (row strides lda,
  *   ldc): the four first 1x1 convs of the RMB as one GEMM (card.py:28,38). 
@@ -173,15 +177,18 @@ int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C,
  * trk_enc_dsc_gemm: both DSC 1x1 GEMMs (card.py:53-56, depth.2 + point.2 with
  *   eval-BN folded): Y2 [M, 2*Kg] (reinforce half | normal half), W2
  *   [2][Ng][Kg], bias [2*Ng] -> XRN [M, 2*Ng] = [SiLU(x_r) | Hardswish(x_n)],
- *   sums [ROIs][2*Ng] = per-ROI sums of SiLU(x_r) (SE squeeze, card.py:75)
- *   and Hardswish(x_n) (GAP).
+ *   sums [ROIs][TRK_ENC_PARTS][2*Ng] = per-ROI partial sums of SiLU(x_r) (SE
+ *   squeeze, card.py:75) and Hardswish(x_n) (GAP).
  * trk_enc_transition_gemm: T = [x_f * s | x_n] . Wt^T + bias (card.py:78 +
  *   :138-139) with XRN = [x_f | x_n], the SE scale s[roi] applied to the first
  *   kscale columns while staging; only the per-ROI sums of SiLU(T) are
- *   produced (sums [ROIs][N]); T is never stored.
+ *   produced (partials [ROIs][TRK_ENC_PARTS][N]); T is never stored.
  * ---------------------------------------------------------------------- */
+#define TRK_ENC_PARTS 3
 int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
                  int64_t ldc, void* stream);
+/* out[roi][c] = (float)(sum_j part[roi][j][c] * 2^-24) for the partial sums above. */
+int trk_enc_sums_reduce(const long long* part, int64_t R, int64_t P, int64_t ld, float* out, void* stream);
 /* trk_enc_g1_dwconv: trk_enc_gemm (K = 512) followed by the 1024-channel
  *   depthwise 5x5 (card.py:29,39) in one kernel for 10x10 ROIs (M = ROIs x 100):
  *   Y2 = dwconv5(bf16(X . W1^T)) with weights tap-major [25][N] f32; Y1 never
@@ -194,16 +201,17 @@ int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, co
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
 
 /* Per-ROI tail of the encoder (f32, 16 ROIs per workgroup, f32-input MFMA).
- * trk_enc_se: squeeze means and SE excitation (card.py:59-78) from the sums of
- *   trk_enc_dsc_gemm ([R][ld_sums], ld_sums >= 2C: C sums of SiLU(x_r), then C of
- *   Hardswish(x_n)): m_r, m_n [R][C] = (float)(sum * 2^-24) / P;
+ * trk_enc_se: squeeze means and SE excitation (card.py:59-78) from the partial
+ *   sums of trk_enc_dsc_gemm ([R][TRK_ENC_PARTS][ld_sums], ld_sums >= 2C: C sums
+ *   of SiLU(x_r), then C of Hardswish(x_n)): m_r, m_n [R][C] = (float)(sum *
+ *   2^-24) / P;
  *   s [R][C] = hardsigmoid(w2 . relu(w1 . m_r + b1) + b2), w1 [H][C], w2 [C][H].
  * trk_enc_head: g = 0.5 m_cat + 0.5 (alpha (s m_r) + (1 - alpha) m_n) (Shake2
  *   eval + GAP, card.py:83-96, :128-148; m_cat from the trk_enc_transition_gemm
- *   sums [R][C]) -> ProjectionHead (card.py:151-169): out [R][D] =
+ *   partials [R][TRK_ENC_PARTS][C]) -> ProjectionHead (card.py:151-169): out [R][D] =
  *   normalize(w4 . silu(LayerNorm(w0 . g; ln_w, ln_b, ln_eps)) + b4), w0 [C][C],
  *   w4 [D][C].  Replaces ~25 small torch launches between and after the GEMMs.
- * C, H, D multiples of 16, <= 1024. */
+ * C, H, D multiples of 16, <= 1024; P <= 256. */
 int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int64_t P, int64_t C, const float* w1,
                const float* b1, int64_t H, const float* w2, const float* b2, float* m_r, float* m_n, float* s,
                void* stream);

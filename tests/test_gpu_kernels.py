@@ -377,6 +377,21 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     A = torch.cat([xs, XRN[:, Ng:].float()], 1)
     ref_t = F.silu(A @ Wt.float().t() + bt).view(R, P, Ng).sum(1)
     assert (st - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item()
+    # the pipelined 128 x 256 kernels (default) vs the 128 x 128 / 128 x 256 kernels:
+    # same math, another f32 summation order
+    L = ops.lib()
+    try:
+        assert L.trk_set_tuning(b"enc_gemm", 0) == 0
+        XRN0, sr0, sn0 = ops.enc_dsc_gemm(Y2, P, W2, b2)
+        st0 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+    finally:
+        assert L.trk_set_tuning(b"enc_gemm", 1) == 0
+    assert (XRN0.float() - XRN.float()).abs().max().item() <= 1e-2 * max(1.0, XRN.float().abs().max().item())
+    assert (sr0 - sr).abs().max().item() <= 1e-3 * sr.abs().max().item()
+    assert (sn0 - sn).abs().max().item() <= 1e-3 * sn.abs().max().item()
+    assert (st0 - st).abs().max().item() <= 1e-3 * st.abs().max().item()
+    st2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+    assert torch.equal(st, st2)
     # plain GEMM (the first 1x1 convs), strided A rows
     W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
     A = Y2[:, :512]
@@ -393,6 +408,23 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         assert torch.equal(Yf, Yu)
 
 
+def _partials(total, P, parts=3):
+    """split int64 per-ROI totals [R, ld] into the GEMMs' partial layout
+    [R, parts, ld] (one entry per 128-row tile covering the ROI; the rest junk)"""
+    R, ld = total.shape
+    out = torch.full((R, parts, ld), -(2 ** 40), dtype=torch.int64)  # never read
+    g = torch.Generator().manual_seed(R)
+    for r in range(R):
+        cnt = (r * P + P - 1) // 128 - (r * P) // 128 + 1
+        left = total[r].clone()
+        for j in range(cnt - 1):
+            x = torch.randint(-2 ** 30, 2 ** 30, (ld,), generator=g, dtype=torch.int64)
+            out[r, j] = x
+            left -= x
+        out[r, cnt - 1] = left
+    return out
+
+
 @pytest.mark.parametrize("R", [1, 37, 2048])
 def test_enc_se_head_vs_torch_fp32(trk, gpu, R):
     """trk_enc_se / trk_enc_head vs the same math in torch fp32 (the encoder's own
@@ -407,26 +439,28 @@ def test_enc_se_head_vs_torch_fp32(trk, gpu, R):
     W = m._fused_weights(torch.bfloat16, gpu)
     g = torch.Generator().manual_seed(R)
     P = 100
-    sums = (torch.randn(R, 1024, generator=g) * 40 * 2 ** 24).to(torch.int64).to(gpu)
-    m_r, m_n, s = ops.enc_se(sums, P, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
-    f = (sums.double() * 2.0 ** -24).float()
+    sums = (torch.randn(R, 1024, generator=g) * 40 * 2 ** 24).to(torch.int64)
+    m_r, m_n, s = ops.enc_se(_partials(sums, P).to(gpu), P, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+    f = (sums.double() * 2.0 ** -24).float().to(gpu)
     # correctly rounded f32 division by P (torch's GPU tensor / scalar multiplies by 1/P: <= 1 ulp apart)
     assert torch.allclose(m_r, f[:, :512] / P, rtol=1.2e-7, atol=0)
     assert torch.allclose(m_n, f[:, 512:] / P, rtol=1.2e-7, atol=0)
     with torch.no_grad():
         s_ref = m._se(m_r)
     assert (s - s_ref).abs().max().item() <= 2e-6
-    tsums = (torch.randn(R, 512, generator=g) * 30 * 2 ** 24).to(torch.int64).to(gpu)
+    tsums = (torch.randn(R, 512, generator=g) * 30 * 2 ** 24).to(torch.int64)
+    tpart = _partials(tsums, P).to(gpu)
+    assert torch.equal(ops.enc_sums_reduce(tpart, P), (tsums.double() * 2.0 ** -24).float().to(gpu))
     for a in (0.5, 0.3141592653589793):
-        z = ops.enc_head(tsums, P, s, m_r, m_n, a, W["h0"], W["ln_w"], W["ln_b"], m.head.net[1].eps,
+        z = ops.enc_head(tpart, P, s, m_r, m_n, a, W["h0"], W["ln_w"], W["ln_b"], m.head.net[1].eps,
                          W["h4"], W["h4b"])
-        m_cat = (tsums.double() * 2.0 ** -24).float() / P
+        m_cat = (tsums.double() * 2.0 ** -24).float().to(gpu) / P
         with torch.no_grad():
             z_ref = m._head(0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n))
         assert z.shape == (R, 128)
         assert (z - z_ref).abs().max().item() <= 2e-5, a
     # deterministic
-    z2 = ops.enc_head(tsums, P, s, m_r, m_n, a, W["h0"], W["ln_w"], W["ln_b"], m.head.net[1].eps,
+    z2 = ops.enc_head(tpart, P, s, m_r, m_n, a, W["h0"], W["ln_w"], W["ln_b"], m.head.net[1].eps,
                       W["h4"], W["h4b"])
     assert torch.equal(z, z2)
 
