@@ -9,6 +9,8 @@ Feature-Extractor- (reference tracking.py:193-329, model/mainTracking.py):
   hungarian_assign / linear_sum_assignment hung.py / scipy LSAP (HIP SAP)
   Tracking                                 mainTracking.Tracking
   MultiStreamTracker                       device-resident multi-stream tracker
+  non_max_suppression / YoloPostprocess    YOLOv7 post-processing (HIP NMS)
+  preprocess_roi                           PreProcess._preprocess_roi (training ROIs)
 
 Import with importlib (the directory name is not an identifier):
     trk = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd")
@@ -20,9 +22,12 @@ from .hung import hungarian_assign
 from .costcard import cal_cost, bbox_cost, conf_cost
 from .encoder import Model
 from .tracking import Tracking, MultiStreamTracker, TrackTable, tracker_conf, load_conf
+from .detect import (letterbox_geometry, scale_coords_params, non_max_suppression, det_nms_batched,
+                     YoloPostprocess, preprocess_roi, train_rois)
 
 __all__ = ["TrkError", "lib", "header_symbols", "roi_align", "roi_align_from_input_boxes",
            "build_cost", "cost_combine", "lsap_batched", "linear_sum_assignment",
            "default_cost_params", "CostParams", "hungarian_assign", "cal_cost", "bbox_cost",
            "conf_cost", "Model", "Tracking", "MultiStreamTracker", "TrackTable", "tracker_conf",
-           "load_conf"]
+           "load_conf", "letterbox_geometry", "scale_coords_params", "non_max_suppression",
+           "det_nms_batched", "YoloPostprocess", "preprocess_roi", "train_rois"]

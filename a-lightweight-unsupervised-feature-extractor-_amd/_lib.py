@@ -92,8 +92,18 @@ def _declare(L):
         fn.restype = res
 
 
-# entry points added by later modules register here before first load
+# entry points added by later modules register here (register() also declares them
+# on an already-loaded library)
 _EXTRA: dict = {}
+
+
+def register(entries: dict):
+    _EXTRA.update(entries)
+    if _lib is not None:
+        for name, (args, res) in entries.items():
+            fn = getattr(_lib, name)
+            fn.argtypes = args
+            fn.restype = res
 
 
 def lib():

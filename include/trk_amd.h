@@ -254,6 +254,39 @@ int trk_track_init(int64_t n, const int32_t* slots, const int32_t* dets, const f
                    float* last_conf, float* enc, float* bank, int32_t* bank_len,
                    int32_t* bank_head, int64_t T, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Detector-side boundary.
+ *
+ * YOLOv7 post-processing as YoloDetects.run_with_tensor applies it
+ * (reference model/yolov7/yoloDetects2.py:111-160) to the raw head output
+ * pred [B][A][no] f32 (no = 5 + nc: cx, cy, w, h, obj, cls...):
+ *   cand_count[b] = #(obj > conf_thres)              yoloDetects2.py:124-125
+ *   if cand_count < cand_gate: no detections          :127-129
+ *   else non_max_suppression(pred, conf_thres, iou_thres)  general.py:608-700
+ *        (defaults: best class only, class-offset batched NMS with
+ *        max_wh 4096 unless agnostic, torchvision nms, first max_det kept)
+ *   det[b][k] = (x1, y1, x2, y2, conf, cls) in input (letterbox) pixels,
+ *   k < det_count[b], in keep order (descending conf).
+ *   xywh (optional, may be NULL): scale_coords(img1, det, img0).round() then
+ *   xyxy2xywh (general.py:320-341, :255-262), with host_scale = {gain, pad_w,
+ *   pad_h, img0_w, img0_h} (the Python doubles of scale_coords; HOST array).
+ * workspace: >= trk_det_workspace_bytes(B, A), 16-B aligned; B <= 32.
+ * Numerics: the reference CPU path (torch CPU kernels; torchvision 0.20.1 CPU
+ * nms with its stable descending score sort), bit-exact.
+ * ---------------------------------------------------------------------- */
+size_t trk_det_workspace_bytes(int64_t B, int64_t A);
+int trk_det_nms(const float* pred, int64_t B, int64_t A, int64_t no, float conf_thres, double iou_thres,
+                int max_det, int max_nms, int agnostic, int cand_gate, float* det, int32_t* det_count,
+                int32_t* cand_count, const float* host_scale, float* xywh, void* workspace,
+                size_t workspace_bytes, void* stream);
+/* PreProcess._preprocess_roi box preparation (reference
+ * model/utils/trainingScr/trainingCard.py:24-79): boxes [N][4] image xyxy ->
+ * rois [N][5] = (0, x1, y1, x2, y2) in feature pixels (sorted corners, scale
+ * Wf/img_w and Hf/img_h, clamp to [0, W-1], minimum size enforce_min_size if
+ * > 0), for trk_roi_align_fwd with spatial_scale = 1. */
+int trk_train_rois(const float* boxes, int64_t N, int64_t Hf, int64_t Wf, double img_h, double img_w,
+                   float enforce_min_size, float* rois, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

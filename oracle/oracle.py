@@ -18,6 +18,13 @@ Contents
   encoder_forward(sd, x)  plain-torch fp32 restatement of the encoder eval graph
                           (encoderAndHead.py:21-26, card.py:48-169), pinned
                           against tests/golden/encoder_golden.npz.
+  det_nms(pred, ...)      ora_det_nms: YOLOv7 non_max_suppression defaults +
+                          torchvision CPU nms + scale_coords/xyxy2xywh
+                          (general.py:255-341,608-700; yoloDetects2.py:111-160).
+                          torchvision absent: pinned by KATs in tests/test_detect.py.
+  train_rois(...)         PreProcess._preprocess_roi box preparation
+                          (trainingCard.py:24-69) in numpy f32; unpinned by a
+                          reference run (torchvision/cv2 imports), KATs only.
   KalmanFilterRestated    filterpy 1.4.5 KalmanFilter predict/update restated
                           (third-party, absent from reference + image; used
                           via KalmanFilter.py:57-101).
@@ -56,6 +63,9 @@ def lib():
         L.ora_cost_build.restype = None
         L.ora_cost_combine.argtypes = [P, i, i, P, P, P, P, P, P, P, P, P, P, P, P]
         L.ora_cost_combine.restype = None
+        L.ora_det_nms.argtypes = [P, ctypes.c_int64, i, ctypes.c_float, ctypes.c_double, i, i, i, i,
+                                  P, P, P, P]
+        L.ora_det_nms.restype = i
         L.ora_lsap.argtypes = [P, ctypes.c_int64, ctypes.c_int64, P, P]
         L.ora_lsap.restype = ctypes.c_int
         _lib = L
@@ -276,3 +286,38 @@ class KalmanFilterRestated:
         self.z = z.copy()
         self.x_post = self.x.copy()
         self.P_post = self.P.copy()
+
+
+def det_nms(pred: np.ndarray, conf_thres: float = 0.4, iou_thres: float = 0.45, *, max_det: int = 300,
+            max_nms: int = 30000, agnostic: bool = False, cand_gate: int = 0, scale=None):
+    """One image: pred [A, no] f32 -> (det [k, 6], xywh [k, 4] or None, cand_count)."""
+    pred = np.ascontiguousarray(pred, dtype=np.float32)
+    A, no = pred.shape
+    det = np.zeros((max_det, 6), np.float32)
+    xywh = np.zeros((max_det, 4), np.float32) if scale is not None else None
+    sc = np.asarray(scale, np.float32) if scale is not None else None
+    cand = ctypes.c_int(0)
+    k = lib().ora_det_nms(_p(pred), A, no, float(conf_thres), float(iou_thres), max_det, max_nms,
+                          int(agnostic), cand_gate, _p(sc) if sc is not None else None, _p(det),
+                          _p(xywh) if xywh is not None else None, ctypes.byref(cand))
+    return det[:k], (xywh[:k] if xywh is not None else None), cand.value
+
+
+def train_rois(boxes: np.ndarray, Hf: int, Wf: int, img_hw, enforce_min_size: float = 1.0) -> np.ndarray:
+    """PreProcess._preprocess_roi (trainingCard.py:36-69) box preparation, f32 numpy ops in the
+    reference's order: [N, 4] image xyxy -> [N, 5] rois in feature pixels."""
+    b = np.asarray(boxes, np.float32).reshape(-1, 4)
+    img_h, img_w = img_hw
+    f = np.float32
+    with np.errstate(invalid="ignore"):
+        x1 = np.minimum(b[:, 0], b[:, 2]); y1 = np.minimum(b[:, 1], b[:, 3])
+        x2 = np.maximum(b[:, 0], b[:, 2]); y2 = np.maximum(b[:, 1], b[:, 3])
+        sx, sy = f(Wf / float(img_w)), f(Hf / float(img_h))
+        x1, x2, y1, y2 = x1 * sx, x2 * sx, y1 * sy, y2 * sy
+        cl = lambda v, hi: np.where(np.isnan(v), v, np.minimum(np.maximum(v, f(0)), f(hi)))
+        x1, x2, y1, y2 = cl(x1, Wf - 1), cl(x2, Wf - 1), cl(y1, Hf - 1), cl(y2, Hf - 1)
+        if enforce_min_size > 0:
+            ms = f(enforce_min_size)
+            x2 = cl(np.maximum(x2, x1 + ms), Wf - 1)
+            y2 = cl(np.maximum(y2, y1 + ms), Hf - 1)
+    return np.stack([np.zeros_like(x1), x1, y1, x2, y2], 1).astype(np.float32)

@@ -348,3 +348,124 @@ done:
   free(SR); free(SC); free(rem); free(tmp);
   return status;
 }
+
+/* ------------------------------------------------------------------------ */
+/* YOLOv7 post-processing, one image, restated literally:                    */
+/*   non_max_suppression (reference model/yolov7/utils/general.py:608-700)   */
+/*   with its defaults (classes None, agnostic False unless asked,           */
+/*   multi_label False, labels ()); torchvision 0.20.1 CPU nms               */
+/*   (nms_kernel.cpp: stable descending score sort, greedy suppression with  */
+/*   `ovr > iou_threshold` in double); scale_coords(...).round() and         */
+/*   xyxy2xywh (general.py:320-341, :255-262) as run_with_tensor applies     */
+/*   them (yoloDetects2.py:136-148).  torchvision is absent: parity pinned   */
+/*   by the known-answer tests in tests/test_detect.py only.                 */
+/* pred [A][no] f32.  Returns the number of kept rows; det [max_det][6],     */
+/* xywh [max_det][4] (xywh may be NULL); *cand = #(obj > conf_thres).        */
+/* ------------------------------------------------------------------------ */
+typedef struct { float conf; int64_t idx; } ora_sc;
+
+static int cmp_sc(const void* a, const void* b) {   /* conf desc, then position (stable) */
+  const ora_sc* x = (const ora_sc*)a;
+  const ora_sc* y = (const ora_sc*)b;
+  if (x->conf > y->conf) return -1;
+  if (x->conf < y->conf) return 1;
+  return (x->idx > y->idx) - (x->idx < y->idx);
+}
+
+static float std_maxf(float a, float b) { return (a < b) ? b : a; }
+static float std_minf(float a, float b) { return (b < a) ? b : a; }
+
+int ora_det_nms(const float* pred, int64_t A, int no, float conf_thres, double iou_thres,
+                int max_det, int max_nms, int agnostic, int cand_gate,
+                const float* scale /* gain, pad_w, pad_h, img0_w, img0_h or NULL */,
+                float* det, float* xywh, int* cand) {
+  const int nc = no - 5;
+  int64_t ncand = 0, n = 0;
+  for (int64_t a = 0; a < A; ++a) ncand += pred[a * no + 4] > conf_thres;
+  *cand = (int)ncand;
+  if (ncand < cand_gate) return 0;
+  float* x = (float*)malloc((size_t)(ncand ? ncand : 1) * 6 * sizeof(float));
+  for (int64_t a = 0; a < A; ++a) {
+    const float* r = pred + a * no;
+    if (!(r[4] > conf_thres)) continue;           /* x = x[xc[xi]] */
+    /* x[:, 5:] *= x[:, 4:5] (nc == 1: = x[:, 4:5]); conf, j = x[:, 5:].max(1) */
+    float best = nc == 1 ? r[4] : r[5] * r[4];
+    int bj = 0, nan = best != best;
+    for (int c = 1; c < nc; ++c) {
+      const float v = r[5 + c] * r[4];
+      if (v != v) nan = 1;
+      else if (v > best) { best = v; bj = c; }
+    }
+    if (nan || !(best > conf_thres)) continue;   /* [conf.view(-1) > conf_thres] */
+    float* o = x + n * 6;
+    o[0] = r[0] - r[2] / 2.0f; o[1] = r[1] - r[3] / 2.0f;   /* xywh2xyxy */
+    o[2] = r[0] + r[2] / 2.0f; o[3] = r[1] + r[3] / 2.0f;
+    o[4] = best; o[5] = (float)bj;
+    ++n;
+  }
+  int kept = 0;
+  if (n > 0) {
+    ora_sc* ord = (ora_sc*)malloc((size_t)n * sizeof(ora_sc));
+    for (int64_t i = 0; i < n; ++i) { ord[i].conf = x[i * 6 + 4]; ord[i].idx = i; }
+    qsort(ord, (size_t)n, sizeof(ora_sc), cmp_sc);
+    int64_t m = n;
+    if (n > max_nms) {                            /* x = x[argsort(desc)[:max_nms]] */
+      m = max_nms;
+      float* y = (float*)malloc((size_t)m * 6 * sizeof(float));
+      for (int64_t i = 0; i < m; ++i) memcpy(y + i * 6, x + ord[i].idx * 6, 6 * sizeof(float));
+      free(x);
+      x = y;
+      for (int64_t i = 0; i < m; ++i) { ord[i].conf = x[i * 6 + 4]; ord[i].idx = i; }
+    }
+    /* boxes = x[:, :4] + x[:, 5:6] * max_wh; torchvision nms (CPU) */
+    float* bx = (float*)malloc((size_t)m * 5 * sizeof(float));
+    for (int64_t i = 0; i < m; ++i) {
+      const float c = agnostic ? 0.0f : x[i * 6 + 5] * 4096.0f;
+      for (int e = 0; e < 4; ++e) bx[i * 5 + e] = x[i * 6 + e] + c;
+      bx[i * 5 + 4] = (bx[i * 5 + 2] - bx[i * 5 + 0]) * (bx[i * 5 + 3] - bx[i * 5 + 1]);  /* areas */
+    }
+    /* order = scores.sort(stable, descending); ord already is that order */
+    char* sup = (char*)calloc((size_t)m, 1);
+    int64_t* keep = (int64_t*)malloc((size_t)m * sizeof(int64_t));
+    int64_t nk = 0;
+    for (int64_t _i = 0; _i < m; ++_i) {
+      const int64_t i = ord[_i].idx;
+      if (sup[i]) continue;
+      keep[nk++] = i;
+      const float ix1 = bx[i * 5], iy1 = bx[i * 5 + 1], ix2 = bx[i * 5 + 2], iy2 = bx[i * 5 + 3];
+      const float iarea = bx[i * 5 + 4];
+      for (int64_t _j = _i + 1; _j < m; ++_j) {
+        const int64_t j = ord[_j].idx;
+        if (sup[j]) continue;
+        const float xx1 = std_maxf(ix1, bx[j * 5]), yy1 = std_maxf(iy1, bx[j * 5 + 1]);
+        const float xx2 = std_minf(ix2, bx[j * 5 + 2]), yy2 = std_minf(iy2, bx[j * 5 + 3]);
+        const float w = std_maxf(0.0f, xx2 - xx1), h = std_maxf(0.0f, yy2 - yy1);
+        const float inter = w * h;
+        const float ovr = inter / (iarea + bx[j * 5 + 4] - inter);
+        if ((double)ovr > iou_thres) sup[j] = 1;
+      }
+    }
+    kept = (int)(nk < max_det ? nk : max_det);    /* i = i[:max_det] */
+    for (int k = 0; k < kept; ++k) {
+      const float* r = x + keep[k] * 6;
+      memcpy(det + k * 6, r, 6 * sizeof(float));
+      if (xywh && scale) {
+        float c4[4];
+        for (int e = 0; e < 4; ++e) {
+          float v = r[e] - ((e & 1) ? scale[2] : scale[1]);
+          v = v / scale[0];
+          const float hi = (e & 1) ? scale[4] : scale[3];
+          if (v == v) v = v < 0.0f ? 0.0f : (v > hi ? hi : v);
+          c4[e] = rintf(v);
+        }
+        xywh[k * 4 + 0] = (c4[0] + c4[2]) / 2.0f;
+        xywh[k * 4 + 1] = (c4[1] + c4[3]) / 2.0f;
+        xywh[k * 4 + 2] = c4[2] - c4[0];
+        xywh[k * 4 + 3] = c4[3] - c4[1];
+      }
+    }
+    free(ord); free(bx); free(sup); free(keep);
+  }
+  free(x);
+  return kept;
+}
