@@ -37,6 +37,10 @@
 int g_enc_gemm = 1;      // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
 int g_enc_gemm_dbg = 0;     // trk_set_tuning("enc_gemm_dbg"): experiments (1 skip epilogue, 2 stores, 4 sums, 8 sum
                             // writes; g1dw: 16 no depthwise, 32 two K steps only)
+int g_g1dw_persist = 0;     // trk_set_tuning("g1dw_persist"): 0 = one workgroup per tile; v > 0 = persistent
+                            // tile queue, 2 workgroups per CU, the second started (v - 1) x 2048 cycles late
+int g_g1dw_mode = 1;        // trk_set_tuning("g1dw_mode"): where the K loop issues its LDS-DMA (0 top, 1 after the
+                            // MFMAs, 2 interleaved)
 int g_enc_gemm_offset = 0;  // trk_set_tuning("enc_gemm_offset"): > 0 runs gemm4 persistent (2 workgroups per CU)
                             // with each CU's second workgroup started that many x 2048 cycles late
 
@@ -377,6 +381,57 @@ int launch(const EncGemmArgs& a, hipStream_t st) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// Persistent tile queue: tiles are dealt from 8 per-XCD ranges (tile order as
+// xcd_remap, so one XCD's L2 sees contiguous M tiles); a workgroup takes tiles of
+// its own range first (blockIdx % 8, the dispatcher's round-robin -- placement is a
+// speed hint only) and then steals from the others, so workgroups that start late
+// -- behind CUs another stream still holds -- just take fewer tiles.  The last
+// workgroup to leave resets the counters for the next launch using this slot.
+constexpr int kQueues = 64;                 // launch slots (round-robin on the host)
+__device__ unsigned int g_tileq[kQueues][10];  // [0..7] next index per XCD range, [8] workgroups done
+
+struct TileQueue {
+  unsigned int* q;
+  int64_t ntiles;
+  __device__ int64_t range_lo(int x) const {
+    const int64_t b = ntiles / 8, r = ntiles % 8;
+    return x * b + (x < r ? x : r);
+  }
+  // next tile for this workgroup (uniform), or -1; tid 0 fetches, LDS broadcast
+  __device__ int64_t next(int* slot, int& cur) const {
+    if (threadIdx.x == 0) {
+      int64_t t = -1;
+      for (; cur < 8 && t < 0; ) {
+        const int x = (int)((blockIdx.x + cur) & 7);
+        const int64_t lo = range_lo(x), n = range_lo(x + 1) - lo;
+        const unsigned int i = atomicAdd(&q[x], 1u);
+        if ((int64_t)i < n) t = lo + i;
+        else ++cur;
+      }
+      *slot = (int)t;
+    }
+    __syncthreads();
+    const int t = *slot;
+    __syncthreads();
+    return t;
+  }
+  __device__ void finish() const {
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(&q[8], 1u) == gridDim.x - 1) {
+        for (int x = 0; x < 9; ++x) atomicExch(&q[x], 0u);
+        __threadfence();
+      }
+    }
+  }
+};
+
+int next_queue_slot() {
+  static int s = 0;
+  s = (s + 1) % kQueues;
+  return s;
+}
+
 // ---------------------------------------------------------------------------
 // First 1x1 convs + the four depthwise 5x5 convs in one kernel (10x10 ROIs).
 //
@@ -384,10 +439,10 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 // rows 200..223 belong to the next tile and are discarded), so the 5x5
 // neighbourhood of every output pixel is inside the tile: Y1 = X . W1^T is
 // rounded to bf16 into LDS (exactly what the plain GEMM would store) and the
-// depthwise conv runs from there with the same f32 FMA order as
-// dwconv5_rows2_kernel, writing only Y2.  Y1 never reaches HBM.  N tile = 128
-// channels; 8 waves: wave w owns column tile w & 3 and row tiles
-// (w >> 2) + 2t.  K loop as enc_gemm_kernel (LDS-DMA ring, NSTAGE = 3).
+// depthwise conv runs from there with dwconv5_rows2_kernel's f32 FMA order (taps
+// in the zero padding skipped), writing only Y2.  Y1 never reaches HBM.  N tile =
+// 128 channels; 8 waves: wave w owns column tile w & 3 and row tiles (w >> 2) +
+// 2t.  K loop as enc_gemm_kernel (LDS-DMA ring, NSTAGE = 3).
 constexpr int G1_ROWS = 224, G1_BN = 128, G1_S = 10, G1_P = 100;
 constexpr int G1_AP = G1_ROWS * CPR;               // A 16-B pieces per stage (896)
 constexpr size_t G1_STAGE = (size_t)(G1_ROWS + G1_BN) * CPR * 16;
@@ -395,17 +450,18 @@ constexpr size_t G1_TILE = (size_t)2 * G1_P * (G1_BN / 2) * 4;   // bf16 pairs [
 constexpr size_t G1_W = (size_t)25 * (G1_BN / 2) * 8;            // f32 pairs [25][64]
 constexpr size_t G1_LDS = NSTAGE * G1_STAGE > G1_TILE + G1_W ? NSTAGE * G1_STAGE : G1_TILE + G1_W;
 
-__global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                                   const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                   int M, int N, int dbg) {
-  extern __shared__ __align__(16) unsigned char smem[];
+template <int MODE>
+__device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
+                                          const float* __restrict__ wdw, uint16_t* __restrict__ Y2, int M, int N,
+                                          int dbg, int64_t lb, unsigned char* smem) {
   uint4* As = reinterpret_cast<uint4*>(smem);       // [NSTAGE][224 * CPR]
   uint4* Bs = As + NSTAGE * G1_AP;                   // [NSTAGE][128 * CPR]
-  const int tid = threadIdx.x, lane = tid & 63;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));                      // per tile: keep lane addresses out of the tile loop
+  const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave & 3, wr = wave >> 2;
   const int ntile_n = N / G1_BN;
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
   const int n0 = (int)(lb % ntile_n) * G1_BN;
   const int64_t m0 = (lb / ntile_n) * (2 * G1_P);   // two ROIs per tile
   constexpr int K = 512;
@@ -423,11 +479,22 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
     const int p = tid, r = p / CPR, c = unswz_c(p);
     bsrc = W1 + (int64_t)(n0 + r) * K + c * 8;
   }
+  // DMA op j (0: A rows 0..127, 1: A rows 128..223 (waves 0..5), 2: B) of a stage
+  auto issue_op = [&](int j, int stage, int k0) {
+    if (dbg & 128) return;  // experiment: no operand loads
+    if (j == 0)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
+    else if (j == 1) {
+      if (wave < (G1_AP - 512) / 64)
+        __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
+    } else {
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
+    }
+  };
   auto issue = [&](int stage, int k0) {
-    __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
-    if (wave < (G1_AP - 512) / 64)
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
+    issue_op(0, stage, k0);
+    issue_op(1, stage, k0);
+    issue_op(2, stage, k0);
   };
   // row tiles of this wave: wr, wr + 2, wr + 4 (+ wr + 6 for wr == 0)
   constexpr int TMX = 4;
@@ -452,21 +519,35 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue((kt + 2) % NSTAGE, (kt + 2) * BK);
+    const bool pf = kt + 2 < nk;
+    const int pst = (kt + 2) % NSTAGE, pk = (kt + 2) * BK;
+    if (MODE == 0 && pf) issue(pst, pk);
     const uint4* as = As + st * G1_AP;
     const uint4* bs = Bs + st * G1_BN * CPR;
+    if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int c = ks * 2 + (lane >> 5);
-      const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int c = ks * 2 + (lane >> 5);
+        const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
 #pragma unroll
-      for (int i = 0; i < TMX; ++i) {
-        if (i < ntm) {
-          const int rt = wr + 2 * i;
-          const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
+        for (int i = 0; i < TMX; ++i) {
+          if (i < ntm) {
+            const int rt = wr + 2 * i;
+            const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
+          }
+          // MODE 2: the stage's three DMA ops interleaved with the MFMAs
+          if (MODE == 2 && pf && ((ks == 0 && (i == 0 || i == 2)) || (ks == 1 && i == 0))) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_op(ks == 0 ? i / 2 : 2, pst, pk);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
+    }
+    if (MODE == 1 && pf) {  // after this step's MFMAs are issued
+      __builtin_amdgcn_sched_barrier(0);
+      issue(pst, pk);
     }
   }
   __syncthreads();
@@ -508,17 +589,13 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
     for (int r = 0; r < 6; ++r) {
       const int yy = y0 - 2 + r;
       if (yy < 0 || yy >= G1_S) continue;
-      dw_pair_t rr[G1_S + 4];
+      dw_pair_t rr[G1_S];
 #pragma unroll
-      for (int x = 0; x < G1_S + 4; ++x) {
-        const int xx = x - 2;
-        if (xx >= 0 && xx < G1_S) {
-          const uint32_t v = src[(yy * G1_S + xx) * (G1_BN / 2) + cp];
-          rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
-        } else {
-          rr[x] = dw_pair_t{0.f, 0.f};
-        }
+      for (int x = 0; x < G1_S; ++x) {
+        const uint32_t v = src[(yy * G1_S + x) * (G1_BN / 2) + cp];
+        rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
       }
+      // taps in the zero padding (x + kx - 2 outside the ROI) are skipped
       if (r <= 4) {
         dw_pair_t wv[5];
 #pragma unroll
@@ -526,7 +603,8 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
 #pragma unroll
         for (int x = 0; x < G1_S; ++x)
 #pragma unroll
-          for (int kx = 0; kx < 5; ++kx) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx], a0[x]);
+          for (int kx = 0; kx < 5; ++kx)
+            if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
       }
       if (r >= 1) {
         dw_pair_t wv[5];
@@ -535,7 +613,8 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
 #pragma unroll
         for (int x = 0; x < G1_S; ++x)
 #pragma unroll
-          for (int kx = 0; kx < 5; ++kx) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx], a1[x]);
+          for (int kx = 0; kx < 5; ++kx)
+            if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
       }
     }
     uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
@@ -545,6 +624,231 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
       dst[((y0 + 1) * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a1[x].x, a1[x].y);
     }
   }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
+                                                   const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
+                                                   int M, int N, int dbg) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  g1dw_tile<MODE>(X, W1, wdw, Y2, M, N, dbg, xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// persistent: two workgroups per CU take tiles from the queue; each CU's second
+// workgroup starts offset x 2048 cycles late so its K loop runs beside the first
+// one's depthwise phase
+__global__ void __launch_bounds__(512) g1dw_persist_kernel(const uint16_t* __restrict__ X,
+                                                           const uint16_t* __restrict__ W1,
+                                                           const float* __restrict__ wdw,
+                                                           uint16_t* __restrict__ Y2, int M, int N, int dbg,
+                                                           int64_t ntiles, int qslot, int offset) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const TileQueue tq{g_tileq[qslot], ntiles};
+  if (offset > 0 && blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < offset; ++i) __builtin_amdgcn_s_sleep(32);
+  int cur = 0;
+  for (;;) {
+    const int64_t t = tq.next(reinterpret_cast<int*>(smem), cur);  // LDS is free between tiles
+    if (t < 0) break;
+    g1dw_tile<0>(X, W1, wdw, Y2, M, N, dbg, t, smem);
+    __syncthreads();  // the next tile's DMA reuses the LDS the depthwise phase read
+  }
+  tq.finish();
+}
+
+
+// ---------------------------------------------------------------------------
+// g1dw, interleaved (persistent, one workgroup per CU): the depthwise 5x5 of
+// the previous tile runs INSIDE the K loop of the current tile's GEMM, so its
+// VALU work fills the MFMA / LDS-DMA latency of the K loop instead of running
+// as a separate phase.  LDS: a 4-stage operand ring (three K steps in flight),
+// the previous tile's Y1 [200][64 pairs] and its depthwise weights.
+//   per tile t:  K step kt: barrier, DMA of step kt + 3, MFMAs of tile t, and on
+//                even kt one depthwise input-row step of tile t - 1;
+//                barrier; Y1(t) and weights(t) -> LDS; next tile.
+// Depthwise work per tile = 10 (ROI, output row pair) tasks = 52 valid input-row
+// steps: waves 0..5 own one interior task each (6 steps), waves 6..7 own the
+// two border tasks of one ROI (4 + 4 steps); every wave is done by K step 14.
+// Same arithmetic as g1dw_kernel (bit-identical).
+constexpr int IL_NST = 4;
+constexpr size_t IL_RING = (size_t)IL_NST * G1_STAGE;                 // 90112
+constexpr size_t IL_LDS = IL_RING + G1_TILE + G1_W + 16;               // 154128
+static_assert(IL_LDS <= 160 * 1024, "g1dw_il: one workgroup per CU");
+
+// one input row yy (kernel rows r / r - 1 for output rows y0 / y0 + 1)
+__device__ __forceinline__ void il_dw_row(const uint32_t* __restrict__ src, const dw_pair_t* __restrict__ wl, int yy,
+                                          int r, dw_pair_t (&a0)[G1_S], dw_pair_t (&a1)[G1_S], int cp) {
+  dw_pair_t rr[G1_S];
+#pragma unroll
+  for (int x = 0; x < G1_S; ++x) {
+    const uint32_t v = src[(yy * G1_S + x) * (G1_BN / 2) + cp];
+    rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+  }
+  if (r <= 4) {
+    dw_pair_t wv[5];
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G1_BN / 2) + cp];
+#pragma unroll
+    for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx)
+        if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
+  }
+  if (r >= 1) {
+    dw_pair_t wv[5];
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G1_BN / 2) + cp];
+#pragma unroll
+    for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx)
+        if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
+  }
+}
+
+__global__ void __launch_bounds__(512) g1dw_il_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
+                                                      const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
+                                                      int M, int N, int64_t ntiles, int qslot) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* As = reinterpret_cast<uint4*>(smem);                     // [IL_NST][224 * CPR]
+  uint4* Bs = As + IL_NST * G1_AP;                                 // [IL_NST][128 * CPR]
+  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem + IL_RING);      // previous tile's Y1
+  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + IL_RING + G1_TILE);
+  int* slot = reinterpret_cast<int*>(smem + IL_RING + G1_TILE + G1_W);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3, wr = wave >> 2;
+  const int ntile_n = N / G1_BN;
+  constexpr int K = 512, NK = K / BK;
+  const TileQueue tq{g_tileq[qslot], ntiles};
+  int cur = 0;
+  // depthwise plan of this wave: (roi, y0, first / last input-row step r)
+  const int d_roi = wave < 6 ? wave / 3 : wave - 6;
+  const int d_y0a = wave < 6 ? 2 * (1 + wave % 3) : 0;    // interior pair, or border pair 0
+  const int ops = wave < (G1_AP - 512) / 64 ? 3 : 2;      // DMA ops per stage of this wave
+
+  int64_t t = tq.next(slot, cur), tp = -1;
+  while (t >= 0 || tp >= 0) {
+    const bool gemm = t >= 0;
+    const int n0 = gemm ? (int)(t % ntile_n) * G1_BN : 0;
+    const int64_t m0 = gemm ? (t / ntile_n) * (2 * G1_P) : 0;
+    const uint16_t* asrc[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = min(q * 512 + tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
+      asrc[q] = X + min(m0 + r, (int64_t)M - 1) * K + c * 8;
+    }
+    const uint16_t* bsrc = W1 + (int64_t)(n0 + tid / CPR) * K + unswz_c(tid) * 8;
+    auto issue = [&](int stage, int k0) {
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
+      if (ops == 3)
+        __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
+    };
+    // previous tile's depthwise target
+    const int pn0 = tp >= 0 ? (int)(tp % ntile_n) * G1_BN : 0;
+    const int64_t prbase = tp >= 0 ? (tp / ntile_n) * (2 * G1_P) + d_roi * G1_P : M;
+    const bool dw = tp >= 0 && prbase < M;
+    const uint32_t* dsrc = y1 + d_roi * G1_P * (G1_BN / 2);
+    uint32_t* ddst = reinterpret_cast<uint32_t*>(Y2 + (dw ? prbase : 0) * N + pn0);
+    dw_pair_t a0[G1_S], a1[G1_S];
+
+    constexpr int TMX = 4;
+    const int ntm = wr == 0 ? 4 : 3;
+    f16_t acc[TMX];
+#pragma unroll
+    for (int i = 0; i < TMX; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    if (gemm) {
+      issue(0, 0);
+      issue(1, BK);
+      issue(2, 2 * BK);
+    }
+#pragma unroll 1
+    for (int kt = 0; kt < NK; ++kt) {
+      if (gemm) {
+        // stage kt landed; kt + 1, kt + 2 (and at most one step's Y2 stores) may stay in flight
+        if (kt + 2 < NK) {
+          if (ops == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else if (kt + 1 < NK) {
+          if (ops == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (gemm) {
+        if (kt + 3 < NK) issue((kt + 3) % IL_NST, (kt + 3) * BK);
+        const uint4* as = As + (kt % IL_NST) * G1_AP;
+        const uint4* bs = Bs + (kt % IL_NST) * G1_BN * CPR;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+          const int c = ks * 2 + (lane >> 5);
+          const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
+#pragma unroll
+          for (int i = 0; i < TMX; ++i) {
+            if (i < ntm) {
+              const int rt = wr + 2 * i;
+              const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
+              acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
+            }
+          }
+        }
+      }
+      // one depthwise input-row step of the previous tile on even K steps
+      if (dw && !(kt & 1)) {
+        const int s = kt >> 1;
+        int y0, r;
+        if (wave < 6) { y0 = d_y0a; r = s; }
+        else if (s < 4) { y0 = 0; r = s + 2; }          // border pair 0: input rows 0..3
+        else { y0 = 8; r = s - 4; }                      // border pair 4: input rows 6..9
+        const bool active = wave < 6 ? s < 6 : true;
+        if (active) {
+          const bool first = wave < 6 ? s == 0 : (s == 0 || s == 4);
+          const bool last = wave < 6 ? s == 5 : (s == 3 || s == 7);
+          if (first) {
+#pragma unroll
+            for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
+          }
+          il_dw_row(dsrc, wl, y0 - 2 + r, r, a0, a1, lane);
+          if (last) {
+#pragma unroll
+            for (int x = 0; x < G1_S; ++x) {
+              ddst[(y0 * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a0[x].x, a0[x].y);
+              ddst[((y0 + 1) * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a1[x].x, a1[x].y);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // every read of Y1(tp) / weights(tp) and of the ring is done
+    if (gemm) {
+      const int cl = wn * 32 + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < TMX; ++i) {
+        if (i < ntm) {
+          const int rt = wr + 2 * i;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
+          }
+        }
+      }
+      for (int q = tid; q < 25 * (G1_BN / 2); q += 512) {
+        const int k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
+        wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
+      }
+    }
+    tp = t;
+    t = gemm ? tq.next(slot, cur) : -1;  // next() ends with a barrier: Y1 / weights visible
+    if (!gemm) break;                     // the drain pass ran the last tile's depthwise
+  }
+  tq.finish();
 }
 
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
@@ -726,8 +1030,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   g4_barrier();
 
+  // tile kt + 2's DMA is issued after step kt's MFMAs (its buffer was last read in
+  // step kt - 1): the MFMAs start as soon as the fragments are read, and the DMA
+  // issue -- which stalls while the memory pipeline is full -- runs beside them
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 2 < nk) issue(kt + 2);
     const uint4* buf = ring + (kt % 3) * G4_BUF;
     bf8v bfr[8], afr[4];
 #pragma unroll
@@ -739,6 +1045,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 #pragma unroll
       for (int t = 0; t < 8; ++t)
         acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[t], acc[i][t], 0, 0, 0);
+    if (kt + 2 < nk) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 2);
+    }
     if (kt + 1 < nk) {
       if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -874,14 +1184,23 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 // one's MFMA loop runs under the other's VALU / store epilogue instead of both
 // alternating between them in lockstep.
 template <int EPI>
-__global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles, int offset) {
+__global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles, int offset, int qslot) {
   extern __shared__ __align__(16) unsigned char smem[];
+  if (qslot < 0) {  // one workgroup per tile
+    gemm4_tile<EPI>(a, xcd_remap(blockIdx.x, ntiles), smem);
+    return;
+  }
+  const TileQueue tq{g_tileq[qslot], ntiles};
   if (offset > 0 && blockIdx.x >= gridDim.x / 2)
     for (int i = 0; i < offset; ++i) __builtin_amdgcn_s_sleep(32);
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    gemm4_tile<EPI>(a, xcd_remap(t, ntiles), smem);
+  int cur = 0;
+  for (;;) {
+    const int64_t t = tq.next(reinterpret_cast<int*>(smem), cur);  // LDS is free between tiles
+    if (t < 0) break;
+    gemm4_tile<EPI>(a, t, smem);
     __syncthreads();  // the next tile's DMA reuses the LDS the epilogue read
   }
+  tq.finish();
 }
 
 int cu_count() {
@@ -910,7 +1229,8 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   }
   EncGemmArgs b = a;
   b.dbg = g_enc_gemm_dbg;
-  hipLaunchKernelGGL((gemm4_kernel<EPI>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg, g_enc_gemm_offset);
+  hipLaunchKernelGGL((gemm4_kernel<EPI>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg, g_enc_gemm_offset,
+                     g_enc_gemm_offset > 0 ? next_queue_slot() : -1);
   return trk::check_launch("gemm4_kernel");
 }
 
@@ -1004,12 +1324,38 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_g1_dwconv: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)G1_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_persist_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     attr = true;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(g1dw_kernel, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
+  if (g_g1dw_persist == 66) {   // interleaved depthwise, one workgroup per CU
+    static bool attr_il = false;
+    if (!attr_il) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_il_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)IL_LDS);
+      attr_il = true;
+    }
+    const int64_t grid = std::min<int64_t>(nwg, (int64_t)cu_count());
+    hipLaunchKernelGGL(g1dw_il_kernel, dim3((unsigned)grid), dim3(512), IL_LDS, st, (const uint16_t*)X,
+                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, nwg, next_queue_slot());
+    return trk::check_launch("g1dw_il_kernel");
+  }
+  if (g_g1dw_persist > 0) {
+    const int64_t grid = std::min<int64_t>(nwg, 2 * (int64_t)cu_count());
+    hipLaunchKernelGGL(g1dw_persist_kernel, dim3((unsigned)grid), dim3(512), G1_LDS, st, (const uint16_t*)X,
+                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg, nwg,
+                       next_queue_slot(), g_g1dw_persist - 1);
+    return trk::check_launch("g1dw_persist_kernel");
+  }
+  auto kern = g_g1dw_mode == 1 ? g1dw_kernel<1> : g_g1dw_mode == 2 ? g1dw_kernel<2> : g1dw_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
                      (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
   return trk::check_launch("g1dw_kernel");
 }

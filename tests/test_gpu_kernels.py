@@ -406,6 +406,23 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         Yf = ops.enc_g1_dwconv(X, W1, wdw)
         Yu = ops.dwconv5_nhwc(ops.enc_gemm(X, W1).view(R, 10, 10, 1024), wdw).view(M, 1024)
         assert torch.equal(Yf, Yu)
+        # persistent tile-queue variants compute the same tiles: same bits
+        for v in (1, 4, 66):   # 66: depthwise interleaved into the next tile's K loop
+            try:
+                assert L.trk_set_tuning(b"g1dw_persist", v) == 0
+                Yp = ops.enc_g1_dwconv(X, W1, wdw)
+                Yp2 = ops.enc_g1_dwconv(X, W1, wdw)   # the queue resets itself between launches
+            finally:
+                assert L.trk_set_tuning(b"g1dw_persist", 0) == 0
+            assert torch.equal(Yp, Yu) and torch.equal(Yp2, Yu)
+    for v in (1, 3):
+        try:
+            assert L.trk_set_tuning(b"enc_gemm_offset", v) == 0
+            XRNp, srp, snp = ops.enc_dsc_gemm(Y2, P, W2, b2)
+            stp = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+        finally:
+            assert L.trk_set_tuning(b"enc_gemm_offset", 0) == 0
+        assert torch.equal(XRNp, XRN) and torch.equal(srp, sr) and torch.equal(snp, sn) and torch.equal(stp, st)
 
 
 def _partials(total, P, parts=3):

@@ -36,17 +36,30 @@ def timeit(fn, reps=10):
 
 
 items = {
-    "g1dw": (lambda: ops.enc_g1_dwconv(X, W1, wdw), [0, 16, 32, 48], 2 * M * 512 * 1024),
+    "g1dw": (lambda: ops.enc_g1_dwconv(X, W1, wdw), [0, 16, 32, 48, 16 | 64, 16 | 128, 16 | 64 | 128], 2 * M * 512 * 1024),
     "plain256": (lambda: ops.enc_gemm(X, W1), [0], 2 * M * 512 * 1024),
-    "dsc": (lambda: ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True), [0, 1, 2, 4, 6], 2 * M * 1024 * 512),
-    "trans": (lambda: ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True), [0, 1, 4], 2 * M * 1024 * 512),
+    "dsc": (lambda: ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True), [0, 1, 16, 17], 2 * M * 1024 * 512),
+    "trans": (lambda: ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True), [0, 1, 16, 17], 2 * M * 1024 * 512),
 }
+offsets = [int(v) for v in os.environ.get("ENC_OFFSETS", "0").split(",")]
+g1p = [int(v) for v in os.environ.get("G1P", "0").split(",")]
+g1m = [int(v) for v in os.environ.get("G1M", "0").split(",")]   # g1dw_mode: DMA placement
 for name, (fn, dbgs, flops) in items.items():
     if only != "all" and name not in only.split(","):
         continue
-    for d in (dbgs if not os.environ.get("ENC_DBG0") else [0]):
-        L.trk_set_tuning(b"enc_gemm_dbg", d)
-        t = timeit(fn)
-        print(json.dumps({"item": name, "dbg": d, "us": round(t, 1), "TFLOPs": round(flops / t / 1e6, 1)}), flush=True)
+    for off in ([p * 10 + m for p in g1p for m in g1m] if name == "g1dw" else offsets):
+        if name == "g1dw":
+            L.trk_set_tuning(b"g1dw_persist", off // 10)
+            L.trk_set_tuning(b"g1dw_mode", off % 10)
+        else:
+            L.trk_set_tuning(b"enc_gemm_offset", off)
+        for d in (dbgs if not os.environ.get("ENC_DBG0") else [0]):
+            L.trk_set_tuning(b"enc_gemm_dbg", d)
+            t = timeit(fn)
+            print(json.dumps({"item": name, "offset": off, "dbg": d, "us": round(t, 1),
+                              "TFLOPs": round(flops / t / 1e6, 1)}), flush=True)
 L.trk_set_tuning(b"enc_gemm_dbg", 0)
+L.trk_set_tuning(b"enc_gemm_offset", 0)
+L.trk_set_tuning(b"g1dw_persist", 0)
+L.trk_set_tuning(b"g1dw_mode", 1)
 torch.cuda.synchronize()

@@ -42,6 +42,9 @@ def main():
                        "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost",
                        "enc_gemm_kernel<0": "enc_gemm_dsc", "enc_gemm_kernel<1": "enc_gemm_trans",
                        "enc_gemm_kernel<2": "enc_gemm_plain", "g1dw_kernel": "enc_g1_dwconv",
+                       "g1dw_il_kernel": "enc_g1_dwconv", "g1dw_persist_kernel": "enc_g1_dwconv",
+                       "gemm4_kernel<0": "enc_gemm_dsc", "gemm4_kernel<1": "enc_gemm_trans",
+                       "enc_se_kernel": "enc_se", "enc_head_kernel": "enc_head", "det_nms_kernel": "det_nms",
                        "lsap_kernel": "lsap", "act_mean_kernel": "act_mean", "scale_rows_kernel": "scale_rows",
                        "nchw_to_nhwc_kernel": "nchw_to_nhwc", "track_update_kernel": "track_update"}
         tab = {}
