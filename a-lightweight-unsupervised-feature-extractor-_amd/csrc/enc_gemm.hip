@@ -500,6 +500,7 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
   constexpr int TMX = 4;
   const int ntm = wr == 0 ? 4 : 3;
   f16_t acc[TMX];
+  bf8_t x_b[BK / 16], x_a[BK / 16][TMX];  // MODE 3 experiment only
 #pragma unroll
   for (int i = 0; i < TMX; ++i)
 #pragma unroll
@@ -524,7 +525,24 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
     if (MODE == 0 && pf) issue(pst, pk);
     const uint4* as = As + st * G1_AP;
     const uint4* bs = Bs + st * G1_BN * CPR;
-    if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
+    if (MODE == 3 && !(dbg & 64)) {  // experiment: MFMAs on fragments read once per tile (no LDS reads)
+      if (kt == 0) {
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+          const int c = ks * 2 + (lane >> 5);
+          x_b[ks] = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
+#pragma unroll
+          for (int i = 0; i < TMX; ++i)
+            x_a[ks][i] = *reinterpret_cast<const bf8_t*>(&as[swz((wr + 2 * (i < ntm ? i : 0)) * 32 + (lane & 31), c)]);
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks)
+#pragma unroll
+        for (int i = 0; i < TMX; ++i)
+          if (i < ntm) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x_a[ks][i], x_b[ks], acc[i], 0, 0, 0);
+    }
+    if (MODE != 3 && !(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         const int c = ks * 2 + (lane >> 5);
@@ -545,7 +563,7 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
         }
       }
     }
-    if (MODE == 1 && pf) {  // after this step's MFMAs are issued
+    if ((MODE == 1 || MODE == 3) && pf) {  // after this step's MFMAs are issued
       __builtin_amdgcn_sched_barrier(0);
       issue(pst, pk);
     }
@@ -632,6 +650,169 @@ __global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ 
                                                    int M, int N, int dbg) {
   extern __shared__ __align__(16) unsigned char smem[];
   g1dw_tile<MODE>(X, W1, wdw, Y2, M, N, dbg, xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// ---------------------------------------------------------------------------
+// g1dw, warp-specialised: 10 waves = 8 MFMA waves (the tile split of g1dw_tile)
+// + 2 DMA waves that issue the whole stage (22 LDS-DMA wave-instructions).  The
+// K loop is L2->LDS bound (~27 TB/s chip-wide for this tile shape) and a wave
+// that issues LDS-DMA stalls while the memory pipeline is full; with the issue
+// on waves of their own, the MFMA waves keep the matrix pipe busy meanwhile.
+// One s_barrier per K step for all 10 waves: the DMA waves wait (vmcnt) for
+// stage kt, the barrier publishes it, then they issue stage kt + 2 while the
+// MFMA waves consume stage kt.  The depthwise phase runs on all 10 waves, one
+// (ROI, output row pair) task each.  Same arithmetic as g1dw_kernel.
+__global__ void __launch_bounds__(640, 5) g1dw_ws_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
+                                                      const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
+                                                      int M, int N) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* As = reinterpret_cast<uint4*>(smem);       // [NSTAGE][224 * CPR]
+  uint4* Bs = As + NSTAGE * G1_AP;                   // [NSTAGE][128 * CPR]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntile_n = N / G1_BN;
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(lb % ntile_n) * G1_BN;
+  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);
+  constexpr int K = 512, NK = K / BK, NBLK = (G1_AP + G1_BN * CPR) / 64;  // 22 blocks of 64 pieces
+  constexpr int NI = NBLK / 2;                                             // per DMA wave (11)
+  static_assert(NBLK % 2 == 0 && G1_AP % 64 == 0, "DMA blocks");
+  const bool dmaw = wave >= 8;
+
+  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
+  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G1_TILE);
+  if (dmaw) {
+    // ---- DMA waves: piece q = 64 b + lane of a block sits at row 16 b + lane / 4 (of A,
+    // or of B past the A blocks), chunk unswz_c(lane); 32-bit element offsets from the
+    // uniform operand bases (M * 512 < 2^31: checked on the host)
+    const int p = wave - 8;
+    const int lrow = lane >> 2, lcol = unswz_c(lane) * 8;
+    auto issue = [&](int stage, int k0) {
+      int lr = lrow;
+      asm volatile("" : "+v"(lr));  // offsets rebuilt per stage: no hoisted per-block state
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int b = 2 * i + p;
+        if (b < G1_AP / 64) {
+          const int row = min((int)m0 + 16 * b + lr, M - 1);
+          __builtin_amdgcn_global_load_lds(GPTR(X + (row * K + lcol + k0)), LPTR(As + stage * G1_AP + b * 64), 16,
+                                           0, 0);
+        } else {
+          const int row = n0 + 16 * (b - G1_AP / 64) + lr;
+          __builtin_amdgcn_global_load_lds(GPTR(W1 + (row * K + lcol + k0)),
+                                           LPTR(Bs + stage * G1_BN * CPR + (b - G1_AP / 64) * 64), 16, 0, 0);
+        }
+      }
+    };
+    issue(0, 0);
+    issue(1, BK);
+#pragma unroll 1
+    for (int kt = 0; kt < NK; ++kt) {
+      if (kt + 1 < NK) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");   // stage kt landed, kt + 1 in flight
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < NK) issue((kt + 2) % NSTAGE, (kt + 2) * BK);  // buffer last read in step kt - 1
+    }
+    __syncthreads();
+  } else {
+    // ---- MFMA waves: the g1dw_tile split (wave: column tile wave & 3, row tiles (wave >> 2) + 2t)
+    constexpr int TMX = 4;
+    const int wn = wave & 3, wr = wave >> 2;
+    const int ntm = wr == 0 ? 4 : 3;
+    f16_t acc[TMX];
+#pragma unroll
+    for (int i = 0; i < TMX; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll 1
+    for (int kt = 0; kt < NK; ++kt) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const uint4* as = As + (kt % NSTAGE) * G1_AP;
+      const uint4* bs = Bs + (kt % NSTAGE) * G1_BN * CPR;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int c = ks * 2 + (lane >> 5);
+        const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
+#pragma unroll
+        for (int i = 0; i < TMX; ++i) {
+          if (i < ntm) {
+            const int rt = wr + 2 * i;
+            const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int cl = wn * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TMX; ++i) {
+      if (i < ntm) {
+        const int rt = wr + 2 * i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
+        }
+      }
+    }
+  }
+  for (int q = tid; q < 25 * (G1_BN / 2); q += 640) {
+    const int k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
+    wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
+  }
+  __syncthreads();
+
+  // depthwise 5x5: one (ROI, output row pair) task per wave
+  {
+    const int roi = wave / (G1_S / 2), y0 = 2 * (wave % (G1_S / 2));
+    const int64_t rbase = m0 + roi * G1_P;
+    if (rbase < M) {
+      const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2);
+      dw_pair_t a0[G1_S], a1[G1_S];
+#pragma unroll
+      for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const int yy = y0 - 2 + r;
+        if (yy < 0 || yy >= G1_S) continue;
+        dw_pair_t rr[G1_S];
+#pragma unroll
+        for (int x = 0; x < G1_S; ++x) {
+          const uint32_t v = src[(yy * G1_S + x) * (G1_BN / 2) + lane];
+          rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+        }
+        if (r <= 4) {
+          dw_pair_t wv[5];
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G1_BN / 2) + lane];
+#pragma unroll
+          for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+            for (int kx = 0; kx < 5; ++kx)
+              if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
+        }
+        if (r >= 1) {
+          dw_pair_t wv[5];
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G1_BN / 2) + lane];
+#pragma unroll
+          for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+            for (int kx = 0; kx < 5; ++kx)
+              if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
+        }
+      }
+      uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
+#pragma unroll
+      for (int x = 0; x < G1_S; ++x) {
+        dst[(y0 * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a0[x].x, a0[x].y);
+        dst[((y0 + 1) * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a1[x].x, a1[x].y);
+      }
+    }
+  }
 }
 
 // persistent: two workgroups per CU take tiles from the queue; each CU's second
@@ -1330,6 +1511,8 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<3>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_persist_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     attr = true;
@@ -1354,7 +1537,20 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
                        next_queue_slot(), g_g1dw_persist - 1);
     return trk::check_launch("g1dw_persist_kernel");
   }
-  auto kern = g_g1dw_mode == 1 ? g1dw_kernel<1> : g_g1dw_mode == 2 ? g1dw_kernel<2> : g1dw_kernel<0>;
+  if (g_g1dw_mode == 4) {
+    TRK_REQUIRE(M * 512 < (int64_t)1 << 31, "enc_g1_dwconv: M * 512 must stay below 2^31");
+    static bool attr_ws = false;
+    if (!attr_ws) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_ws_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
+      attr_ws = true;
+    }
+    hipLaunchKernelGGL(g1dw_ws_kernel, dim3((unsigned)nwg), dim3(640), G1_LDS, st, (const uint16_t*)X,
+                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+    return trk::check_launch("g1dw_ws_kernel");
+  }
+  auto kern = g_g1dw_mode == 1 ? g1dw_kernel<1> : g_g1dw_mode == 2 ? g1dw_kernel<2>
+            : g_g1dw_mode == 3 ? g1dw_kernel<3> : g1dw_kernel<0>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
                      (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
   return trk::check_launch("g1dw_kernel");

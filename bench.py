@@ -99,7 +99,12 @@ class Pipeline:
         self.sc, self.model, self.S = sc, model, S
         self.tracker = trk.MultiStreamTracker(sc["streams"], capacity=1024, device=sc["feat"].device)
         self.ids = {}
-        self.side = torch.cuda.Stream(device=sc["feat"].device)
+        # consecutive frames' embeddings alternate between two side streams, so the
+        # low-occupancy tail of frame f's encoder (SE / head: 128 workgroups) runs
+        # beside frame f+1's ROI Align and first GEMM instead of before them
+        n_side = int(os.environ.get("TRK_EMBED_STREAMS", "2"))
+        self.sides = [torch.cuda.Stream(device=sc["feat"].device) for _ in range(n_side)]
+        self.side = self.sides[0]
         self.pending = {}  # frame -> (embeddings, ready event)
         self.graphs = None
         # enqueue frame f+1's embedding at the start of step f (measured 1.13M vs
@@ -107,6 +112,7 @@ class Pipeline:
         # cost build and solver of f then share the GPU with it instead of
         # serialising between consecutive encoder runs
         self.prefetch_early = os.environ.get("TRK_PREFETCH_EARLY", "1") == "1"
+        self.depth = int(os.environ.get("TRK_PREFETCH_DEPTH", "1"))  # frames embedded ahead
 
     def capture(self):
         """Capture roi_align + encoder as two hipGraphs (static ROI / embedding
@@ -145,8 +151,12 @@ class Pipeline:
         if f in self.pending or f >= len(self.sc["rois"]):
             return
         main = torch.cuda.current_stream()
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
+        side = self.sides[f % len(self.sides)]
+        if len(self.sides) == 1 or self.graphs is not None:
+            side.wait_stream(main)  # graph replays reuse per-parity buffers main may still read
+        # (with two side streams no wait on main: an embedding reads only the frame's
+        # static map / boxes and writes buffers of its own; main waits on `ev`)
+        with torch.cuda.stream(side):
             if self.graphs is not None:
                 g, rois, emb = self.graphs[f & 1]
                 rois.copy_(self.sc["rois"][f], non_blocking=True)
@@ -154,7 +164,7 @@ class Pipeline:
             else:
                 emb = self.stage_embed(self.stage_roi(f))
             ev = torch.cuda.Event()
-            ev.record(self.side)
+            ev.record(side)
         emb.record_stream(main)
         self.pending[f] = (emb, ev)
 
@@ -164,7 +174,8 @@ class Pipeline:
         emb, ev = self.pending.pop(f)
         torch.cuda.current_stream().wait_event(ev)
         if self.prefetch_early:  # next frame's embedding before this frame's cost build
-            self.embed_async(f + 1)
+            for d in range(1, self.depth + 1):
+                self.embed_async(f + d)
             hook = None
         else:
             hook = lambda: self.embed_async(f + 1)
@@ -388,9 +399,10 @@ def main():
     model.load_state_dict(sd, strict=True)
     model = model.to(dev)
 
-    # +1 frame: the last timed step enqueues the next frame's embedding (pipelining),
-    # so the timed region does exactly `steps` embeddings and `steps` assignments
-    frames = PREROLL + args.warmup + args.steps + 1
+    # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
+    # the syncs around the timed region make it do exactly `steps` embeddings (those of
+    # frames first + depth .. last + depth) and `steps` assignments
+    frames = PREROLL + args.warmup + args.steps + int(os.environ.get("TRK_PREFETCH_DEPTH", "1"))
     sc = make_scenes(dev, args.streams, args.n, frames, seed=1000 + rank)
     pipe = Pipeline(sc, model)
     if args.graph:
