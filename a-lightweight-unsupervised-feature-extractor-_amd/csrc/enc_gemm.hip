@@ -40,7 +40,7 @@ int g_enc_gemm_dbg = 0;     // trk_set_tuning("enc_gemm_dbg"): experiments (1 sk
 int g_g1dw_persist = 0;     // trk_set_tuning("g1dw_persist"): 0 = one workgroup per tile; v > 0 = persistent
                             // tile queue, 2 workgroups per CU, the second started (v - 1) x 2048 cycles late
 int g_g1dw_mode = 1;        // trk_set_tuning("g1dw_mode"): where the K loop issues its LDS-DMA (0 top, 1 after the
-                            // MFMAs, 2 interleaved)
+                            // MFMAs, 2 interleaved; 4 = warp-specialised DMA waves); all bit-identical
 int g_enc_gemm_offset = 0;  // trk_set_tuning("enc_gemm_offset"): > 0 runs gemm4 persistent (2 workgroups per CU)
                             // with each CU's second workgroup started that many x 2048 cycles late
 
@@ -500,7 +500,6 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
   constexpr int TMX = 4;
   const int ntm = wr == 0 ? 4 : 3;
   f16_t acc[TMX];
-  bf8_t x_b[BK / 16], x_a[BK / 16][TMX];  // MODE 3 experiment only
 #pragma unroll
   for (int i = 0; i < TMX; ++i)
 #pragma unroll
@@ -525,24 +524,7 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
     if (MODE == 0 && pf) issue(pst, pk);
     const uint4* as = As + st * G1_AP;
     const uint4* bs = Bs + st * G1_BN * CPR;
-    if (MODE == 3 && !(dbg & 64)) {  // experiment: MFMAs on fragments read once per tile (no LDS reads)
-      if (kt == 0) {
-#pragma unroll
-        for (int ks = 0; ks < BK / 16; ++ks) {
-          const int c = ks * 2 + (lane >> 5);
-          x_b[ks] = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
-#pragma unroll
-          for (int i = 0; i < TMX; ++i)
-            x_a[ks][i] = *reinterpret_cast<const bf8_t*>(&as[swz((wr + 2 * (i < ntm ? i : 0)) * 32 + (lane & 31), c)]);
-        }
-      }
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks)
-#pragma unroll
-        for (int i = 0; i < TMX; ++i)
-          if (i < ntm) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x_a[ks][i], x_b[ks], acc[i], 0, 0, 0);
-    }
-    if (MODE != 3 && !(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
+    if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         const int c = ks * 2 + (lane >> 5);
@@ -563,7 +545,7 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
         }
       }
     }
-    if ((MODE == 1 || MODE == 3) && pf) {  // after this step's MFMAs are issued
+    if (MODE == 1 && pf) {  // after this step's MFMAs are issued
       __builtin_amdgcn_sched_barrier(0);
       issue(pst, pk);
     }
@@ -1511,8 +1493,6 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<3>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_persist_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
     attr = true;
@@ -1549,8 +1529,7 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
                        (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
     return trk::check_launch("g1dw_ws_kernel");
   }
-  auto kern = g_g1dw_mode == 1 ? g1dw_kernel<1> : g_g1dw_mode == 2 ? g1dw_kernel<2>
-            : g_g1dw_mode == 3 ? g1dw_kernel<3> : g1dw_kernel<0>;
+  auto kern = g_g1dw_mode == 1 ? g1dw_kernel<1> : g_g1dw_mode == 2 ? g1dw_kernel<2> : g1dw_kernel<0>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
                      (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
   return trk::check_launch("g1dw_kernel");
