@@ -245,10 +245,13 @@ class LiveProbe:
         torch.cuda.synchronize()
         return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e3 for k, v in self.ev.items() if v}
 
-    def embed_gaps_us(self):
+    def embed_gaps_us(self, n_side=1):
         """mean time between one frame's last encoder launch ending (enc_head)
         and the next frame's roi stage starting, on the side stream: the side
-        stream's idle time per frame"""
+        stream's idle time per frame (None with several side streams: frames
+        then overlap on purpose)"""
+        if n_side != 1:
+            return None
         ends, starts = self.ev["enc_head"], self.ev["roi_stage"]
         gaps = [e1.elapsed_time(s0) * 1e3 for (_, e1), (s0, _) in zip(ends, starts[1:])]
         return float(np.mean(gaps)) if gaps else None
@@ -418,7 +421,7 @@ def main():
                                torch.cuda.synchronize, dev)
     probe.on = False
     live = probe.means_us()
-    side_gap = probe.embed_gaps_us()
+    side_gap = probe.embed_gaps_us(len(pipe.sides))
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
@@ -481,8 +484,10 @@ def main():
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
           "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": algo[dom][0],
           "algorithmic_flops_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
-          "kernel_us_source": {k: ("live: HIP events around each launch in the timed region" if k in live
-                                   else "isolated: back-to-back launches after the timed region") for k in kt},
+          "kernel_us_source": {k: ("live: HIP events around each launch in the timed region (with two "
+                                   "embedding streams a launch can share the GPU with the other frame's)"
+                                   if k in live else "isolated: back-to-back launches after the timed region")
+                               for k in kt},
           "isolated_us": {k: round(v, 2) for k, v in iso.items()},
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2),
           "embed_stream_idle_us_per_step": None if side_gap is None else round(side_gap, 2)}
