@@ -105,6 +105,21 @@ __device__ __forceinline__ float hswish_f(float v) {
   return v * fminf(fmaxf(v + 3.0f, 0.0f), 6.0f) * (1.0f / 6.0f);
 }
 
+// cross-lane exchanges without the LDS pipe (ds_bpermute): DPP quad_perm for lane ^ 1,
+// gfx950's v_permlane16/32_swap for the half-row / half-wave sums; a + b in either
+// order, so the sums equal x + __shfl_xor(x, 16 / 32) bit for bit
+__device__ __forceinline__ float lane_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ float sum_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
   const int64_t nx = 8;
   if (nwg < nx) return bid;
@@ -301,8 +316,8 @@ __global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
             else s_hi += act;
           }
         }
-        s_lo += __shfl_xor(s_lo, 32);
-        s_hi += __shfl_xor(s_hi, 32);
+        s_lo = sum_xor32(s_lo);
+        s_hi = sum_xor32(s_hi);
         if (lane < 32 && r0 < a.M) {
           const int slot = (int)(roi0 - roi_base);
           atomicAdd(&red[slot * BN + cl], (unsigned long long)llrintf(s_lo * kFix));
@@ -1288,8 +1303,8 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       }
 #pragma unroll
       for (int q = 0; q < G4_WSLOTS; ++q) {
-        ssum[q] += __shfl_xor(ssum[q], 16);
-        ssum[q] += __shfl_xor(ssum[q], 32);
+        ssum[q] = sum_xor16(ssum[q]);
+        ssum[q] = sum_xor32(ssum[q]);
       }
       if (lane < 16) {
 #pragma unroll
@@ -1307,8 +1322,8 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const f4v v = acc[i][t];
-        const float x0 = __shfl_xor(odd ? v[0] : v[2], 1);
-        const float x1 = __shfl_xor(odd ? v[1] : v[3], 1);
+        const float x0 = lane_xor1(odd ? v[0] : v[2]);
+        const float x1 = lane_xor1(odd ? v[1] : v[3]);
         const int rb = wr * 64 + i * 16 + fc * 4 + (odd ? 2 : 0);
         const int cp = (wc * 128 + t * 16 + fr) >> 1;
         stage[rb * G4_SLD + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);

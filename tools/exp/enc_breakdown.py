@@ -38,8 +38,8 @@ def timeit(fn, reps=10):
 items = {
     "g1dw": (lambda: ops.enc_g1_dwconv(X, W1, wdw), [0, 16, 32, 48, 16 | 64, 16 | 128, 16 | 64 | 128], 2 * M * 512 * 1024),
     "plain256": (lambda: ops.enc_gemm(X, W1), [0], 2 * M * 512 * 1024),
-    "dsc": (lambda: ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True), [0, 1, 16, 17], 2 * M * 1024 * 512),
-    "trans": (lambda: ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True), [0, 1, 16, 17], 2 * M * 1024 * 512),
+    "dsc": (lambda: ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True), [0, 1, 2, 4], 2 * M * 1024 * 512),
+    "trans": (lambda: ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True), [0, 1, 4], 2 * M * 1024 * 512),
 }
 offsets = [int(v) for v in os.environ.get("ENC_OFFSETS", "0").split(",")]
 g1p = [int(v) for v in os.environ.get("G1P", "0").split(",")]
