@@ -120,6 +120,11 @@ def lib():
                 _declare(L)
                 if L.trk_abi_version() != 1:
                     raise TrkError("libtrk_amd ABI version mismatch")
+                # TRK_TUNE="key=value,..." applies trk_set_tuning knobs at load (A/B runs)
+                for kv in filter(None, os.environ.get("TRK_TUNE", "").split(",")):
+                    k, v = kv.split("=")
+                    if L.trk_set_tuning(k.strip().encode(), int(v)) != 0:
+                        raise TrkError(f"TRK_TUNE: {L.trk_last_error().decode()}")
                 _lib = L
     return _lib
 

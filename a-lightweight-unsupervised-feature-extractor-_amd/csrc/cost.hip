@@ -22,6 +22,8 @@
 // the one FMA torch's CPU norm performs is written as an explicit fmaf.
 #include "trk_common.h"
 
+int g_cost_v2 = 1;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel (Nmax <= 272), 0 = cost_kernel
+
 namespace {
 
 constexpr int D = 128;           // embedding dim (mainTracking.py:109-110,267-268)
@@ -229,6 +231,116 @@ cost_kernel(const CostArgs A) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// cost2_kernel (default): the track's bank is the resident operand, the
+// detections stream.  Workgroup = (4 tracks, frame), one wave per track.  The
+// prologue renormalises the frame's detections once into LDS (the same double
+// sum-of-squares / f32 divide as cost_kernel, so every B fragment is bit-identical)
+// and precomputes their box / conf / KF-measurement terms; each wave then loads
+// its track's <=30x128 bank into registers ONCE (cost_kernel re-read it for every
+// 32-detection tile: 178 MB of HBM reads per 8 x 256 x 256 launch against 33 MB of
+// algorithmic bytes) and walks the detection tiles with the B fragments read from
+// LDS (row stride 132 floats: the 16-lane groups of a ds_read_b128 hit distinct
+// banks).  MFMA chain, top-k and epilogue are cost_kernel's: identical outputs.
+constexpr int C2_LD = D + 4;
+struct DetTerms {
+  float ccx, ccy, Ac, ccv;
+  double z0, z1, z2, z3;
+};
+constexpr size_t c2_lds_bytes(int nmax) { return (size_t)nmax * C2_LD * 4 + (size_t)nmax * sizeof(DetTerms); }
+
+__global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
+  extern __shared__ __align__(16) float dl[];
+  const int f = blockIdx.y;
+  const int M = A.M[f], N = A.N[f];
+  if ((int)blockIdx.x * 4 >= M || N == 0) return;  // whole workgroup: before any barrier
+  DetTerms* dt_lds = reinterpret_cast<DetTerms*>(dl + (size_t)A.Nmax * C2_LD);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // ---- prologue: renormalised detections (thread pair 2j, 2j + 1 = halves of row j)
+  for (int q = threadIdx.x; q < 2 * N; q += 256) {
+    const int j = q >> 1, h = q & 1;
+    float b[64];
+    load_a_frag(A.det_emb + ((int64_t)f * A.Nmax + j) * D + 64 * h, true, b);
+    double ss = 0.0;
+#pragma unroll
+    for (int s = 0; s < 64; ++s) ss += (double)b[s] * (double)b[s];
+    ss += __shfl_xor(ss, 1);
+    const float nrm = (float)sqrt(ss) + 1e-12f;
+    float* o = dl + j * C2_LD + 64 * h;
+#pragma unroll
+    for (int s = 0; s < 64; s += 4)
+      *reinterpret_cast<float4*>(o + s) = make_float4(b[s] / nrm, b[s + 1] / nrm, b[s + 2] / nrm, b[s + 3] / nrm);
+  }
+  for (int j = threadIdx.x; j < N; j += 256) {
+    DetTerms t;
+    det_terms(A.dbox + ((int64_t)f * A.Nmax + j) * 4, A.conf_cur[(int64_t)f * A.Nmax + j], t.ccx, t.ccy, t.Ac,
+              t.ccv, t.z0, t.z1, t.z2, t.z3);
+    dt_lds[j] = t;
+  }
+  __syncthreads();
+
+  const int i = blockIdx.x * 4 + wave;
+  if (i >= M) return;
+  const int col = lane & 31, h = lane >> 5;
+  const int64_t slot = A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.Mmax + i] : (int64_t)f * A.Mmax + i;
+  const int T = min(A.bank_len[slot], A.Tmax);
+  float a[64];
+  load_a_frag(A.bank + (slot * A.Tmax + col) * D + 64 * h, col < T, a);
+  const int topk = A.p.topk;
+  const bool gate = A.p.gate && A.gate_on[slot];
+  for (int j0 = 0; j0 < N; j0 += 32) {
+    const int j = j0 + col;
+    const bool jok = j < N;
+    float b[64];
+    {
+      const float* bp = dl + (jok ? j : 0) * C2_LD + 64 * h;
+#pragma unroll
+      for (int s = 0; s < 64; s += 4) {
+        const float4 v = jok ? *reinterpret_cast<const float4*>(bp + s) : make_float4(0.f, 0.f, 0.f, 0.f);
+        b[s] = v.x; b[s + 1] = v.y; b[s + 2] = v.z; b[s + 3] = v.w;
+      }
+    }
+    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    float tk[kMaxTopk];
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = (r & 3) + 8 * (r >> 2) + 4 * h;
+      topk_insert(tk, t < T ? acc[r] : -INFINITY);
+    }
+    float other[kMaxTopk];
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) other[q] = __shfl_xor(tk[q], 32);
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) topk_insert(tk, other[q]);
+    const int k = min(topk, T);
+    float app;
+    if (k <= 0) {
+      app = 1.0f;
+    } else {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < kMaxTopk; ++q)
+        if (q < k) sum = sum + tk[q];
+      app = 1.0f - sum / (float)k;
+    }
+    if (h != 0 || !jok) continue;
+    const DetTerms t = dt_lds[j];
+    float cen, scl, cf;
+    const float tot = combine(A.p, app, A.pbox + slot * 4, A.conf_prev[slot], t.ccx, t.ccy, t.Ac, t.ccv, gate,
+                              A.gmean + slot * 4, A.gsinv + slot * 16, t.z0, t.z1, t.z2, t.z3, cen, scl, cf);
+    const int64_t o = ((int64_t)f * A.Mmax + i) * A.Nmax + j;
+    if (A.C_total) A.C_total[o] = tot;
+    if (A.C_app) A.C_app[o] = app;
+    if (A.C_center) A.C_center[o] = cen;
+    if (A.C_scale) A.C_scale[o] = scl;
+    if (A.C_conf) A.C_conf[o] = cf;
+  }
+}
+
 // C_app given (costCard.cal_cost API): elementwise combine over [M, N].
 __global__ void __launch_bounds__(256)
 combine_kernel(int M, int N, const float* __restrict__ C_app, const float* __restrict__ pbox,
@@ -332,6 +444,19 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
     a.C_scale = C_scale ? C_scale + co : nullptr;
     a.C_conf = C_conf ? C_conf + co : nullptr;
     a.p = *host_params;
+    const size_t lds2 = c2_lds_bytes((int)Nmax);
+    if (g_cost_v2 && lds2 <= 160 * 1024) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(cost2_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      dim3 grid((unsigned)((mmax + 3) / 4), (unsigned)nf);
+      hipLaunchKernelGGL(cost2_kernel, grid, dim3(256), lds2, st, a);
+      if (int e = trk::check_launch("cost2_kernel")) return e;
+      continue;
+    }
     dim3 grid((unsigned)((nmax + 31) / 32), (unsigned)((mmax + kRowsPerWG - 1) / kRowsPerWG), (unsigned)nf);
     hipLaunchKernelGGL(cost_kernel, grid, dim3(256), 0, st, a);
     if (int e = trk::check_launch("cost_kernel")) return e;

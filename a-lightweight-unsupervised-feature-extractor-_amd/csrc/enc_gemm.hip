@@ -812,6 +812,163 @@ __global__ void __launch_bounds__(640, 5) g1dw_ws_kernel(const uint16_t* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// g1dw with 256-channel N tiles (g1dw_mode 5): one 16-wave workgroup per CU per
+// tile of 2 ROIs x 256 channels.  Against the 128-channel tile it halves the
+// L2 -> LDS traffic of the A operand (each X row is staged 4 instead of 8 times:
+// 1.9 instead of 2.95 GB per launch), which the K loop pays for one-to-one
+// (DESIGN.md §4).  Waves: row parity wr = wave >> 3 (row tiles wr + 2t), column
+// tile wave & 7 (the g1dw_tile split over 8 column tiles).  Depthwise: 20 tasks
+// (ROI, output row pair, 128-channel half) over the 16 waves.  LDS: Y1 [200][128
+// pairs] + weights [25][128] (128 KiB), the operand ring aliased below it.
+constexpr int G2_BN = 256;
+constexpr size_t G2_STAGE = (size_t)(G1_ROWS + G2_BN) * CPR * 16;      // 30 KiB
+constexpr size_t G2_TILE = (size_t)2 * G1_P * (G2_BN / 2) * 4;         // 100 KiB
+constexpr size_t G2_W = (size_t)25 * (G2_BN / 2) * 8;                  // 25 KiB
+constexpr size_t G2_LDS = NSTAGE * G2_STAGE > G2_TILE + G2_W ? NSTAGE * G2_STAGE : G2_TILE + G2_W;
+static_assert(G2_LDS <= 160 * 1024, "g1dw256 LDS");
+
+__global__ void __launch_bounds__(1024) g1dw256_kernel(const uint16_t* __restrict__ X,
+                                                       const uint16_t* __restrict__ W1,
+                                                       const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
+                                                       int M, int N) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* As = reinterpret_cast<uint4*>(smem);          // [NSTAGE][224 * CPR]
+  uint4* Bs = As + NSTAGE * G1_AP;                      // [NSTAGE][256 * CPR]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 7, wr = wave >> 3;
+  const int ntile_n = N / G2_BN;
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(lb % ntile_n) * G2_BN;
+  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);
+  constexpr int K = 512, NK = K / BK;
+  constexpr int BP = G2_BN * CPR;                       // B pieces per stage (1024)
+
+  // DMA: A pieces 0..895 (threads 0..895), B pieces 0..1023 (all threads)
+  const uint16_t* asrc;
+  {
+    const int p = min(tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
+    asrc = X + min(m0 + r, (int64_t)M - 1) * K + c * 8;
+  }
+  const uint16_t* bsrc = W1 + (int64_t)(n0 + tid / CPR) * K + unswz_c(tid) * 8;
+  const bool adma = wave < G1_AP / 64;                  // waves 0..13 stage A pieces
+  auto issue = [&](int stage, int k0) {
+    if (adma) __builtin_amdgcn_global_load_lds(GPTR(asrc + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * BP + wave * 64), 16, 0, 0);
+  };
+  constexpr int TMX = 4;
+  const int ntm = wr == 0 ? 4 : 3;
+  f16_t acc[TMX];
+#pragma unroll
+  for (int i = 0; i < TMX; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  issue(0, 0);
+  issue(1, BK);
+  for (int kt = 0; kt < NK; ++kt) {
+    if (kt + 1 < NK) {
+      if (adma) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const uint4* as = As + (kt % NSTAGE) * G1_AP;
+    const uint4* bs = Bs + (kt % NSTAGE) * BP;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int c = ks * 2 + (lane >> 5);
+      const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
+#pragma unroll
+      for (int i = 0; i < TMX; ++i) {
+        if (i < ntm) {
+          const int rt = wr + 2 * i;
+          const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    if (kt + 2 < NK) {  // after this step's MFMAs (g1dw_mode 1); the buffer was last read in step kt - 1
+      __builtin_amdgcn_sched_barrier(0);
+      issue((kt + 2) % NSTAGE, (kt + 2) * BK);
+    }
+  }
+  __syncthreads();
+
+  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
+  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G2_TILE);
+  {
+    const int cl = wn * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TMX; ++i) {
+      if (i < ntm) {
+        const int rt = wr + 2 * i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G2_BN + cl] = trk::f32_to_bf16(acc[i][r]);
+        }
+      }
+    }
+  }
+  for (int q = tid; q < 25 * (G2_BN / 2); q += 1024) {
+    const int k = q / (G2_BN / 2), pp = q % (G2_BN / 2);
+    wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
+  }
+  __syncthreads();
+
+  // depthwise 5x5: task = (ROI, output row pair, 128-channel half), lane = channel pair
+  for (int task = wave; task < 20; task += 16) {
+    const int roi = task / 10, rem = task % 10, y0 = 2 * (rem % 5), cp = (rem / 5) * 64 + lane;
+    const int64_t rbase = m0 + roi * G1_P;
+    if (rbase >= M) continue;
+    const uint32_t* src = y1 + roi * G1_P * (G2_BN / 2);
+    dw_pair_t a0[G1_S], a1[G1_S];
+#pragma unroll
+    for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int yy = y0 - 2 + r;
+      if (yy < 0 || yy >= G1_S) continue;
+      dw_pair_t rr[G1_S];
+#pragma unroll
+      for (int x = 0; x < G1_S; ++x) {
+        const uint32_t v = src[(yy * G1_S + x) * (G2_BN / 2) + cp];
+        rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+      }
+      if (r <= 4) {
+        dw_pair_t wv[5];
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G2_BN / 2) + cp];
+#pragma unroll
+        for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx)
+            if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
+      }
+      if (r >= 1) {
+        dw_pair_t wv[5];
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G2_BN / 2) + cp];
+#pragma unroll
+        for (int x = 0; x < G1_S; ++x)
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx)
+            if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
+      }
+    }
+    uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
+#pragma unroll
+    for (int x = 0; x < G1_S; ++x) {
+      dst[(y0 * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a0[x].x, a0[x].y);
+      dst[((y0 + 1) * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a1[x].x, a1[x].y);
+    }
+  }
+}
+
 // persistent: two workgroups per CU take tiles from the queue; each CU's second
 // workgroup starts offset x 2048 cycles late so its K loop runs beside the first
 // one's depthwise phase
@@ -1531,6 +1688,18 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
                        (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg, nwg,
                        next_queue_slot(), g_g1dw_persist - 1);
     return trk::check_launch("g1dw_persist_kernel");
+  }
+  if (g_g1dw_mode == 5 && N % 256 == 0) {
+    static bool attr_256 = false;
+    if (!attr_256) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw256_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G2_LDS);
+      attr_256 = true;
+    }
+    const int64_t nwg2 = (M / 200 + (M % 200 ? 1 : 0)) * (N / 256);
+    hipLaunchKernelGGL(g1dw256_kernel, dim3((unsigned)nwg2), dim3(1024), G2_LDS, st, (const uint16_t*)X,
+                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+    return trk::check_launch("g1dw256_kernel");
   }
   if (g_g1dw_mode == 4) {
     TRK_REQUIRE(M * 512 < (int64_t)1 << 31, "enc_g1_dwconv: M * 512 must stay below 2^31");

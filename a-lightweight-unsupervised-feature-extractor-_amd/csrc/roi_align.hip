@@ -712,7 +712,8 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "roi_sweep")) { TRK_REQUIRE(value >= 0 && value <= 2, "roi_sweep in {0,1,2}"); g_roi_sweep = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm_offset")) { extern int g_enc_gemm_offset; TRK_REQUIRE(value >= 0 && value <= 64, "enc_gemm_offset in [0, 64]"); g_enc_gemm_offset = value; return TRK_OK; }
   if (!strcmp(key, "g1dw_persist")) { extern int g_g1dw_persist; TRK_REQUIRE(value >= 0 && value <= 66, "g1dw_persist in [0, 66]"); g_g1dw_persist = value; return TRK_OK; }
-  if (!strcmp(key, "g1dw_mode")) { extern int g_g1dw_mode; TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "g1dw_mode in {0, 1, 2, 4}"); g_g1dw_mode = value; return TRK_OK; }
+  if (!strcmp(key, "g1dw_mode")) { extern int g_g1dw_mode; TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 5, "g1dw_mode in {0, 1, 2, 4, 5}"); g_g1dw_mode = value; return TRK_OK; }
+  if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm_dbg")) { extern int g_enc_gemm_dbg; g_enc_gemm_dbg = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value == 0 || value == 1, "enc_gemm in {0,1}"); g_enc_gemm = value; return TRK_OK; }
   if (!strcmp(key, "dw_fast")) { extern int g_dw_fast; TRK_REQUIRE(value == 0 || value == 1, "dw_fast in {0,1}"); g_dw_fast = value; return TRK_OK; }

@@ -208,6 +208,15 @@ def test_cost_kernel_full_size_vs_oracle(trk, oracle, gpu):
     assert np.array_equal(got["C_total"] >= 1e9, exp["C_total"] >= 1e9)
     assert np.max(np.abs(got["C_total"] - exp["C_total"])) <= 2e-6
     assert (exp["C_total"] >= 1e9).mean() > 0.5  # the gate is exercised
+    # bank-resident kernel (cost_v2, default) and the det-tile kernel: identical outputs
+    L = trk.lib()
+    try:
+        assert L.trk_set_tuning(b"cost_v2", 0) == 0
+        got1 = _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf)
+    finally:
+        assert L.trk_set_tuning(b"cost_v2", 1) == 0
+    for k in got:
+        assert np.array_equal(got[k], got1[k]), k
 
 
 def test_cost_batched_frames_with_row_slots(trk, oracle, gpu):
@@ -415,7 +424,7 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
             finally:
                 assert L.trk_set_tuning(b"g1dw_persist", 0) == 0
             assert torch.equal(Yp, Yu) and torch.equal(Yp2, Yu)
-        for mode in (0, 2, 4, 1):   # DMA placement / warp-specialised variants (1: default)
+        for mode in (0, 2, 4, 5, 1):   # DMA placement / warp-specialised / 256-wide variants (1: default)
             assert L.trk_set_tuning(b"g1dw_mode", mode) == 0
             assert torch.equal(ops.enc_g1_dwconv(X, W1, wdw), Yu), mode
     for v in (1, 3):
