@@ -22,7 +22,8 @@
 // the one FMA torch's CPU norm performs is written as an explicit fmaf.
 #include "trk_common.h"
 
-int g_cost_v2 = 1;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel (Nmax <= 272), 0 = cost_kernel
+int g_cost_v2 = 0;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel (Nmax <= 272; its 147 KiB LDS
+                    // workgroups stall behind the encoder in the pipeline: 1.23M vs 1.51M ROIs/s), 0 = cost_kernel
 
 namespace {
 

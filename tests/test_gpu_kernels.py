@@ -208,13 +208,13 @@ def test_cost_kernel_full_size_vs_oracle(trk, oracle, gpu):
     assert np.array_equal(got["C_total"] >= 1e9, exp["C_total"] >= 1e9)
     assert np.max(np.abs(got["C_total"] - exp["C_total"])) <= 2e-6
     assert (exp["C_total"] >= 1e9).mean() > 0.5  # the gate is exercised
-    # bank-resident kernel (cost_v2, default) and the det-tile kernel: identical outputs
+    # det-tile kernel (default) and the bank-resident kernel (cost_v2): identical outputs
     L = trk.lib()
     try:
-        assert L.trk_set_tuning(b"cost_v2", 0) == 0
+        assert L.trk_set_tuning(b"cost_v2", 1) == 0
         got1 = _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf)
     finally:
-        assert L.trk_set_tuning(b"cost_v2", 1) == 0
+        assert L.trk_set_tuning(b"cost_v2", 0) == 0
     for k in got:
         assert np.array_equal(got[k], got1[k]), k
 
