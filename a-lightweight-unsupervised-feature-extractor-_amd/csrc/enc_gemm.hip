@@ -1416,9 +1416,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
         acc[i][t][2 * h + 1] = v.y;
       }
   }
-  unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));
-  for (int q = tid; q < G4_SLOTS * 256; q += 256) red[q] = 0ull;
-  __syncthreads();
+  // per-ROI column sums: each row-half wave (wr) writes its f32 partials for every tile
+  // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
+  // consumer adds llrintf(p0 * 2^24) + llrintf(p1 * 2^24) (the former int64 atomics' sum)
+  float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [2][SLOTS][256]
   if (!(a.dbg & 4)) {
     const int64_t r0w = m0 + wr * 64;
     const int64_t roiw = r0w / a.P;
@@ -1465,9 +1466,13 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       }
       if (lane < 16) {
 #pragma unroll
-        for (int q = 0; q < G4_WSLOTS; ++q)
-          if (q <= slot && wslot0 + q < G4_SLOTS && ssum[q] != 0.f)
-            atomicAdd(&red[(wslot0 + q) * 256 + colq + t * 16], (unsigned long long)llrintf(ssum[q] * kFix));
+        for (int ts = 0; ts < G4_SLOTS; ++ts) {
+          float v = 0.f;
+#pragma unroll
+          for (int q = 0; q < G4_WSLOTS; ++q)
+            if (q <= slot && wslot0 + q == ts) v = ssum[q];
+          part[(wr * G4_SLOTS + ts) * 256 + colq + t * 16] = v;
+        }
       }
     }
   }
@@ -1496,7 +1501,8 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
         const int slot = q >> 8, c = q & 255;
         const int64_t roi = roi_base + slot;
         const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
-        a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] = (long long)red[q];
+        a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] =
+            llrintf(part[slot * 256 + c] * kFix) + llrintf(part[(G4_SLOTS + slot) * 256 + c] * kFix);
       }
   }
   if (EPI == EPI_DSC && !(a.dbg & 2)) {
