@@ -390,8 +390,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # RCCL ("nccl") over xGMI; TRK_DIST_BACKEND=gloo rehearses the multi-rank path with
+        # several ranks on one device (RCCL refuses two ranks per GPU)
+        backend = os.environ.get("TRK_DIST_BACKEND", "nccl")
+        if backend != "nccl":
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
