@@ -38,11 +38,20 @@ enum { TRK_NCHW = 0, TRK_NHWC = 1 };
 
 int trk_abi_version(void);
 const char* trk_last_error(void);
-/* Performance knobs (process-global; results are bit-identical for every value):
+/* Performance knobs (process-global; results are bit-identical for every value
+ * unless noted; the defaults are the fastest measured in the pipelined bench):
  *   "roi_window_kb"  LDS budget (KiB) for staging a ROI's source window; 0 = never stage
  *   "roi_vec"        channels per lane in roi_align (0 = auto, 1, 2, 4)
  *   "roi_sweep"      1 (default): NHWC output through the row-sweep kernel; 0: per-sample taps
- *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel */
+ *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel
+ *   "enc_gemm"       1 (default): pipelined 128x256 DSC / transition GEMMs; 0: the 128x128 /
+ *                    128x256 kernels (same math, another f32 summation order)
+ *   "enc_gemm_offset" 0 (default): one workgroup per tile; > 0: persistent tile queue
+ *   "g1dw_mode"      first-GEMM + depthwise kernel: 1 (default) DMA after the MFMAs, 0 before,
+ *                    2 interleaved, 4 dedicated DMA waves, 5 256-channel tiles
+ *   "g1dw_persist"   0 (default); > 0: persistent tile queue; 66: depthwise interleaved into the
+ *                    next tile's K loop
+ *   "cost_v2"        0 (default): detection-tile cost kernel; 1: bank-resident kernel */
 int trk_set_tuning(const char* key, int value);
 
 /* ------------------------------------------------------------------------
