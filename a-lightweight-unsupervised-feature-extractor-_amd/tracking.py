@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -155,6 +156,7 @@ class MultiStreamTracker:
         self.streams = [StreamState(capacity, s * capacity) for s in range(n_streams)]
         self.params = default_cost_params(self.cfg, gate=True)
         self.params_nogate = default_cost_params(self.cfg, gate=False)
+        self.sync_wait_s = 0.0  # host time blocked on the per-frame index copies (bench diagnostics)
 
     # ------------------------------------------------------------ helpers --
     def _i32(self, a) -> torch.Tensor:
@@ -252,8 +254,10 @@ class MultiStreamTracker:
             if after_launch is not None:
                 after_launch()
                 after_launch = None
+            t_w = time.perf_counter()
             st_h = lres["status"].cpu().numpy()
             assign = lres["assign"].cpu().numpy()  # the host sync of mainTracking.py:503
+            self.sync_wait_s += time.perf_counter() - t_w
             for s in active:
                 if len(main[s]) == 0:
                     continue

@@ -213,7 +213,9 @@ class LiveProbe:
 
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
-             "trk_enc_se": "enc_se", "trk_enc_head": "enc_head"}
+             "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
+             "trk_lsap": "lsap_live", "trk_kf_predict": "kf_predict", "trk_track_update": "track_update",
+             "trk_track_init": "track_init"}
 
     def __init__(self):
         self.on = False
@@ -244,6 +246,13 @@ class LiveProbe:
     def means_us(self):
         torch.cuda.synchronize()
         return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e3 for k, v in self.ev.items() if v}
+
+    def sum_per_step_us(self, steps):
+        """summed device time of every probed launch per step: compared with
+        ms_per_step it shows whether streams overlapped (sum > step) or the GPU
+        idled (sum < step)"""
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for v in self.ev.values() for a, b in v) * 1e3 / max(steps, 1)
 
     def embed_gaps_us(self, n_side=1):
         """mean time between one frame's last encoder launch ending (enc_head)
@@ -425,10 +434,13 @@ def main():
 
     probe = LiveProbe()
     probe.on = True
+    pipe.tracker.sync_wait_s = 0.0
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
                                torch.cuda.synchronize, dev)
     probe.on = False
+    kernel_sum = probe.sum_per_step_us(args.steps)
     live = probe.means_us()
+    live = {k: v for k, v in live.items() if not k.endswith("_live")}
     side_gap = probe.embed_gaps_us(len(pipe.sides))
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
@@ -499,6 +511,34 @@ def main():
           "isolated_us": {k: round(v, 2) for k, v in iso.items()},
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2),
           "embed_stream_idle_us_per_step": None if side_gap is None else round(side_gap, 2)}
+    # end-to-end ROIs/s against min(HBM / B_roi, MFMA / F_roi), with
+    # B_roi = 12,800 (map share) + 2 x 102,400 (bf16 ROI tensor written + read) + 512
+    # (embedding) + 16,900 (cost share) B and F_roi = the encoder's flops per ROI
+    b_roi = Fs * 512 * 40 * 40 * 4 / K + 2 * 512 * S * S * 2 + 512 + 16900
+    cap = min(HBM_PEAK_GBS * 1e9 / b_roi, BF16_PEAK_TFLOPS * 1e12 / ENC_FLOP_PER_ROI[S])
+    rf["end_to_end"] = {"achieved": round(value / world, 1), "unit": "ROIs/s per GPU", "cap": round(cap, 1),
+                        "frac": round(value / world / cap, 4), "bytes_per_roi": round(b_roi),
+                        "flops_per_roi": ENC_FLOP_PER_ROI[S],
+                        "cap_rule": "min(8 TB/s / bytes_per_roi, 2.5 PFLOP/s / flops_per_roi)"}
+    # PMC bytes over algorithmic bytes per kernel (committed profile), beside each stage's fraction
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as fh:
+            pk = json.load(fh)["kernels"]
+        rf["traffic_over_algorithmic"] = {k: round((pk[k]["read_bytes"] + pk[k]["write_bytes"]) / algo[k][0], 3)
+                                          for k in algo if k in pk}
+    except (OSError, KeyError, ValueError):
+        rf["traffic_over_algorithmic"] = None
+    rf["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL",
+                                                "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
+                 if os.environ.get(k) is not None}
+    step_us = el / args.steps * 1e6
+    rf["step_breakdown"] = {
+        "step_us": round(step_us, 1),
+        "kernel_sum_us": round(kernel_sum, 1),
+        "overlap": round(kernel_sum / step_us, 3),
+        "host_sync_wait_us": round(pipe.tracker.sync_wait_s / args.steps * 1e6, 1),
+        "note": "kernel_sum = device time of every probed launch per step (live HIP events); overlap > 1 "
+                "means streams ran concurrently; host_sync_wait = time the host blocked on the index copy"}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",
         "value": round(value, 1), "unit": "ROIs/s", "n_gpus": world, "steps": args.steps,

@@ -1,0 +1,146 @@
+"""End-to-end chains of the hot path on the GPU (through the C ABI).
+
+* c3 size (BASELINE.json configs[2], the bench's shape): 8 frames x 256 ROIs
+  of 10x10 = 2,048 ROIs = 204,800 encoder GEMM rows, through the bf16 fused
+  encoder (default g1dw / gemm4 paths, full XCD-remapped grids) against the
+  fp32 encoder path, which tests/test_gpu_kernels.py pins to the reference's
+  golden (<= 1e-4).  Tolerances: per-row cosine >= 0.999; LSAP assignments
+  from build_cost identical (and equal to the synthetic identity) on
+  margin-separated tracks.
+* c2 chain (configs[1]): [1,512,40,40], N = M = 64, fp32:
+  roi_align -> encoder -> build_cost (gated) -> lsap on the GPU against
+  oracle.roi_align -> oracle.encoder_forward -> oracle.cost_build ->
+  oracle.lsap.  Tolerances: embeddings and costs <= 1e-4 (north_star),
+  assignment indices equal.
+References: encoderAndHead.py:21-26, tracking.py:193-221, mainTracking.py:141-338,
+hung.py:5-45.
+"""
+import numpy as np
+import pytest
+import torch
+
+import gen_common as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _boxes(rng, n, img=1280, pad=280):
+    w = rng.uniform(32, 320, n)
+    h = rng.uniform(32, 320, n)
+    x1 = rng.uniform(0, img - w)
+    y1 = rng.uniform(pad, img - pad - h)
+    return np.stack([x1, y1, x1 + w, y1 + h], 1).astype(np.float32)
+
+
+def _renorm(x):
+    x = np.asarray(x, np.float32)
+    n = np.sqrt((x.astype(np.float64) ** 2).sum(-1, keepdims=True)).astype(np.float32) + np.float32(1e-12)
+    return (x / n).astype(np.float32)
+
+
+def _model(trk, gpu):
+    sd = {k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict(sd, strict=True)
+    return m.to(gpu), sd
+
+
+def _tracks_for(rng, emb, dbox, noise=0.05):
+    """tracks whose banks / predicted boxes follow the detections through a
+    permutation: track i <-> detection perm[i]"""
+    N = emb.shape[0]
+    perm = rng.permutation(N)
+    bank = _renorm(emb[perm][:, None, :] + noise * rng.standard_normal((N, 30, 128)))
+    pbox = (dbox[perm] + rng.normal(0, 1.0, (N, 4))).astype(np.float32)
+    lconf = rng.uniform(0.55, 0.99, N).astype(np.float32)
+    return perm, bank, pbox, lconf
+
+
+def test_c3_bf16_encoder_full_size_vs_fp32(trk, gpu):
+    rng = np.random.default_rng(2048)
+    F, N = 8, 256
+    feat = torch.from_numpy(G.silu_np(rng.standard_normal((F, 512, 40, 40)).astype(np.float32))
+                            .astype(np.float32)).to(gpu)
+    boxes = np.stack([_boxes(rng, N) for _ in range(F)])
+    rois = np.concatenate([np.repeat(np.arange(F), N).astype(np.float32)[:, None], boxes.reshape(-1, 4)], 1)
+    r = torch.from_numpy(rois).to(gpu)
+    model, _ = _model(trk, gpu)
+    with torch.no_grad():
+        roi32 = trk.roi_align(feat, r, (10, 10), 40 / 1280.0, 2, True)
+        z32 = model(roi32)
+        roib = trk.roi_align(feat, r, (10, 10), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16,
+                             channels_last=True)
+        zb = model(roib)
+    assert zb.shape == (F * N, 128) and zb.dtype == torch.float32
+    assert torch.isfinite(zb).all()
+    cos = (zb * z32).sum(1)
+    assert cos.min().item() >= 0.999, cos.min().item()
+    # deterministic at full size (fixed-point ROI sums, no atomics on values)
+    with torch.no_grad():
+        zb2 = model(roib)
+    assert torch.equal(zb, zb2)
+    # assignments: one gated cost + LSAP launch over the 8 frames, per embedding path
+    e32 = z32.view(F, N, 128).cpu().numpy()
+    banks, pboxes, lconfs, perms = [], [], [], []
+    for f in range(F):
+        perm, bank, pbox, lconf = _tracks_for(rng, e32[f], boxes[f])
+        banks.append(bank); pboxes.append(pbox); lconfs.append(lconf); perms.append(perm)
+    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(gpu, dt)
+    bank = t(np.concatenate(banks))
+    dconf = rng.uniform(0.55, 0.99, (F, N)).astype(np.float32)
+    assigns = []
+    for emb in (z32, zb):
+        C = trk.build_cost(M=[N] * F, N=[N] * F, bank=bank, bank_len=t(np.full(F * N, 30, np.int32), torch.int32),
+                           pbox=t(np.concatenate(pboxes)), conf_prev=t(np.concatenate(lconfs)),
+                           det_emb=emb.view(F, N, 128).contiguous(), dbox=t(boxes), conf_cur=t(dconf),
+                           params=trk.default_cost_params(gate=False))["C_total"]
+        res = trk.lsap_batched(C, [N] * F, [N] * F, cost_max=50.0)
+        assert (res["status"].cpu().numpy() == 0).all()
+        assigns.append(res["assign"].cpu().numpy())
+    assert np.array_equal(assigns[0], assigns[1])
+    for f in range(F):
+        assert np.array_equal(assigns[0][f], perms[f]), f
+
+
+def test_c2_chain_fp32_vs_oracle(trk, oracle, gpu):
+    rng = np.random.default_rng(64)
+    N = 64
+    feat = G.silu_np(rng.standard_normal((1, 512, 40, 40)).astype(np.float32)).astype(np.float32)
+    boxes = _boxes(rng, N)
+    rois = np.concatenate([np.zeros((N, 1), np.float32), boxes], 1)
+    model, sd = _model(trk, gpu)
+    # 1) roi_align: bit-exact
+    roi = trk.roi_align(torch.from_numpy(feat).to(gpu), torch.from_numpy(rois).to(gpu), (10, 10), 40 / 1280.0,
+                        2, True)
+    roi_o = oracle.roi_align(feat, rois, (10, 10), 40 / 1280.0, 2, True)
+    assert np.array_equal(roi.cpu().numpy(), roi_o)
+    # 2) encoder: <= 1e-4
+    with torch.no_grad():
+        emb = model(roi)
+        emb_o = oracle.encoder_forward(sd, torch.from_numpy(roi_o)).numpy()
+    assert np.max(np.abs(emb.cpu().numpy() - emb_o)) <= 1e-4
+    # 3) gated cost on tracks built from the oracle's embeddings: <= 1e-4, same gate decisions
+    perm, bank, pbox, lconf = _tracks_for(rng, emb_o, boxes, noise=0.08)
+    dconf = rng.uniform(0.55, 0.99, N).astype(np.float32)
+    x = np.zeros((N, 8))
+    x[:, :4] = np.stack([(pbox[:, 0] + pbox[:, 2]) / 2, (pbox[:, 1] + pbox[:, 3]) / 2,
+                         (pbox[:, 2] - pbox[:, 0]) / (pbox[:, 3] - pbox[:, 1]), pbox[:, 3] - pbox[:, 1]], 1)
+    P = np.tile(np.diag([10., 10, 10, 10, 1000, 1000, 1000, 1000]), (N, 1, 1))
+    gm, gs = oracle.gate_params(x, P)
+    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(gpu, dt)
+    out = trk.build_cost(M=[N], N=[N], bank=t(bank), bank_len=t(np.full(N, 30, np.int32), torch.int32),
+                         pbox=t(pbox), conf_prev=t(lconf), det_emb=emb.view(1, N, 128).contiguous(),
+                         dbox=t(boxes[None]), conf_cur=t(dconf[None]), params=trk.default_cost_params(gate=True),
+                         gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
+                         gate_on=t(np.ones(N, np.int32), torch.int32), want=("C_total", "C_app"))
+    exp = oracle.cost_build(bank, np.full(N, 30, np.int32), emb_o, pbox, boxes, lconf, dconf, gm, gs,
+                            np.ones(N, np.int32))
+    C = out["C_total"][0].cpu().numpy()
+    assert np.max(np.abs(out["C_app"][0].cpu().numpy() - exp["C_app"])) <= 1e-4
+    assert np.array_equal(C >= 1e9, exp["C_total"] >= 1e9)
+    assert np.max(np.abs(C - exp["C_total"])) <= 1e-4
+    # 4) LSAP on each side's own cost: identical indices (and the synthetic identity)
+    r, c = trk.linear_sum_assignment(out["C_total"][0])
+    er, ec = oracle.lsap(exp["C_total"])
+    assert np.array_equal(r, er) and np.array_equal(c, ec)
+    assert np.array_equal(r, np.arange(N)) and np.array_equal(c, perm)
