@@ -35,6 +35,25 @@ class CostParams(ctypes.Structure):
                 ("inf_cost", ctypes.c_float), ("topk", ctypes.c_int), ("gate", ctypes.c_int)]
 
 
+_STEP_PTRS = ("x P pbox last_conf gmean gsinv enc bank bank_len bank_head alive tid miss age last_frame "
+              "order n_live next_id ndet frame_id flags m1 row1 m2 row2 n2 ud freelist e2 b2 c2 ap_n ap_slot "
+              "ap_det ap_kind ap_cost lsap_status result").split()
+
+
+class StepState(ctypes.Structure):
+    # mirrors trk_step_state (include/trk_amd.h): device pointers, in declaration order
+    _fields_ = [(n, ctypes.c_void_p) for n in _STEP_PTRS]
+
+
+class StepConfig(ctypes.Structure):
+    # mirrors trk_step_config (include/trk_amd.h)
+    _fields_ = [("S", ctypes.c_int64), ("cap", ctypes.c_int64), ("Nmax", ctypes.c_int64), ("T", ctypes.c_int64),
+                ("lost_reid_after", ctypes.c_int), ("max_age", ctypes.c_int),
+                ("init_conf_min", ctypes.c_double), ("conf_update_min", ctypes.c_double),
+                ("cost_update_max", ctypes.c_double), ("reid_only_cost_max", ctypes.c_double),
+                ("maha_thr", ctypes.c_double), ("ema_alpha", ctypes.c_float)]
+
+
 def _declare(L):
     P, i32, i64, sz, f32, f64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t,
                                  ctypes.c_float, ctypes.c_double)
@@ -86,6 +105,20 @@ def _declare(L):
     L.trk_track_update.restype = i32
     L.trk_track_init.argtypes = [i64, P, P, P, P, P, P, P, P, P, P, P, P, P, i64, P]
     L.trk_track_init.restype = i32
+    SP, SC = ctypes.POINTER(StepState), ctypes.POINTER(StepConfig)
+    L.trk_step_result_stride.argtypes = [i64, i64]
+    L.trk_step_result_stride.restype = i64
+    L.trk_step_begin.argtypes = [SP, SC, P, P, i64, P]
+    L.trk_step_mid.argtypes = [SP, SC, i64, P, P, P, P, P, P]
+    L.trk_step_end.argtypes = [SP, SC, i64, P, P, P, P, P]
+    L.trk_step_apply.argtypes = [SP, SC, P, P, P, P, P]
+    for n in ("trk_step_begin", "trk_step_mid", "trk_step_end", "trk_step_apply"):
+        getattr(L, n).restype = i32
+    L.trk_build_cost_dev.argtypes = [i64, i64, i64, P, P, P, i64, i64, P, P, P, P, P, P, P, P, P, P,
+                                     ctypes.POINTER(CostParams), P, P, P]
+    L.trk_build_cost_dev.restype = i32
+    L.trk_lsap_dev.argtypes = [i64, P, i32, i64, i64, P, P, i64, i64, i64, P, P, P, P, P, i64, f64, P]
+    L.trk_lsap_dev.restype = i32
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

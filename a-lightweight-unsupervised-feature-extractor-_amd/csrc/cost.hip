@@ -38,6 +38,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 struct CostArgs {
   int F, Mmax, Nmax, Tmax;
+  int rs_ld;                // row_slot row stride
+  const int32_t* dev_M;     // per-frame sizes in device memory (trk_build_cost_dev), else M / N below
+  const int32_t* dev_N;
   const int32_t* row_slot;
   const float* bank;
   const int32_t* bank_len;
@@ -140,7 +143,8 @@ cost_kernel(const CostArgs A) {
   const int f = blockIdx.z;
   const int j0 = blockIdx.x * 32;
   const int i0 = blockIdx.y * kRowsPerWG + wave * kRowsPerWave;
-  const int M = A.M[f], N = A.N[f];
+  const int M = A.dev_M ? min(A.dev_M[f], A.Mmax) : A.M[f];
+  const int N = A.dev_N ? min(A.dev_N[f], A.Nmax) : A.N[f];
   if (j0 >= N || blockIdx.y * kRowsPerWG >= M) return;
   const int col = lane & 31, h = lane >> 5;
   const int j = j0 + col;
@@ -169,7 +173,7 @@ cost_kernel(const CostArgs A) {
   const int Tmax = A.Tmax;
   const int topk = A.p.topk;
   auto slot_of = [&](int i) -> int64_t {
-    return A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.Mmax + i] : (int64_t)f * A.Mmax + i;
+    return A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.rs_ld + i] : (int64_t)f * A.Mmax + i;
   };
 
   float a[64];
@@ -253,7 +257,8 @@ constexpr size_t c2_lds_bytes(int nmax) { return (size_t)nmax * C2_LD * 4 + (siz
 __global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
   extern __shared__ __align__(16) float dl[];
   const int f = blockIdx.y;
-  const int M = A.M[f], N = A.N[f];
+  const int M = A.dev_M ? min(A.dev_M[f], A.Mmax) : A.M[f];
+  const int N = A.dev_N ? min(A.dev_N[f], A.Nmax) : A.N[f];
   if ((int)blockIdx.x * 4 >= M || N == 0) return;  // whole workgroup: before any barrier
   DetTerms* dt_lds = reinterpret_cast<DetTerms*>(dl + (size_t)A.Nmax * C2_LD);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -283,7 +288,7 @@ __global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
   const int i = blockIdx.x * 4 + wave;
   if (i >= M) return;
   const int col = lane & 31, h = lane >> 5;
-  const int64_t slot = A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.Mmax + i] : (int64_t)f * A.Mmax + i;
+  const int64_t slot = A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.rs_ld + i] : (int64_t)f * A.Mmax + i;
   const int T = min(A.bank_len[slot], A.Tmax);
   float a[64];
   load_a_frag(A.bank + (slot * A.Tmax + col) * D + 64 * h, col < T, a);
@@ -424,7 +429,7 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
     }
     if (mmax == 0 || nmax == 0) continue;
     const int64_t fr = f0;
-    a.F = nf; a.Mmax = (int)Mmax; a.Nmax = (int)Nmax; a.Tmax = (int)Tmax;
+    a.F = nf; a.Mmax = (int)Mmax; a.Nmax = (int)Nmax; a.Tmax = (int)Tmax; a.rs_ld = (int)Mmax;
     a.row_slot = row_slot ? row_slot + fr * Mmax : nullptr;
     // without row_slot, slot = f*Mmax + i indexes the per-frame-packed arrays
     const int64_t so = row_slot ? 0 : fr * Mmax;
@@ -459,6 +464,48 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
       continue;
     }
     dim3 grid((unsigned)((nmax + 31) / 32), (unsigned)((mmax + kRowsPerWG - 1) / kRowsPerWG), (unsigned)nf);
+    hipLaunchKernelGGL(cost_kernel, grid, dim3(256), 0, st, a);
+    if (int e = trk::check_launch("cost_kernel")) return e;
+  }
+  return TRK_OK;
+}
+
+extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* dev_M, const int32_t* dev_N,
+                                  const int32_t* row_slot, int64_t rs_ld, int64_t Tmax, const float* bank,
+                                  const int32_t* bank_len, const float* pbox, const float* conf_prev,
+                                  const double* gmean, const double* gsinv, const int32_t* gate_on,
+                                  const float* det_emb, const float* dbox, const float* conf_cur,
+                                  const trk_cost_params* host_params, float* C_total, float* C_app, void* stream) {
+  TRK_REQUIRE(F >= 0 && Mmax >= 0 && Nmax >= 0, "build_cost_dev: negative shape");
+  TRK_REQUIRE(host_params, "build_cost_dev: null params");
+  TRK_REQUIRE(Tmax >= 1 && Tmax <= 32, "build_cost_dev: Tmax (hist_max) must be in [1, 32], got %lld",
+              (long long)Tmax);
+  TRK_REQUIRE(host_params->topk >= 0 && host_params->topk <= kMaxTopk, "build_cost_dev: topk must be in [0, %d]",
+              kMaxTopk);
+  TRK_REQUIRE(Mmax < (1 << 30) && Nmax < (1 << 30) && rs_ld >= 0 && rs_ld < (1 << 30), "build_cost_dev: shape too large");
+  if (F == 0 || Mmax == 0 || Nmax == 0) return TRK_OK;
+  TRK_REQUIRE(dev_M && dev_N && row_slot, "build_cost_dev: null size / row_slot arrays");
+  TRK_REQUIRE(bank && bank_len && pbox && conf_prev && det_emb && dbox && conf_cur, "build_cost_dev: null input");
+  TRK_REQUIRE(!host_params->gate || (gmean && gsinv && gate_on), "build_cost_dev: gating needs gmean/gsinv/gate_on");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t f0 = 0; f0 < F; f0 += kMaxFrames) {
+    const int nf = (int)std::min<int64_t>(kMaxFrames, F - f0);
+    CostArgs a;
+    memset(&a, 0, sizeof a);
+    a.F = nf; a.Mmax = (int)Mmax; a.Nmax = (int)Nmax; a.Tmax = (int)Tmax; a.rs_ld = (int)rs_ld;
+    a.dev_M = dev_M + f0;
+    a.dev_N = dev_N + f0;
+    a.row_slot = row_slot + f0 * rs_ld;
+    a.bank = bank; a.bank_len = bank_len; a.pbox = pbox; a.conf_prev = conf_prev;
+    a.gmean = gmean; a.gsinv = gsinv; a.gate_on = gate_on;
+    a.det_emb = det_emb + f0 * Nmax * D;
+    a.dbox = dbox + f0 * Nmax * 4;
+    a.conf_cur = conf_cur + f0 * Nmax;
+    const int64_t co = f0 * Mmax * Nmax;
+    a.C_total = C_total ? C_total + co : nullptr;
+    a.C_app = C_app ? C_app + co : nullptr;
+    a.p = *host_params;
+    dim3 grid((unsigned)((Nmax + 31) / 32), (unsigned)((Mmax + kRowsPerWG - 1) / kRowsPerWG), (unsigned)nf);
     hipLaunchKernelGGL(cost_kernel, grid, dim3(256), 0, st, a);
     if (int e = trk::check_launch("cost_kernel")) return e;
   }

@@ -51,6 +51,9 @@ struct LsapArgs {
   int32_t* assign;
   double cost_max;
   int ring_rows;  // RB (ring capacity in rows) for the largest working nc of the batch
+  const int32_t* dev_nr;  // trk_lsap_dev: shapes in device memory, bounded by nr_bound / nc_bound
+  const int32_t* dev_nc;
+  int nr_bound, nc_bound;
   int nr[kMaxBatch];
   int nc[kMaxBatch];
 };
@@ -109,11 +112,21 @@ lsap_kernel(const LsapArgs A) {
   const int f = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nr0 = A.nr[f], nc0 = A.nc[f];
+  int nr0 = A.nr[f], nc0 = A.nc[f];
   const T* C = reinterpret_cast<const T*>(A.C) + (int64_t)f * A.batch_stride;
   int32_t* assign = A.assign ? A.assign + (int64_t)f * A.nr_max : nullptr;
   int64_t* orows = A.rows + (int64_t)f * A.kmax;
   int64_t* ocols = A.cols + (int64_t)f * A.kmax;
+  if (A.dev_nr) {
+    nr0 = A.dev_nr[f];
+    nc0 = A.dev_nc[f];
+    if (nr0 < 0 || nc0 < 0 || nr0 > A.nr_bound || nc0 > A.nc_bound) {  // outside the launch's sizing
+      if (assign)
+        for (int r = threadIdx.x; r < A.nr_bound; r += blockDim.x) assign[r] = -1;
+      if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = -4; }
+      return;
+    }
+  }
   if (nr0 == 0 || nc0 == 0) {
     if (assign)
       for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
@@ -186,6 +199,7 @@ lsap_kernel(const LsapArgs A) {
     double v[KS], spc[KS];
     int path[KS], r4c[KS], pos[KS];
     bool exists[KS], alive[KS];
+    const int ks = (nc + 63) >> 6;  // column slots in use (KS is the launch's bound)
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       exists[k] = lane + 64 * k < nc;
@@ -225,21 +239,22 @@ lsap_kernel(const LsapArgs A) {
           const int slot = whole ? i : i % RB;
           const T* lrow = ring + (int64_t)slot * nc;
 #pragma unroll
-          for (int k = 0; k < KS; ++k) cv[k] = exists[k] ? lrow[lane + 64 * k] : (T)0;
+          for (int k = 0; k < KS; ++k) cv[k] = (k < ks && exists[k]) ? lrow[lane + 64 * k] : (T)0;
         } else {
 #pragma unroll
-          for (int k = 0; k < KS; ++k) cv[k] = alive[k] ? gload(i, lane + 64 * k) : (T)0;
+          for (int k = 0; k < KS; ++k) cv[k] = (k < ks && alive[k]) ? gload(i, lane + 64 * k) : (T)0;
         }
         double best = INFINITY;
         int bkey = 0x7fffffff, bcol = -1;
 #pragma unroll
         for (int k = 0; k < KS; ++k) {  // branch-free: dead columns are masked
+          // (k < ks: uniform skip of the slots past the matrix width)
           const double r = ((minVal + (double)cv[k]) - ui) - v[k];
-          const bool upd = alive[k] && r < spc[k];
+          const bool upd = k < ks && alive[k] && r < spc[k];
           path[k] = upd ? i : path[k];
           spc[k] = upd ? r : spc[k];
           const int key = r4c[k] == -1 ? -1 - pos[k] : pos[k];
-          const bool take = alive[k] && key_less(spc[k], key, best, bkey);
+          const bool take = k < ks && alive[k] && key_less(spc[k], key, best, bkey);
           best = take ? spc[k] : best;
           bkey = take ? key : bkey;
           bcol = take ? lane + 64 * k : bcol;
@@ -269,7 +284,7 @@ lsap_kernel(const LsapArgs A) {
       wave_sync();
 #pragma unroll
       for (int k = 0; k < KS; ++k) {
-        if (!exists[k] || alive[k]) continue;
+        if (k >= ks || !exists[k] || alive[k]) continue;
         const double d = minVal - spc[k];
         if (lane + 64 * k != sink) u[r4c[k]] += d;
         v[k] -= d;
@@ -412,6 +427,59 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
     rb = std::max(rb, 2);
     a.ring_rows = rb;
     const size_t lds = fixed + (size_t)rb * row_bytes + 16;
+    a.C = reinterpret_cast<const char*>(C) + (size_t)f0 * batch_stride * esz;
+    a.ld = ld;
+    a.batch_stride = batch_stride;
+    a.kmax = kmax;
+    a.nr_max = nr_max;
+    a.rows = rows + f0 * kmax;
+    a.cols = cols + f0 * kmax;
+    a.count = count + f0;
+    a.status = status + f0;
+    a.assign = assign ? assign + f0 * nr_max : nullptr;
+    a.cost_max = cost_max;
+    int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
+                             : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
+    if (e) return e;
+  }
+  return TRK_OK;
+}
+
+extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stride,
+                            const int32_t* dev_nr, const int32_t* dev_nc, int64_t nr_bound, int64_t nc_bound,
+                            int64_t kmax, int64_t* rows, int64_t* cols, int32_t* count, int32_t* status,
+                            int32_t* assign, int64_t nr_max, double cost_max, void* stream) {
+  TRK_REQUIRE(F >= 0, "lsap_dev: negative batch");
+  TRK_REQUIRE(dtype == TRK_F32 || dtype == TRK_F64, "lsap_dev: dtype must be f32 or f64");
+  if (F == 0) return TRK_OK;
+  TRK_REQUIRE(dev_nr && dev_nc && rows && cols && count && status, "lsap_dev: null pointer");
+  TRK_REQUIRE(nr_bound >= 0 && nc_bound >= 0 && nr_bound <= TRK_LSAP_MAX_DIM && nc_bound <= TRK_LSAP_MAX_DIM,
+              "lsap_dev: bounds (%lld, %lld) outside [0, %d]", (long long)nr_bound, (long long)nc_bound,
+              TRK_LSAP_MAX_DIM);
+  TRK_REQUIRE(nc_bound <= ld, "lsap_dev: ld %lld < nc bound %lld", (long long)ld, (long long)nc_bound);
+  TRK_REQUIRE(std::min(nr_bound, nc_bound) <= kmax, "lsap_dev: kmax < min(nr, nc) bound");
+  TRK_REQUIRE(!assign || nr_bound <= nr_max, "lsap_dev: nr_max < nr bound");
+  TRK_REQUIRE(C, "lsap_dev: null cost pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const size_t esz = dtype == TRK_F32 ? 4 : 8;
+  const size_t lds_limit = 156 * 1024;
+  const int wr_max = (int)std::max<int64_t>(1, std::min(nr_bound, nc_bound));
+  const int wc_max = (int)std::max<int64_t>(1, std::max(nr_bound, nc_bound));
+  const size_t fixed = 12 * (size_t)wr_max + 64;
+  const size_t row_bytes = esz * (size_t)wc_max + 4;
+  TRK_REQUIRE(fixed + 2 * row_bytes <= lds_limit, "lsap_dev: matrix too wide for the LDS ring");
+  int rb = (int)std::min<size_t>((lds_limit - fixed) / row_bytes, (size_t)wr_max);
+  rb = std::max(rb, 2);
+  const size_t lds = fixed + (size_t)rb * row_bytes + 16;
+  for (int64_t f0 = 0; f0 < F; f0 += kMaxBatch) {
+    const int nf = (int)std::min<int64_t>(kMaxBatch, F - f0);
+    LsapArgs a;
+    memset(&a, 0, sizeof a);
+    a.ring_rows = rb;
+    a.dev_nr = dev_nr + f0;
+    a.dev_nc = dev_nc + f0;
+    a.nr_bound = (int)nr_bound;
+    a.nc_bound = (int)nc_bound;
     a.C = reinterpret_cast<const char*>(C) + (size_t)f0 * batch_stride * esz;
     a.ld = ld;
     a.batch_stride = batch_stride;

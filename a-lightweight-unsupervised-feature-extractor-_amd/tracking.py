@@ -1,22 +1,23 @@
 """Tracker state machine over device-resident track tables.
 
-Drop-in for reference model/mainTracking.py (class Tracking):
-the per-frame association runs on gfx950 kernels --
+Drop-in for reference model/mainTracking.py (class Tracking).
+Every per-frame decision runs on gfx950 kernels, for all video streams at once:
 
-  predict_all          -> trk_kf_predict   (KF predict + predicted box + gate inputs)
-  cal_cost + gating    -> trk_build_cost   (bank top-k appearance, bbox, conf, Mahalanobis)
-  hungarian_assign     -> trk_lsap         (scipy-exact SAP + the cost_max gate)
-  update_matched       -> trk_track_update (KF update, appearance gates, EMA, bank push)
-  create_new_tracks    -> trk_track_init
+  predict_all + row split        -> trk_step_begin   (:474-487)
+  cal_cost + apply_kalman_gating -> trk_build_cost_dev (bank top-k appearance, bbox, conf, Mahalanobis)
+  hungarian_assign               -> trk_lsap_dev     (scipy-exact SAP + the cost_max gate)
+  stage-1 bookkeeping            -> trk_step_mid     (matches, misses, unmatched dets, stage-2 inputs)
+  stage 2 (ReID-only)            -> trk_build_cost_dev (C_app) + trk_lsap_dev
+  stage-2 bookkeeping, create_new_tracks, purge_dead -> trk_step_end
+  update_matched + new tracks    -> trk_step_apply   (KF update, appearance gates, EMA, bank push, init)
 
--- while the per-track bookkeeping that the reference keeps in Python dicts
-(ids, miss counts, ages, the main / ReID-only row split, purge) stays on the
-host as numpy arrays.  ``MultiStreamTracker`` batches S independent video
-streams through one launch per stage; ``Tracking`` is its single-stream form
-with the reference's method names, argument meanings and error behaviour.
-Host syncs: one per frame after stage 1 (plus one after stage 2 when a
-long-lost ReID-only stage runs), where the reference already syncs
-(mainTracking.py:503,559).
+The ids, miss counts, ages and live lists the reference keeps in Python dicts
+live in HBM next to the Kalman state (TrackTable), so the host enqueues a frame
+and never waits inside it; the frame's results reach the host through one
+device->pinned copy.  ``MultiStreamTracker`` batches S independent streams;
+``Tracking`` is its single-stream form with the reference's method names,
+argument meanings and error behaviour (it waits for each frame, as the
+reference returns each frame's matches).
 """
 from __future__ import annotations
 
@@ -29,7 +30,8 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import check, lib
+from ._lib import (_STEP_PTRS, TRK_F32, TRK_LSAP_MAX_DIM, StepConfig, StepState, TrkError, check,
+                   lib)
 from .ops import (_device, _ptr, _stream, build_cost, cost_combine, default_cost_params,
                   lsap_batched)
 
@@ -73,47 +75,49 @@ def tracker_conf(conf: Optional[Dict[str, Any]] = None, conf_path: Optional[str]
 
 
 class TrackTable:
-    """Slot arrays of every track of every stream (layout: include/trk_amd.h)."""
+    """Slot arrays of every track of every stream (layout: include/trk_amd.h):
+    the Kalman state and memory bank, plus the bookkeeping the reference keeps
+    in its Python dicts (alive, track id, miss count, age, last frame) and, per
+    stream, the live slots in ascending track id with their count and next id."""
 
-    def __init__(self, slots: int, hist_max: int, device):
-        self.S, self.T, self.device = slots, hist_max, device
+    def __init__(self, n_streams: int, cap: int, hist_max: int, device):
+        S = n_streams * cap
+        self.n_streams, self.cap, self.S, self.T, self.device = n_streams, cap, S, hist_max, device
         z = lambda *s, dt=torch.float32: torch.zeros(s, device=device, dtype=dt)
-        self.x = z(slots, 8, dt=torch.float64)
-        self.P = z(slots, 64, dt=torch.float64)
-        self.pbox = z(slots, 4)
-        self.last_conf = z(slots)
-        self.gmean = z(slots, 4, dt=torch.float64)
-        self.gsinv = z(slots, 16, dt=torch.float64)
-        self.gate_on = torch.ones(slots, device=device, dtype=torch.int32)
-        self.enc = z(slots, D)
-        self.bank = z(slots, hist_max, D)
-        self.bank_len = z(slots, dt=torch.int32)
-        self.bank_head = z(slots, dt=torch.int32)
+        self.x = z(S, 8, dt=torch.float64)
+        self.P = z(S, 64, dt=torch.float64)
+        self.pbox = z(S, 4)
+        self.last_conf = z(S)
+        self.gmean = z(S, 4, dt=torch.float64)
+        self.gsinv = z(S, 16, dt=torch.float64)
+        self.gate_on = torch.ones(S, device=device, dtype=torch.int32)
+        self.enc = z(S, D)
+        self.bank = z(S, hist_max, D)
+        self.bank_len = z(S, dt=torch.int32)
+        self.bank_head = z(S, dt=torch.int32)
+        self.alive = z(S, dt=torch.int32)
+        self.tid = torch.full((S,), -1, device=device, dtype=torch.int64)
+        self.miss = z(S, dt=torch.int32)
+        self.age = z(S, dt=torch.int32)
+        self.last_frame = z(S, dt=torch.int64)
+        self.order = z(n_streams, cap, dt=torch.int32)
+        self.n_live = z(n_streams, dt=torch.int32)
+        self.next_id = z(n_streams, dt=torch.int64)
 
+    SLOT_ARRAYS = ("x", "P", "pbox", "last_conf", "gmean", "gsinv", "gate_on", "enc", "bank", "bank_len",
+                   "bank_head", "alive", "tid", "miss", "age", "last_frame")
 
-@dataclass
-class StreamState:
-    """Host bookkeeping of one stream's tracks (Tracking.tracks of the reference)."""
-    cap: int
-    base: int
-    alive: np.ndarray = None
-    tid: np.ndarray = None
-    miss: np.ndarray = None
-    age: np.ndarray = None
-    last_frame: np.ndarray = None
-    next_id: int = 0
-
-    def __post_init__(self):
-        self.alive = np.zeros(self.cap, bool)
-        self.tid = np.full(self.cap, -1, np.int64)
-        self.miss = np.zeros(self.cap, np.int64)
-        self.age = np.zeros(self.cap, np.int64)
-        self.last_frame = np.zeros(self.cap, np.int64)
-
-    def live_sorted(self) -> np.ndarray:
-        """local slots of live tracks in ascending track id (= dict order)."""
-        s = np.flatnonzero(self.alive)
-        return s[np.argsort(self.tid[s], kind="stable")]
+    def grown(self, cap: int) -> "TrackTable":
+        """A copy with `cap` slots per stream (local slot numbers are kept)."""
+        t = TrackTable(self.n_streams, cap, self.T, self.device)
+        n = self.n_streams
+        for k in self.SLOT_ARRAYS:
+            old, new = getattr(self, k), getattr(t, k)
+            new.view(n, cap, *new.shape[1:])[:, :self.cap].copy_(old.view(n, self.cap, *old.shape[1:]))
+        t.order[:, :self.cap].copy_(self.order)
+        t.n_live.copy_(self.n_live)
+        t.next_id.copy_(self.next_id)
+        return t
 
 
 _EMPTY = np.zeros(0, np.int64)
@@ -134,258 +138,302 @@ class FrameResult:
                 [int(x) for x in self.unmatched_dets])
 
 
+class SolverStallError(TrkError):
+    """The LSAP solver's bounded wait expired (an internal stall, not an
+    infeasible matrix); the frame's result is not valid."""
+
+
+def _raise_status(st: int, s: int):
+    if st == -1:
+        raise ValueError("matrix contains invalid numeric entries")
+    if st == -2:
+        raise ValueError("cost matrix is infeasible")
+    if st == -3:
+        raise SolverStallError(f"stream {s}: LSAP solver stalled (bounded wait expired)")
+    if st == -4:
+        raise TrkError(f"stream {s}: live tracks exceed the frame's launch bound (internal error)")
+    if st == -5:
+        raise TrkError(f"stream {s}: track capacity exhausted (internal error: the table grows before a frame)")
+    raise TrkError(f"stream {s}: tracker step failed with status {st}")
+
+
+class StepHandle:
+    """A frame in flight: its results are copied into pinned host memory by the
+    stream; result() waits for that copy only (frames are consumed in order)."""
+
+    def __init__(self, tracker, seq, buf, event, S, Nmax, cap, after_N):
+        self._tr, self.seq, self._buf, self._ev = tracker, seq, buf, event
+        self._S, self._Nmax, self._cap, self._after = S, Nmax, cap, after_N
+        self._res = None
+
+    def done(self) -> bool:
+        return self._res is not None or self._ev.query()
+
+    def result(self) -> List[FrameResult]:
+        if self._res is None:
+            self._tr._consume_through(self)
+        if isinstance(self._res, Exception):
+            raise self._res
+        return self._res
+
+    def _parse(self):
+        self._ev.synchronize()
+        stride, Nmax, cap = self._tr._stride, self._Nmax, self._cap
+        r = self._buf.numpy()[:self._S * stride].reshape(self._S, stride)
+        out, err = [], None
+        for s in range(self._S):
+            h = r[s, :8]
+            if h[4] != 0 and err is None:
+                try:
+                    _raise_status(int(h[4]), s)
+                except Exception as e:  # noqa: BLE001 -- re-raised by result()
+                    err = e
+            nm, nu, nd = int(h[0]), int(h[1]), int(h[2])
+            mt, md = r[s, 8:8 + Nmax], r[s, 8 + Nmax:8 + 2 * Nmax]
+            ut, ud = r[s, 8 + 2 * Nmax:8 + 2 * Nmax + cap], r[s, 8 + 2 * Nmax + cap:8 + 3 * Nmax + cap]
+            out.append(FrameResult(np.stack([mt[:nm], md[:nm]], 1).copy(), ut[:nu].copy(), ud[:nd].copy()))
+        live = r[:, 3].copy()
+        self._res = err if err is not None else out
+        return live
+
+
 class MultiStreamTracker:
     """S independent trackers (one per video stream) advanced together.
 
     step() takes the detections of one frame of every stream, already on the
     device: det_emb [S, Nmax, 128] f32, dbox [S, Nmax, 4] f32, dconf [S, Nmax]
-    f32, plus the host copies of the confidences (creation gate) and the
-    counts N[s].  Returns one FrameResult per stream, identical to what
-    mainTracking.Tracking.update would return for that stream."""
+    f32 and the counts N[s].  Returns one FrameResult per stream, identical to
+    what mainTracking.Tracking.update would return for that stream.
+
+    Every per-frame decision is made on the device (trk_step_* + the cost and
+    LSAP kernels, one launch sequence per frame for all streams): the host
+    enqueues a frame and never waits inside it.  step_async() returns a
+    StepHandle whose results arrive through one device->pinned-host copy; at
+    most `max_inflight` frames are left unread (the oldest is then consumed).
+    The table grows (doubling `capacity`) when a frame could overflow it, as the
+    reference's dict of tracks does (mainTracking.py:362-373)."""
 
     def __init__(self, n_streams: int, conf: Optional[Dict[str, Any]] = None, *,
-                 capacity: int = 1024, device=None, conf_path: Optional[str] = None):
+                 capacity: int = 1024, device=None, conf_path: Optional[str] = None, max_inflight: int = 3):
         self.cfg = tracker_conf(conf, conf_path)
         self.n_streams = n_streams
-        self.cap = capacity
         self.device = torch.device(device) if device is not None else _device()
         self.T = int(self.cfg["hist_max"])
         if self.T > 32:
             raise NotImplementedError("hist_max > 32 is not supported by the cost kernel")
-        self.table = TrackTable(n_streams * capacity, self.T, self.device)
-        self.streams = [StreamState(capacity, s * capacity) for s in range(n_streams)]
+        self.table = TrackTable(n_streams, int(capacity), self.T, self.device)
         self.params = default_cost_params(self.cfg, gate=True)
         self.params_nogate = default_cost_params(self.cfg, gate=False)
-        self.sync_wait_s = 0.0  # host time blocked on the per-frame index copies (bench diagnostics)
+        self.max_inflight = max(1, int(max_inflight))
+        self._nmax = 0
+        self._pending: List[StepHandle] = []
+        self._pool: List[torch.Tensor] = []
+        self._seq = 0
+        self._live_exact = np.zeros(n_streams, np.int64)   # n_live after the last consumed frame
+        self._cum_N = np.zeros(n_streams, np.int64)        # detections launched so far
+        self._cum_at_exact = np.zeros(n_streams, np.int64)
+        self.sync_wait_s = 0.0  # host time blocked waiting on results (bench diagnostics)
 
-    # ------------------------------------------------------------ helpers --
-    def _i32(self, a) -> torch.Tensor:
-        return torch.as_tensor(np.ascontiguousarray(a, np.int32)).to(self.device, non_blocking=True)
+    @property
+    def cap(self) -> int:
+        return self.table.cap
+
+    # ---------------------------------------------------------- buffers --
+    def _scratch(self, Nmax: int):
+        """per-frame device scratch sized for (capacity, Nmax)"""
+        if Nmax <= self._nmax and self._scr_cap == self.cap:
+            return
+        self._nmax = max(Nmax, self._nmax)
+        self._scr_cap = self.cap
+        S, cap, Nm, dev = self.n_streams, self.cap, self._nmax, self.device
+        i32 = lambda *s: torch.zeros(s, device=dev, dtype=torch.int32)
+        f32 = lambda *s: torch.zeros(s, device=dev, dtype=torch.float32)
+        self._scr = dict(ndet=i32(S), frame_id=torch.zeros(S, device=dev, dtype=torch.int64), flags=i32(S),
+                         m1=i32(S), row1=i32(S, cap), m2=i32(S), row2=i32(S, cap), n2=i32(S), ud=i32(S, Nm),
+                         freelist=i32(S, cap), e2=f32(S, Nm, D), b2=f32(S, Nm, 4), c2=f32(S, Nm),
+                         ap_n=i32(S), ap_slot=i32(S, Nm), ap_det=i32(S, Nm), ap_kind=i32(S, Nm), ap_cost=f32(S, Nm),
+                         lsap_status=i32(2, S))
+        self._stride = int(lib().trk_step_result_stride(cap, Nm))
+        self._scr["result"] = torch.zeros(S * self._stride, device=dev, dtype=torch.int64)
+        km = min(cap, Nm)
+        self._lsap = [dict(rows=torch.empty((S, km), device=dev, dtype=torch.int64),
+                           cols=torch.empty((S, km), device=dev, dtype=torch.int64),
+                           count=torch.empty(S, device=dev, dtype=torch.int32),
+                           assign=torch.empty((S, cap), device=dev, dtype=torch.int32)) for _ in range(2)]
+        self._C = [torch.empty(S * cap * Nm, device=dev, dtype=torch.float32) for _ in range(2)]
+        self._pool = []  # result buffers of the old layout
+        t = self.table
+        self._state = StepState(*[_ptr(getattr(t, n)) if hasattr(t, n) and n not in self._scr else
+                                  _ptr(self._scr[n]) for n in _STEP_PTRS])
+        self._conf = StepConfig(S, cap, Nm, self.T, int(self.cfg["lost_reid_after"]), int(self.cfg["max_age"]),
+                                float(self.cfg["init_conf_min"]), float(self.cfg["conf_update_min"]),
+                                float(self.cfg["cost_update_max"]), float(self.cfg["reid_only_cost_max"]),
+                                float(self.cfg["maha_thr"]), float(self.cfg["ema_alpha"]))
+
+    _scr_cap = -1
+
+    def _result_buf(self) -> torch.Tensor:
+        if self._pool:
+            return self._pool.pop()
+        return torch.empty(self.n_streams * self._stride, dtype=torch.int64, pin_memory=True)
+
+    # ------------------------------------------------------- consumption --
+    def _consume_through(self, h: StepHandle):
+        t0 = time.perf_counter()
+        while self._pending:
+            q = self._pending.pop(0)
+            live = q._parse()
+            self._live_exact = live
+            self._cum_at_exact = q._after
+            if q._buf.numel() == self.n_streams * self._stride:
+                self._pool.append(q._buf)
+            if q is h:
+                break
+        self.sync_wait_s += time.perf_counter() - t0
+
+    def drain(self):
+        """Wait for every frame in flight (their results stay readable)."""
+        if self._pending:
+            self._consume_through(self._pending[-1])
+
+    def _live_ub(self) -> np.ndarray:
+        """upper bound of each stream's live tracks now: the last read count plus
+        every detection launched since (each can at most start a track)"""
+        return self._live_exact + (self._cum_N - self._cum_at_exact)
+
+    def _grow(self, need: int):
+        cap = self.cap
+        while cap < need:
+            cap *= 2
+        self.drain()
+        self.table = self.table.grown(cap)
+        self._nmax = 0
+        self._scratch(max(1, self._last_nmax))
+
+    # --------------------------------------------------------------- step --
+    def step_async(self, det_emb: torch.Tensor, dbox: torch.Tensor, dconf: torch.Tensor, N: Sequence[int],
+                   frame_ids: Optional[Sequence[int]] = None, dconf64: Optional[torch.Tensor] = None,
+                   after_launch: Optional[Any] = None) -> StepHandle:
+        S = self.n_streams
+        if det_emb.dim() != 3 or det_emb.shape[0] != S or det_emb.shape[2] != D:
+            raise ValueError(f"det_embs must be [S, Nmax, {D}], got {tuple(det_emb.shape)}")
+        Nmax = det_emb.shape[1]
+        N = np.asarray([int(n) for n in N], np.int64)
+        if len(N) != S or (N < 0).any() or (N > Nmax).any():
+            raise ValueError("N must hold one count in [0, Nmax] per stream")
+        if Nmax == 0:  # pad to one (never read) detection row
+            det_emb = torch.zeros((S, 1, D), device=self.device)
+            dbox = torch.zeros((S, 1, 4), device=self.device)
+            dconf = torch.zeros((S, 1), device=self.device)
+            dconf64 = None
+            Nmax = 1
+        det_emb = det_emb.to(self.device, torch.float32).contiguous()
+        dbox = dbox.to(self.device, torch.float32).contiguous()
+        dconf = dconf.to(self.device, torch.float32).contiguous()
+        if dconf64 is not None:
+            dconf64 = dconf64.to(self.device, torch.float64).contiguous()
+        self._last_nmax = Nmax
+        # a frame can add at most N[s] tracks: grow the table before it could overflow
+        if (self._live_ub() + N > self.cap).any():
+            self.drain()
+            need = int((self._live_exact + N).max())
+            if need > self.cap:
+                self._grow(need)
+        self._scratch(Nmax)
+        if Nmax > self._nmax:
+            raise AssertionError("scratch sizing")
+        if len(self._pending) >= self.max_inflight:
+            self._consume_through(self._pending[0])
+        Mb = int(min(self.cap, max(1, self._live_ub().max())))
+        if Mb > TRK_LSAP_MAX_DIM:
+            raise NotImplementedError(f"more than {TRK_LSAP_MAX_DIM} live tracks in one stream")
+        fid = np.asarray(list(frame_ids) if frame_ids is not None else [0] * S, np.int64)
+        st, cf, t, sc = self._state, self._conf, self.table, self._scr
+        Nm = self._nmax
+        if Nm != Nmax:  # detections laid out with the scratch's stride
+            pad = lambda x, *tail: torch.nn.functional.pad(x, (0, 0) * len(tail) + (0, Nm - Nmax))
+            det_emb, dbox, dconf = pad(det_emb, D), pad(dbox, 4), pad(dconf)
+            if dconf64 is not None:
+                dconf64 = pad(dconf64)
+        stream = _stream(self.device)
+        L = lib()
+        hN = (ctypes.c_int32 * S)(*N.tolist())
+        hF = (ctypes.c_int64 * S)(*fid.tolist())
+        check(L.trk_step_begin(ctypes.byref(st), ctypes.byref(cf), hN, hF, Mb, stream), "step_begin")
+        C1, C2 = self._C
+        l1, l2 = self._lsap
+        p = ctypes.byref
+        check(L.trk_build_cost_dev(S, Mb, Nm, _ptr(sc["m1"]), _ptr(sc["ndet"]), _ptr(sc["row1"]), self.cap, self.T,
+                                   _ptr(t.bank), _ptr(t.bank_len), _ptr(t.pbox), _ptr(t.last_conf), _ptr(t.gmean),
+                                   _ptr(t.gsinv), _ptr(t.gate_on), _ptr(det_emb), _ptr(dbox), _ptr(dconf),
+                                   p(self.params), _ptr(C1), None, stream), "build_cost (stage 1)")
+        check(L.trk_lsap_dev(S, _ptr(C1), TRK_F32, Nm, Mb * Nm, _ptr(sc["m1"]), _ptr(sc["ndet"]), Mb, Nm,
+                             min(self.cap, Nm), _ptr(l1["rows"]), _ptr(l1["cols"]), _ptr(l1["count"]),
+                             _ptr(sc["lsap_status"][0]), _ptr(l1["assign"]), Mb, float(self.cfg["cost_max"]), stream),
+              "lsap (stage 1)")
+        check(L.trk_step_mid(p(st), p(cf), Mb, _ptr(C1), _ptr(l1["assign"]), _ptr(det_emb), _ptr(dbox), _ptr(dconf),
+                             stream), "step_mid")
+        check(L.trk_build_cost_dev(S, Mb, Nm, _ptr(sc["m2"]), _ptr(sc["n2"]), _ptr(sc["row2"]), self.cap, self.T,
+                                   _ptr(t.bank), _ptr(t.bank_len), _ptr(t.pbox), _ptr(t.last_conf), None, None, None,
+                                   _ptr(sc["e2"]), _ptr(sc["b2"]), _ptr(sc["c2"]), p(self.params_nogate), None,
+                                   _ptr(C2), stream), "build_cost (stage 2)")
+        check(L.trk_lsap_dev(S, _ptr(C2), TRK_F32, Nm, Mb * Nm, _ptr(sc["m2"]), _ptr(sc["n2"]), Mb, Nm,
+                             min(self.cap, Nm), _ptr(l2["rows"]), _ptr(l2["cols"]), _ptr(l2["count"]),
+                             _ptr(sc["lsap_status"][1]), _ptr(l2["assign"]), Mb,
+                             float(self.cfg["reid_only_cost_max"]), stream), "lsap (stage 2)")
+        check(L.trk_step_end(p(st), p(cf), Mb, _ptr(C2), _ptr(l2["assign"]), _ptr(dconf64), _ptr(dconf), stream),
+              "step_end")
+        buf = self._result_buf()
+        buf.copy_(sc["result"], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        check(L.trk_step_apply(p(st), p(cf), _ptr(det_emb), _ptr(dbox), _ptr(dconf), _ptr(dconf64), stream),
+              "step_apply")
+        # the caller's detection tensors must outlive the frame's kernels
+        for x in (det_emb, dbox, dconf, dconf64):
+            if x is not None:
+                x.record_stream(torch.cuda.current_stream(self.device))
+        self._cum_N = self._cum_N + N
+        self._seq += 1
+        h = StepHandle(self, self._seq, buf, ev, S, Nm, self.cap, self._cum_N.copy())
+        self._pending.append(h)
+        if after_launch is not None:
+            after_launch()
+        return h
+
+    def step(self, det_emb: torch.Tensor, dbox: torch.Tensor, dconf: torch.Tensor,
+             N: Sequence[int], confs_host: Optional[Sequence[Sequence[float]]] = None,
+             frame_ids: Optional[Sequence[int]] = None,
+             after_launch: Optional[Any] = None) -> List[FrameResult]:
+        """Synchronous step.  confs_host: optional host copies of the confidences
+        (the caller's floats: the creation and appearance gates compare them in
+        double like the reference, mainTracking.py:365,416); otherwise dconf is
+        used.  after_launch: optional callable run once the frame is enqueued and
+        before the host waits for its results."""
+        dconf64 = None
+        if confs_host is not None:
+            Nmax = det_emb.shape[1]
+            h = np.zeros((self.n_streams, max(Nmax, 1)), np.float64)
+            for s, c in enumerate(confs_host):
+                c = np.asarray(c, np.float64).reshape(-1)
+                h[s, :len(c)] = c
+            dconf64 = torch.from_numpy(h[:, :Nmax] if Nmax else h).to(self.device)
+        return self.step_async(det_emb, dbox, dconf, N, frame_ids, dconf64, after_launch).result()
+
+    # ------------------------------------------------------ device views --
+    def live_slots(self, s: int) -> np.ndarray:
+        """global slots of stream s's live tracks in ascending track id (syncs)"""
+        self.drain()
+        n = int(self.table.n_live[s].item())
+        return s * self.cap + self.table.order[s, :n].cpu().numpy().astype(np.int64)
 
     def _predict(self, slots: np.ndarray):
         if len(slots) == 0:
             return
         t = self.table
-        s = self._i32(slots)
-        check(lib().trk_kf_predict(len(slots), _ptr(s), _ptr(t.x), _ptr(t.P), _ptr(t.pbox), _ptr(t.gmean),
+        sl = torch.as_tensor(np.ascontiguousarray(slots, np.int32)).to(self.device)
+        check(lib().trk_kf_predict(len(slots), _ptr(sl), _ptr(t.x), _ptr(t.P), _ptr(t.pbox), _ptr(t.gmean),
                                    _ptr(t.gsinv), _stream(self.device)), "kf_predict")
-
-    def _update(self, slots, dets, cost: Optional[torch.Tensor], cost_idx, cost_update_max, maha_thr,
-                det_emb, dbox, dconf):
-        if len(slots) == 0:
-            return
-        t = self.table
-        s, d = self._i32(slots), self._i32(dets)
-        ci = (torch.as_tensor(np.asarray(cost_idx, np.int64)).to(self.device, non_blocking=True)
-              if cost is not None else None)
-        check(lib().trk_track_update(len(slots), _ptr(s), _ptr(d), _ptr(ci), _ptr(cost), _ptr(dbox),
-                                     _ptr(dconf), _ptr(det_emb), _ptr(t.x), _ptr(t.P), _ptr(t.pbox),
-                                     _ptr(t.last_conf), _ptr(t.enc), _ptr(t.bank), _ptr(t.bank_len),
-                                     _ptr(t.bank_head), self.T, float(self.cfg["ema_alpha"]),
-                                     float(self.cfg["conf_update_min"]), float(cost_update_max),
-                                     float(maha_thr), _stream(self.device)), "track_update")
-
-    def _init(self, slots, dets, det_emb, dbox, dconf):
-        if len(slots) == 0:
-            return
-        t = self.table
-        s, d = self._i32(slots), self._i32(dets)
-        check(lib().trk_track_init(len(slots), _ptr(s), _ptr(d), _ptr(dbox), _ptr(dconf), _ptr(det_emb),
-                                   _ptr(t.x), _ptr(t.P), _ptr(t.pbox), _ptr(t.last_conf), _ptr(t.enc),
-                                   _ptr(t.bank), _ptr(t.bank_len), _ptr(t.bank_head), self.T,
-                                   _stream(self.device)), "track_init")
-
-    # --------------------------------------------------------------- step --
-    def step(self, det_emb: torch.Tensor, dbox: torch.Tensor, dconf: torch.Tensor,
-             N: Sequence[int], confs_host: Sequence[Sequence[float]],
-             frame_ids: Optional[Sequence[int]] = None,
-             after_launch: Optional[Any] = None) -> List[FrameResult]:
-        """after_launch: optional callable run once the stage-1 LSAP is enqueued and
-        before the host waits for its indices -- e.g. to enqueue the next frame's
-        ROI Align + encoder on another stream while the solver runs."""
-        cfg = self.cfg
-        S = self.n_streams
-        if det_emb.dim() != 3 or det_emb.shape[0] != S or det_emb.shape[2] != D:
-            raise ValueError(f"det_embs must be [S, Nmax, {D}], got {tuple(det_emb.shape)}")
-        Nmax = det_emb.shape[1]
-        det_emb, dbox, dconf = det_emb.contiguous(), dbox.contiguous(), dconf.contiguous()
-        frame_ids = list(frame_ids) if frame_ids is not None else [0] * S
-        res = [FrameResult() for _ in range(S)]
-        lost_after = int(cfg["lost_reid_after"])
-
-        # frames without detections: every track missed, then purge (:467-471)
-        active = [s for s in range(S) if int(N[s]) > 0]
-        for s in range(S):
-            if int(N[s]) == 0:
-                st = self.streams[s]
-                live = st.live_sorted()
-                res[s].unmatched_tracks = st.tid[live].copy()
-                st.miss[live] += 1
-                self._purge(st)
-
-        # predict every live track of the active streams (:474-475)
-        live = {s: self.streams[s].live_sorted() for s in active}
-        self._predict(np.concatenate([self.streams[s].base + live[s] for s in active])
-                      if active else np.zeros(0, np.int32))
-
-        # row split (:478-487): rows sorted by track id
-        main = {s: live[s][self.streams[s].miss[live[s]] <= lost_after] for s in active}
-        reid = {s: live[s][self.streams[s].miss[live[s]] > lost_after] for s in active}
-
-        # ---- stage 1: fused cost + gate + LSAP over all active streams
-        Mrow = max([len(main[s]) for s in active], default=0)
-        unmatched_dets = {s: np.arange(int(N[s]), dtype=np.int64) for s in active}
-        stage1 = {}
-        C1 = None
-        if Mrow > 0:
-            row_slot = np.zeros((S, Mrow), np.int32)
-            Ms = [0] * S
-            Ns = [0] * S
-            for s in active:
-                m = main[s]
-                row_slot[s, :len(m)] = self.streams[s].base + m
-                Ms[s], Ns[s] = len(m), int(N[s])
-            t = self.table
-            C1 = build_cost(M=Ms, N=Ns, bank=t.bank, bank_len=t.bank_len, pbox=t.pbox,
-                            conf_prev=t.last_conf, det_emb=det_emb, dbox=dbox, conf_cur=dconf,
-                            params=self.params, gmean=t.gmean, gsinv=t.gsinv, gate_on=t.gate_on,
-                            row_slot=self._i32(row_slot))["C_total"]
-            lres = lsap_batched(C1, Ms, Ns, cost_max=float(cfg["cost_max"]))
-            if after_launch is not None:
-                after_launch()
-                after_launch = None
-            t_w = time.perf_counter()
-            st_h = lres["status"].cpu().numpy()
-            assign = lres["assign"].cpu().numpy()  # the host sync of mainTracking.py:503
-            self.sync_wait_s += time.perf_counter() - t_w
-            for s in active:
-                if len(main[s]) == 0:
-                    continue
-                if st_h[s] == -1:
-                    raise ValueError("matrix contains invalid numeric entries")
-                if st_h[s] == -2:
-                    raise ValueError("cost matrix is infeasible")
-                a = assign[s, :len(main[s])]
-                rows = np.flatnonzero(a >= 0)
-                stage1[s] = (rows, a[rows].astype(np.int64))
-                taken = np.zeros(int(N[s]), bool)
-                taken[a[rows]] = True
-                unmatched_dets[s] = np.flatnonzero(~taken)
-
-        if after_launch is not None:  # no stage-1 rows this frame
-            after_launch()
-
-        # stage-1 state updates (:520-538)
-        up_slots, up_dets, up_ci = [], [], []
-        for s in active:
-            st = self.streams[s]
-            if s in stage1:
-                rows, cols = stage1[s]
-                sl = main[s][rows]
-                up_slots.append(st.base + sl)
-                up_dets.append(s * Nmax + cols)
-                up_ci.append((s * Mrow + rows) * Nmax + cols)
-                st.miss[sl] = 0
-                st.age[sl] += 1
-                st.last_frame[sl] = frame_ids[s]
-                res[s].matches = np.stack([st.tid[sl], cols], 1)
-                keep = np.ones(len(main[s]), bool)
-                keep[rows] = False
-                res[s].unmatched_tracks = st.tid[main[s][keep]].copy()
-                st.miss[main[s][keep]] += 1
-        if up_slots:
-            self._update(np.concatenate(up_slots), np.concatenate(up_dets), C1, np.concatenate(up_ci),
-                         cfg["cost_update_max"], cfg["maha_thr"], det_emb, dbox, dconf)
-
-        # ---- stage 2: long-lost tracks, ReID-only (:545-599)
-        s2 = [s for s in active if len(reid[s]) > 0 and len(unmatched_dets[s]) > 0]
-        for s in active:
-            if len(reid[s]) > 0 and len(unmatched_dets[s]) == 0:
-                st = self.streams[s]
-                res[s].unmatched_tracks = np.concatenate([res[s].unmatched_tracks, st.tid[reid[s]]])
-                st.miss[reid[s]] += 1
-        if s2:
-            M2 = max(len(reid[s]) for s in s2)
-            N2 = max(len(unmatched_dets[s]) for s in s2)
-            F2 = len(s2)
-            row_slot = np.zeros((F2, M2), np.int32)
-            gidx = np.zeros((F2, N2), np.int64)
-            for q, s in enumerate(s2):
-                row_slot[q, :len(reid[s])] = self.streams[s].base + reid[s]
-                u = np.asarray(unmatched_dets[s], np.int64)
-                gidx[q, :len(u)] = s * Nmax + u
-            g = torch.as_tensor(gidx.reshape(-1)).to(self.device)
-            e2 = det_emb.reshape(-1, D).index_select(0, g).view(F2, N2, D)
-            b2 = dbox.reshape(-1, 4).index_select(0, g).view(F2, N2, 4)
-            c2 = dconf.reshape(-1).index_select(0, g).view(F2, N2)
-            t = self.table
-            Ms2 = [len(reid[s]) for s in s2]
-            Ns2 = [len(unmatched_dets[s]) for s in s2]
-            C2 = build_cost(M=Ms2, N=Ns2, bank=t.bank, bank_len=t.bank_len, pbox=t.pbox,
-                            conf_prev=t.last_conf, det_emb=e2, dbox=b2, conf_cur=c2,
-                            params=self.params_nogate, row_slot=self._i32(row_slot),
-                            want=("C_app",))["C_app"]
-            lres = lsap_batched(C2, Ms2, Ns2, cost_max=float(cfg["reid_only_cost_max"]))
-            assign2 = lres["assign"].cpu().numpy()  # mainTracking.py:559
-            st2 = lres["status"].cpu().numpy()
-            up_slots, up_dets, up_ci = [], [], []
-            for q, s in enumerate(s2):
-                if st2[q] == -1:
-                    raise ValueError("matrix contains invalid numeric entries")
-                st = self.streams[s]
-                a = assign2[q, :len(reid[s])]
-                rows = np.flatnonzero(a >= 0)
-                du = a[rows]
-                u = np.asarray(unmatched_dets[s], np.int64)
-                sl = reid[s][rows]
-                up_slots.append(st.base + sl)
-                up_dets.append(s * Nmax + u[du])
-                up_ci.append((q * M2 + rows) * N2 + du)
-                st.miss[sl] = 0
-                st.age[sl] += 1
-                st.last_frame[sl] = frame_ids[s]
-                res[s].matches = np.concatenate([res[s].matches, np.stack([st.tid[sl], u[du]], 1)])
-                keep = np.ones(len(reid[s]), bool)
-                keep[rows] = False
-                res[s].unmatched_tracks = np.concatenate([res[s].unmatched_tracks, st.tid[reid[s][keep]]])
-                st.miss[reid[s][keep]] += 1
-                left = np.ones(len(u), bool)
-                left[du] = False
-                unmatched_dets[s] = u[left]
-            if up_slots:  # stage-2 gates: cost = C_app <= reid_only_cost_max, no motion gate
-                self._update(np.concatenate(up_slots), np.concatenate(up_dets), C2, np.concatenate(up_ci),
-                             cfg["reid_only_cost_max"], 1e18, det_emb, dbox, dconf)
-
-        # ---- new tracks (:602 -> :362-373), then purge (:605)
-        ini_slots, ini_dets = [], []
-        for s in active:
-            st = self.streams[s]
-            ch = np.asarray(confs_host[s], np.float64)
-            ud = unmatched_dets[s]
-            new = ud[ch[ud] >= float(cfg["init_conf_min"])] if len(ud) else ud
-            if len(new):
-                free = np.flatnonzero(~st.alive)
-                if len(free) < len(new):
-                    raise RuntimeError(f"stream {s}: track capacity {st.cap} exhausted")
-                sl = free[:len(new)]
-                st.alive[sl] = True
-                st.tid[sl] = np.arange(st.next_id, st.next_id + len(new))
-                st.next_id += len(new)
-                st.miss[sl] = 0
-                st.age[sl] = 1
-                st.last_frame[sl] = frame_ids[s]
-                ini_slots.append(st.base + sl)
-                ini_dets.append(s * Nmax + np.asarray(new, np.int64))
-            res[s].unmatched_dets = unmatched_dets[s]
-            self._purge(st)
-        if ini_slots:
-            self._init(np.concatenate(ini_slots), np.concatenate(ini_dets), det_emb, dbox, dconf)
-        return res
-
-    def _purge(self, st: StreamState):
-        dead = st.alive & (st.miss > int(self.cfg["max_age"]))
-        st.alive[dead] = False
-        st.tid[dead] = -1
 
 
 # ---------------------------------------------------------------- views --
@@ -440,7 +488,11 @@ class Tracking:
 
     @property
     def next_id(self) -> int:
-        return self._mst.streams[0].next_id
+        self._mst.drain()
+        return int(self._mst.table.next_id[0].item())
+
+    def _i32(self, a) -> torch.Tensor:
+        return torch.as_tensor(np.ascontiguousarray(a, np.int32)).to(self.device)
 
     # -------------------------------------------------------------- update --
     def _dets(self, det_embs, det_boxes, det_confs):
@@ -476,8 +528,9 @@ class Tracking:
 
     # --------------------------------------------- reference helper methods --
     def _rows(self, row_to_tid: Sequence[int]) -> np.ndarray:
-        st = self._mst.streams[0]
-        lut = {int(t): i for i, t in enumerate(st.tid) if st.alive[i]}
+        live = self._mst.live_slots(0)
+        tids = self._mst.table.tid[torch.as_tensor(live, device=self.device)].cpu().numpy()
+        lut = {int(t): int(g) for t, g in zip(tids, live)}
         try:
             return np.asarray([lut[int(t)] for t in row_to_tid], np.int32)
         except KeyError as k:
@@ -485,8 +538,7 @@ class Tracking:
 
     def predict_all(self):
         """mainTracking.py:340-345 on the device table."""
-        st = self._mst.streams[0]
-        self._mst._predict(st.base + st.live_sorted())
+        self._mst._predict(self._mst.live_slots(0))
 
     def build_C_app_topk(self, *, row_to_tid: List[int], det_embs, device=None, topk: int = 5,
                          use_topk_mean: bool = True, fallback_to_ema: bool = True) -> torch.Tensor:
@@ -500,7 +552,7 @@ class Tracking:
         p.topk = int(topk) if use_topk_mean else 1
         t = self._mst.table
         out = build_cost(M=[M], N=[N], bank=t.bank, bank_len=t.bank_len, pbox=t.pbox, conf_prev=t.last_conf,
-                         det_emb=e, dbox=b, conf_cur=c, params=p, row_slot=self._mst._i32(rows[None]),
+                         det_emb=e, dbox=b, conf_cur=c, params=p, row_slot=self._i32(rows[None]),
                          want=("C_app",))
         return out["C_app"][0]
 
@@ -516,7 +568,7 @@ class Tracking:
         t = self._mst.table
         out = build_cost(M=[M], N=[N], bank=t.bank, bank_len=t.bank_len, pbox=t.pbox, conf_prev=t.last_conf,
                          det_emb=e, dbox=b, conf_cur=c, params=self._mst.params_nogate,
-                         row_slot=self._mst._i32(rows[None]),
+                         row_slot=self._i32(rows[None]),
                          want=("C_total", "C_app", "C_center", "C_scale", "C_conf"))
         o = {k: v[0] for k, v in out.items()}
         o["C_bbox"] = self.alpha * o["C_center"] + self.beta * o["C_scale"]
@@ -544,7 +596,7 @@ class Tracking:
         rows = self._rows(row_to_tid)
         dev = self.device
         t = self._mst.table
-        idx = self._mst._i32(rows).long()
+        idx = self._i32(rows).long()
         p = default_cost_params(dict(w_app=1.0, w_bbox=0.0, w_conf=0.0, maha_thr=maha_thr), gate=True)
         p.inf_cost = float(INF)
         out = cost_combine(torch.from_numpy(np.ascontiguousarray(C_total_np, np.float32)).to(dev),
@@ -561,12 +613,11 @@ class Tracking:
     def tracks(self) -> Dict[int, TrackState]:
         """Snapshot of the live tracks (device -> host copy), keyed by track id
         in creation order, like the reference's self.tracks dict."""
-        st = self._mst.streams[0]
         t = self._mst.table
-        live = st.live_sorted()
+        live = self._mst.live_slots(0)
         if len(live) == 0:
             return {}
-        g = torch.as_tensor(st.base + live).to(self.device)
+        g = torch.as_tensor(live).to(self.device)
         x = t.x.index_select(0, g).cpu().numpy()
         P = t.P.index_select(0, g).cpu().numpy().reshape(-1, 8, 8)
         pb = t.pbox.index_select(0, g).cpu().numpy()
@@ -575,15 +626,19 @@ class Tracking:
         bank = t.bank.index_select(0, g).cpu().numpy()
         bl = t.bank_len.index_select(0, g).cpu().numpy()
         bh = t.bank_head.index_select(0, g).cpu().numpy()
+        tid = t.tid.index_select(0, g).cpu().numpy()
+        age = t.age.index_select(0, g).cpu().numpy()
+        miss = t.miss.index_select(0, g).cpu().numpy()
+        lf = t.last_frame.index_select(0, g).cpu().numpy()
         out = {}
-        for q, sl in enumerate(live):
+        for q in range(len(live)):
             n, h = int(bl[q]), int(bh[q])
             order = [(h - n + k) % self._mst.T for k in range(n)]  # oldest first
             mem = TrackMemory(encoder_feat=enc[q], feat_historical=[bank[q, k] for k in order],
-                              last_conf=float(lc[q]), last_update_frame=int(st.last_frame[sl]),
-                              last_bbox=tuple(float(v) for v in pb[q]), age=int(st.age[sl]),
-                              misss_count=int(st.miss[sl]),
-                              state="ACTIVE" if st.miss[sl] == 0 else "LOST")
-            out[int(st.tid[sl])] = TrackState(int(st.tid[sl]), x[q], P[q], mem, age=int(st.age[sl]),
-                                              miss_count=int(st.miss[sl]), state=mem.state)
+                              last_conf=float(lc[q]), last_update_frame=int(lf[q]),
+                              last_bbox=tuple(float(v) for v in pb[q]), age=int(age[q]),
+                              misss_count=int(miss[q]),
+                              state="ACTIVE" if miss[q] == 0 else "LOST")
+            out[int(tid[q])] = TrackState(int(tid[q]), x[q], P[q], mem, age=int(age[q]),
+                                          miss_count=int(miss[q]), state=mem.state)
         return out

@@ -179,12 +179,15 @@ class Pipeline:
             hook = None
         else:
             hook = lambda: self.embed_async(f + 1)
-        return self.tracker.step(emb, sc["dbox"][f], sc["dconf"][f], [sc["N"]] * sc["streams"],
-                                 sc["confs_host"][f], [f] * sc["streams"], after_launch=hook)
+        # the whole tracker step is enqueued (no host wait inside a frame); its
+        # results reach pinned host memory by one copy and are read in order
+        return self.tracker.step_async(emb, sc["dbox"][f], sc["dconf"][f], [sc["N"]] * sc["streams"],
+                                       [f] * sc["streams"], after_launch=hook)
 
     def check_identity(self, f, res):
         """fraction of detections matched to the track that has followed the
         same object since the track was created"""
+        res = res.result() if hasattr(res, "result") else res
         ok = tot = 0
         for s, r in enumerate(res):
             objs = self.sc["obj"][f, s]
@@ -214,8 +217,9 @@ class LiveProbe:
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
-             "trk_lsap": "lsap_live", "trk_kf_predict": "kf_predict", "trk_track_update": "track_update",
-             "trk_track_init": "track_init"}
+             "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
+             "trk_step_begin": "step_begin", "trk_step_mid": "step_mid", "trk_step_end": "step_end",
+             "trk_step_apply": "step_apply"}
 
     def __init__(self):
         self.on = False
@@ -242,6 +246,7 @@ class LiveProbe:
 
         self._proxy = _Proxy()
         ops.lib = lambda: self._proxy
+        trk.tracking.lib = lambda: self._proxy  # the tracker's step launches
 
     def means_us(self):
         torch.cuda.synchronize()
@@ -305,12 +310,12 @@ def kernel_pass(pipe, f, reps=10):
     # tracker kernels on the current track table (rows = all live tracks)
     t = tr.table
     S_, N = sc["streams"], sc["N"]
-    live = [tr.streams[s].live_sorted() for s in range(S_)]
+    live = [tr.live_slots(s) for s in range(S_)]
     M = max(len(l) for l in live)
     row_slot = np.zeros((S_, M), np.int32)
     for s in range(S_):
-        row_slot[s, :len(live[s])] = tr.streams[s].base + live[s]
-    rs = tr._i32(row_slot)
+        row_slot[s, :len(live[s])] = live[s]
+    rs = torch.as_tensor(row_slot).to(emb.device)
     Ms = [len(l) for l in live]
     cost_out = {"C_total": torch.empty((S_, M, N), device=emb.device)}
     timed("cost", lambda: trk.build_cost(M=Ms, N=[N] * S_, bank=t.bank, bank_len=t.bank_len, pbox=t.pbox,
@@ -361,7 +366,7 @@ def cpu_baseline(sc, sd, budget_s=20.0):
                        f"gate (C, 1 thread) + scipy linear_sum_assignment")
 
 
-def timed_region(step, steps, dist, sync, red_dev):
+def timed_region(step, steps, dist, sync, red_dev, finish=None):
     """Run `steps` steps between a barrier + device sync on both sides; return
     the MAX elapsed time over ranks (one all_reduce) and the step outputs."""
     if dist is not None:
@@ -369,6 +374,8 @@ def timed_region(step, steps, dist, sync, red_dev):
     sync()
     t0 = time.perf_counter()
     out = [step(k) for k in range(steps)]
+    if finish is not None:
+        finish()  # every frame's assignment indices read on the host
     sync()
     el = time.perf_counter() - t0
     if dist is not None:
@@ -436,7 +443,7 @@ def main():
     probe.on = True
     pipe.tracker.sync_wait_s = 0.0
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
-                               torch.cuda.synchronize, dev)
+                               torch.cuda.synchronize, dev, finish=pipe.tracker.drain)
     probe.on = False
     kernel_sum = probe.sum_per_step_us(args.steps)
     live = probe.means_us()
@@ -536,9 +543,10 @@ def main():
         "step_us": round(step_us, 1),
         "kernel_sum_us": round(kernel_sum, 1),
         "overlap": round(kernel_sum / step_us, 3),
-        "host_sync_wait_us": round(pipe.tracker.sync_wait_s / args.steps * 1e6, 1),
+        "host_wait_us": round(pipe.tracker.sync_wait_s / args.steps * 1e6, 1),
         "note": "kernel_sum = device time of every probed launch per step (live HIP events); overlap > 1 "
-                "means streams ran concurrently; host_sync_wait = time the host blocked on the index copy"}
+                "means streams ran concurrently; host_wait = time the host blocked reading frame results "
+                "(back-pressure of the asynchronous tracker: at most 3 frames unread)"}
     line = {
         "metric": "ROIs/sec (roi_align->embed->cost->assign), N=256/frame, 1 GPU",
         "value": round(value, 1), "unit": "ROIs/s", "n_gpus": world, "steps": args.steps,

@@ -264,6 +264,95 @@ int trk_track_init(int64_t n, const int32_t* slots, const int32_t* dets, const f
                    int32_t* bank_head, int64_t T, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Device-resident tracker step (Tracking.update, reference
+ * model/mainTracking.py:450-610, for S streams at once) with NO host
+ * round trip inside a frame: the per-track bookkeeping the reference keeps in
+ * Python dicts (ids, miss counts, ages, the main / ReID-only row split, the
+ * cost_max gate outcome, births with fresh ids, purge) lives in HBM next to
+ * the Kalman state and memory bank, and every decision is made by a kernel.
+ * A frame is this launch sequence on one stream (sizes are read from device
+ * memory, so the host never waits on a frame):
+ *   trk_step_begin   N == 0 frames (:467-471); predict_all (:474-475); row split (:478-487)
+ *   trk_build_cost_dev + trk_lsap_dev     stage 1 (gated C_total, cost_max)  (:493-523)
+ *   trk_step_mid     stage-1 matches / misses (:525-541); unmatched dets; stage-2 inputs (:548-552)
+ *   trk_build_cost_dev + trk_lsap_dev     stage 2 (C_app, reid_only_cost_max) (:555-566)
+ *   trk_step_end     stage-2 matches / misses (:568-595); create_new_tracks (:601, :362-373);
+ *                    purge_dead (:604, :357-360); the frame's results
+ *   trk_step_apply   update_matched's KF update / EMA / bank push (:375-448) for both stages
+ *                    and the new tracks' init (creat_item, init_kf_from_bbox), one wave each
+ * Results per stream s: result[s * trk_step_result_stride(cap, Nmax) + ...] int64:
+ *   [0] n_match [1] n_unmatched_tracks [2] n_unmatched_dets [3] n_live [4] status
+ *   (0 ok, -1 invalid cost entries, -2 infeasible, -3 solver stall, -4 launch bound
+ *   exceeded, -5 track capacity exhausted) [5] next_id [6] stage-1 rows [7] stage-2 rows,
+ *   then match_tid[Nmax], match_det[Nmax], unmatched_tid[cap], unmatched_det[Nmax],
+ *   each in the reference's return order.
+ * Slot g of stream s is s * cap + local slot.  Row bound Mb (host): an upper bound
+ * of every stream's live-track count this frame (<= cap), the row stride of the
+ * stage cost matrices [S][Mb][Nmax] and of the assignment arrays [S][Mb].
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  /* Kalman state and memory (the trk_track_update arrays), [S * cap] slots */
+  double* x; double* P; float* pbox; float* last_conf; double* gmean; double* gsinv;
+  float* enc; float* bank; int32_t* bank_len; int32_t* bank_head;
+  /* bookkeeping, [S * cap] */
+  int32_t* alive; int64_t* tid; int32_t* miss; int32_t* age; int64_t* last_frame;
+  /* per stream: live local slots in ascending track id [S][cap], counts [S] */
+  int32_t* order; int32_t* n_live; int64_t* next_id;
+  /* per-frame scratch */
+  int32_t* ndet;      /* [S] detections this frame                          */
+  int64_t* frame_id;  /* [S]                                                 */
+  int32_t* flags;     /* [S] bit 0: frame without detections, bit 1: failed  */
+  int32_t* m1; int32_t* row1;   /* [S], [S][cap] stage-1 rows (global slots)   */
+  int32_t* m2; int32_t* row2;   /* [S], [S][cap] stage-2 rows                  */
+  int32_t* n2; int32_t* ud;     /* [S], [S][Nmax] unmatched dets after stage 1 */
+  int32_t* freelist;            /* [S][cap]                                    */
+  float* e2; float* b2; float* c2;  /* [S][Nmax][128] / [4] / [1] stage-2 detections */
+  int32_t* ap_n; int32_t* ap_slot; int32_t* ap_det; int32_t* ap_kind; float* ap_cost; /* [S], [S][Nmax] */
+  int32_t* lsap_status;         /* [2][S] status of the two LSAP launches       */
+  int64_t* result;              /* [S][trk_step_result_stride]                 */
+} trk_step_state;
+
+typedef struct {
+  int64_t S, cap, Nmax, T;      /* streams, slots per stream, detection stride, hist_max */
+  int lost_reid_after, max_age; /* conf.yaml tracker section                   */
+  double init_conf_min, conf_update_min, cost_update_max, reid_only_cost_max, maha_thr;
+  float ema_alpha;              /* compared / mixed as the reference's Python floats */
+} trk_step_config;
+
+int64_t trk_step_result_stride(int64_t cap, int64_t Nmax);
+/* host_ndet [S], host_frame_id [S]: this frame's detection counts and ids (HOST
+ * arrays, copied into the launch); Mb: the row bound of this frame. */
+int trk_step_begin(const trk_step_state* st, const trk_step_config* cfg, const int32_t* host_ndet,
+                   const int64_t* host_frame_id, int64_t Mb, void* stream);
+/* C1 [S][Mb][Nmax] gated C_total of stage 1, assign1 [S][Mb] (trk_lsap_dev with
+ * cost_max); det arrays [S][Nmax][...] of the frame. */
+int trk_step_mid(const trk_step_state* st, const trk_step_config* cfg, int64_t Mb, const float* C1,
+                 const int32_t* assign1, const float* det_emb, const float* dbox, const float* dconf,
+                 void* stream);
+/* C2 [S][Mb][Nmax] stage-2 C_app, assign2 [S][Mb]; dconf64 [S][Nmax] f64 (the
+ * detections' confidences as the caller's floats, for the creation / appearance
+ * gates; NULL: dconf widened). */
+int trk_step_end(const trk_step_state* st, const trk_step_config* cfg, int64_t Mb, const float* C2,
+                 const int32_t* assign2, const double* dconf64, const float* dconf, void* stream);
+int trk_step_apply(const trk_step_state* st, const trk_step_config* cfg, const float* det_emb,
+                   const float* dbox, const float* dconf, const double* dconf64, void* stream);
+/* trk_build_cost / trk_lsap with the per-frame sizes read from DEVICE arrays
+ * (dev_M / dev_N, dev_nr / dev_nc); Mmax / nr_bound / nc_bound are host upper
+ * bounds that size the launch (a larger device size is an error: status -4 for
+ * the solver, rows past Mmax are not computed by the cost).  row_slot has row
+ * stride rs_ld. */
+int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* dev_M, const int32_t* dev_N,
+                       const int32_t* row_slot, int64_t rs_ld, int64_t Tmax, const float* bank,
+                       const int32_t* bank_len, const float* pbox, const float* conf_prev, const double* gmean,
+                       const double* gsinv, const int32_t* gate_on, const float* det_emb, const float* dbox,
+                       const float* conf_cur, const trk_cost_params* host_params, float* C_total, float* C_app,
+                       void* stream);
+int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stride, const int32_t* dev_nr,
+                 const int32_t* dev_nc, int64_t nr_bound, int64_t nc_bound, int64_t kmax, int64_t* rows,
+                 int64_t* cols, int32_t* count, int32_t* status, int32_t* assign, int64_t nr_max, double cost_max,
+                 void* stream);
+
+/* ------------------------------------------------------------------------
  * Detector-side boundary.
  *
  * YOLOv7 post-processing as YoloDetects.run_with_tensor applies it

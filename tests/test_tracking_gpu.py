@@ -113,3 +113,106 @@ def test_tracking_argument_errors(trk, gpu):
         t.update({"input_hw": (1, 1), "frame_id": 0, "embs": [np.zeros(64)], "bboxes": [[0, 0, 1, 1]],
                   "confs": [0.9]})
     assert t.update({"input_hw": (1, 1), "frame_id": 0}) == ([], [], [])
+
+
+# ------------------------------------------- device bookkeeping vs host ----
+def _random_scene(rng, n_obj, n_frames, p_vis=0.8, img=1280):
+    """objects with fixed appearance moving at constant velocity; each frame a
+    random subset is detected (with occlusion runs), shuffled, noisy"""
+    app = rng.standard_normal((n_obj, 128)).astype(np.float32)
+    app /= np.linalg.norm(app, axis=1, keepdims=True)
+    w, h = rng.uniform(30, 200, n_obj), rng.uniform(30, 200, n_obj)
+    p = np.stack([rng.uniform(0, img - w), rng.uniform(280, 1000 - h)], 1)
+    v = rng.uniform(-3, 3, (n_obj, 2))
+    hidden = np.zeros(n_obj, np.int64)
+    frames = []
+    for f in range(n_frames):
+        hidden = np.maximum(hidden - 1, 0)
+        start = rng.random(n_obj) < 0.04
+        hidden[start] = rng.integers(1, 14, start.sum())  # occlusion runs (some exceed lost_reid_after)
+        vis = np.flatnonzero((hidden == 0) & (rng.random(n_obj) < p_vis))
+        if f % 9 == 4:
+            vis = vis[:0]  # a frame without detections
+        vis = rng.permutation(vis)
+        q = p[vis] + rng.normal(0, 0.7, (len(vis), 2))
+        boxes = np.concatenate([q, q + np.stack([w[vis], h[vis]], 1)], 1).astype(np.float32)
+        emb = (app[vis] + 0.08 * rng.standard_normal((len(vis), 128))).astype(np.float32)
+        conf = rng.uniform(0.3, 0.99, len(vis))
+        frames.append((emb, boxes, conf))
+        p = p + v
+    return frames
+
+
+def _batch(frames_s, f, gpu):
+    S = len(frames_s)
+    Ns = [len(fr[f][2]) for fr in frames_s]
+    Nmax = max(Ns + [0])
+    E = torch.zeros(S, Nmax, 128); B = torch.zeros(S, Nmax, 4); C = torch.zeros(S, Nmax)
+    confs = []
+    for s, fr in enumerate(frames_s):
+        emb, box, conf = fr[f]
+        n = len(conf)
+        E[s, :n] = torch.from_numpy(emb); B[s, :n] = torch.from_numpy(box)
+        C[s, :n] = torch.from_numpy(conf.astype(np.float32))
+        confs.append(conf.tolist())
+    return E.to(gpu), B.to(gpu), C.to(gpu), Ns, confs
+
+
+def _same(a, b):
+    return (np.array_equal(a.matches.reshape(-1, 2), b.matches.reshape(-1, 2)) and
+            np.array_equal(a.unmatched_tracks, b.unmatched_tracks) and
+            np.array_equal(a.unmatched_dets, b.unmatched_dets))
+
+
+def test_device_step_equals_host_bookkeeping_random(trk, gpu):
+    """Every bookkeeping decision on the device (trk_step_*) == the host numpy
+    bookkeeping over the same kernels, on random scenes with occlusions long
+    enough for the ReID-only stage (lost_reid_after 3), purges (max_age 8),
+    frames without detections, low-confidence detections and a varying Nmax."""
+    import hostref_tracker as H
+    conf = dict(lost_reid_after=3, max_age=8)
+    rng = np.random.default_rng(77)
+    S = 3
+    frames = [_random_scene(rng, n, 40) for n in (12, 30, 5)]
+    dev = trk.MultiStreamTracker(S, conf, capacity=64, device=gpu)
+    host = H.HostBookkeepingTracker(S, conf, capacity=256, device=gpu)
+    stage2 = births = 0
+    for f in range(40):
+        E, B, C, Ns, confs = _batch(frames, f, gpu)
+        rd = dev.step(E, B, C, Ns, confs, [f] * S)
+        rh = host.step(E, B, C, Ns, confs, [f] * S)
+        for s in range(S):
+            assert _same(rd[s], rh[s]), (f, s, rd[s], rh[s])
+            births += len(rd[s].unmatched_dets)
+        stage2 += sum(int((host.streams[s].miss > 3).sum()) for s in range(S))
+    assert stage2 > 0 and births > 0  # the ReID-only stage and births were exercised
+    # the device tables agree with the host's live tracks (ids in ascending order)
+    for s in range(S):
+        live = dev.live_slots(s)
+        tids = dev.table.tid[torch.as_tensor(live, device=gpu)].cpu().numpy()
+        st = host.streams[s]
+        assert np.array_equal(tids, st.tid[st.live_sorted()])
+
+
+def test_track_table_grows_past_capacity(trk, gpu):
+    """More live tracks than the initial 1,024 slots: the table doubles before
+    the frame that would overflow it (the reference's dict has no bound,
+    mainTracking.py:362-373), with results equal to the host bookkeeping."""
+    import hostref_tracker as H
+    rng = np.random.default_rng(5)
+    dev = trk.MultiStreamTracker(1, capacity=1024, device=gpu)
+    host = H.HostBookkeepingTracker(1, capacity=4096, device=gpu)
+    for f in range(2):
+        n = 700
+        # frame 1's boxes are >= 300 px away from frame 0's: every pair is gated, all 700 are born
+        xy = np.stack([rng.uniform(0, 1200, n), rng.uniform(280, 400, n) if f == 0 else rng.uniform(700, 900, n)], 1)
+        boxes = np.concatenate([xy, xy + 40], 1).astype(np.float32)
+        emb = rng.standard_normal((n, 128)).astype(np.float32)
+        conf = rng.uniform(0.6, 0.99, n)
+        E = torch.from_numpy(emb)[None].to(gpu); B = torch.from_numpy(boxes)[None].to(gpu)
+        C = torch.from_numpy(conf.astype(np.float32))[None].to(gpu)
+        rd = dev.step(E, B, C, [n], [conf.tolist()], [f])[0]
+        rh = host.step(E, B, C, [n], [conf.tolist()], [f])[0]
+        assert _same(rd, rh), f
+    assert dev.cap >= 2048
+    assert len(dev.live_slots(0)) == len(host.streams[0].live_sorted()) > 1024
