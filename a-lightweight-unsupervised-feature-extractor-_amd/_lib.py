@@ -119,6 +119,8 @@ def _declare(L):
     L.trk_build_cost_dev.restype = i32
     L.trk_lsap_dev.argtypes = [i64, P, i32, i64, i64, P, P, i64, i64, i64, P, P, P, P, P, i64, f64, P]
     L.trk_lsap_dev.restype = i32
+    L.trk_lsap_set_prof.argtypes = [P]
+    L.trk_lsap_set_prof.restype = i32
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

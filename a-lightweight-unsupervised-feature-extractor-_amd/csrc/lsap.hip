@@ -35,6 +35,8 @@
 
 #include <type_traits>
 
+unsigned long long* g_lsap_prof = nullptr;  // trk_set_tuning("lsap_prof", ...) via trk_lsap_set_prof
+
 namespace {
 
 constexpr int kMaxBatch = 64;
@@ -51,12 +53,22 @@ struct LsapArgs {
   int32_t* assign;
   double cost_max;
   int ring_rows;  // RB (ring capacity in rows) for the largest working nc of the batch
+  unsigned long long* prof;  // trk_set_tuning("lsap_prof"): per-matrix solver cycle breakdown, else null
   const int32_t* dev_nr;  // trk_lsap_dev: shapes in device memory, bounded by nr_bound / nc_bound
   const int32_t* dev_nc;
   int nr_bound, nc_bound;
   int nr[kMaxBatch];
   int nc[kMaxBatch];
 };
+
+// shader-clock stamp (diagnostic builds of the breakdown only: A.prof != null)
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 __device__ __forceinline__ bool key_less(double v1, int k1, double v2, int k2) {
   return v1 < v2 || (v1 == v2 && k1 < k2);
@@ -142,35 +154,127 @@ lsap_kernel(const LsapArgs A) {
   // recently solved rows stay resident for revisits (rows on augmenting paths)
   const int LA = whole ? RB : max(1, min(16, RB / 2));
 
-  // LDS: u[nr] f64 | col4row[nr] i32 | ready[RB] i32 | ctl[4] i32 | ring[RB][nc] T
+  // LDS: u[nr] f64 | col4row[nr] i32 | ready[RB] i32 | ctl[8] i32 | ring[RB][nc] T
   double* u = reinterpret_cast<double*>(smem);
   int* col4row = reinterpret_cast<int*>(u + nr);
   int* ready = col4row + nr;     // ready[s] = q + 1 when ring slot s holds row q
-  int* ctl = ready + RB;         // ctl[0] = rows finished by the solver, ctl[1] = invalid entry seen
+  int* ctl = ready + RB;         // [0] rows finished by the solver, [1] invalid entry seen,
+                                 // [2] solver status, [3] shortcut prefix, [4] loader stall
   // offset arithmetic on the LDS base (an integer round trip would turn every
   // ring access into a flat load)
-  const size_t ring_off = ((size_t)(12 * nr + 4 * RB + 16) + 15) & ~size_t(15);
+  const size_t ring_off = ((size_t)(12 * nr + 4 * RB + 32) + 15) & ~size_t(15);
   T* ring = reinterpret_cast<T*>(smem + ring_off);
 
   for (int q = threadIdx.x; q < RB; q += blockDim.x) ready[q] = 0;
-  for (int r = threadIdx.x; r < nr; r += blockDim.x) { u[r] = 0.0; col4row[r] = -1; }
-  if (threadIdx.x < 4) ctl[threadIdx.x] = 0;
-  __syncthreads();
+  if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 
   auto gload = [&](int i, int j) -> T {  // working-matrix element from global
     return tr ? C[(int64_t)j * ld + i] : C[(int64_t)i * ld + j];
   };
 
+  // ---- exact shortcut for the leading rows.  Row cur of the SAP starts with
+  // u[cur] = 0 and, as long as every earlier row was solved by its first scan,
+  // v = 0: its first scan sees spc[j] = ((0 + C[cur][j]) - 0) - 0 over all
+  // columns.  If that minimum is unique and finite and its column is not the
+  // minimum of an earlier row (so still unassigned), the row ends right there:
+  // col4row[cur] = that column, u[cur] = 0 + minimum, v unchanged.  So the
+  // longest prefix of rows with a unique finite minimum in a column no earlier
+  // row's minimum took is solved in one parallel pass with exactly the state
+  // the sequential algorithm reaches; the solver continues after it.
+  const int ks = (nc + 63) >> 6;  // column slots in use (KS is the launch's bound)
+  int* firstrow = reinterpret_cast<int*>(ring);  // [nc]: the ring is idle until the loaders start
+  for (int j = threadIdx.x; j < nc; j += blockDim.x) firstrow[j] = 0x7fffffff;
+  if (threadIdx.x == 0) ctl[3] = nr;
+  __syncthreads();
+  {
+    constexpr int R = KS >= 16 ? 1 : (KS >= 8 ? 2 : (KS >= 4 ? 4 : 8));  // rows in flight per wave
+    int bad = 0;
+    for (int i0 = wave * R; i0 < nr; i0 += 4 * R) {
+      T x[R][KS];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const int c = lane + 64 * k;
+          x[r][k] = (i0 + r < nr && k < ks && c < nc) ? gload(i0 + r, c) : (T)INFINITY;
+        }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int i = i0 + r;
+        if (i < nr) {
+          double best = INFINITY;
+          int bcol = 0x7fffffff, cnt = 0;
+#pragma unroll
+          for (int k = 0; k < KS; ++k) {
+            const int c = lane + 64 * k;
+            const T e = x[r][k];
+            if (k < ks && c < nc) {
+              if (e != e || e == (T)-INFINITY) bad = 1;
+              const double d = (double)e;
+              if (d < best) { best = d; bcol = c; cnt = 1; }
+              else if (d == best) ++cnt;
+            }
+          }
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const double ob = __shfl_xor(best, o);
+            const int oc = __shfl_xor(bcol, o), on = __shfl_xor(cnt, o);
+            if (ob < best) { best = ob; bcol = oc; cnt = on; }
+            else if (ob == best) { cnt += on; bcol = min(bcol, oc); }
+          }
+          if (lane == 0) {
+            const bool uniq = cnt == 1 && best < INFINITY;
+            u[i] = best;
+            col4row[i] = uniq ? bcol : -1;
+            if (uniq) atomicMin(&firstrow[bcol], i);
+            else atomicMin(&ctl[3], i);
+          }
+        }
+      }
+    }
+    if (__any(bad) && lane == 0) ctl[1] = 1;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+    const int c = col4row[i];
+    if (c >= 0 && firstrow[c] != i) atomicMin(&ctl[3], i);  // an earlier row's minimum took c
+  }
+  __syncthreads();
+  const int kpre = ctl[1] ? nr : ctl[3];  // invalid entries: the result is the error, solve nothing
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+    if (i < kpre) {
+      const double spc0 = ((0.0 + u[i]) - 0.0) - 0.0;  // the first scan's spc, exactly
+      u[i] = 0.0 + spc0;                              // u[cur] += minVal
+    } else {
+      u[i] = 0.0;
+      col4row[i] = -1;
+    }
+  }
+  int r4c_pre[KS];  // the solver's row4col for the prefix's columns
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int j = lane + 64 * k;
+    const int fr = (k < ks && j < nc) ? firstrow[j] : 0x7fffffff;
+    r4c_pre[k] = fr < kpre ? fr : -1;
+  }
+  if (threadIdx.x == 0) ctl[0] = kpre;
+  __syncthreads();  // firstrow read: the ring is the loaders' from here
+
   if (wave > 0) {
     // ------------------------------------------------------------ loaders
     int bad = 0;
-    for (int q = wave - 1; q < nr; q += kLoaders) {
+    for (int q = kpre + wave - 1; q < nr; q += kLoaders) {
       // at most LA rows ahead of the solver (ctl[0] = rows it has finished);
       // this also keeps slot q % RB free (row q - RB is long finished)
       uint32_t spins = 0;
+      bool stalled = false;
       while (q >= ld_relaxed(&ctl[0]) + LA) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > kSpinLimit) break;
+        if (++spins > kSpinLimit) { stalled = true; break; }
+      }
+      if (stalled) {  // never overwrite a slot the solver may still read: report and stop
+        if (lane == 0) ctl[4] = 1;
+        break;
       }
       T* dst = ring + (int64_t)(q % RB) * nc;
       constexpr int U = 8;  // loads in flight per lane
@@ -199,16 +303,18 @@ lsap_kernel(const LsapArgs A) {
     double v[KS], spc[KS];
     int path[KS], r4c[KS], pos[KS];
     bool exists[KS], alive[KS];
-    const int ks = (nc + 63) >> 6;  // column slots in use (KS is the launch's bound)
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       exists[k] = lane + 64 * k < nc;
       v[k] = 0.0;
       path[k] = -1;
-      r4c[k] = -1;
+      r4c[k] = r4c_pre[k];
     }
     int status = 0;
-    for (int cur = 0; cur < nr; ++cur) {
+    const bool prof = A.prof != nullptr;
+    unsigned long long p_wait = 0, p_scan = 0, p_dual = 0, p_aug = 0, p_iter = 0, p_t0 = 0, p_t = 0;
+    if (prof) p_t0 = p_t = stamp();
+    for (int cur = kpre; cur < nr; ++cur) {
       {  // wait for row cur
         uint32_t spins = 0;
         while (ld_acquire(&ready[cur % RB]) != cur + 1) {
@@ -217,7 +323,8 @@ lsap_kernel(const LsapArgs A) {
         }
         if (status) break;
       }
-      if (ld_relaxed(&ctl[1])) { status = -1; break; }  // invalid entry: result is the error
+      if (ld_relaxed(&ctl[1])) { status = -1; break; }  // invalid entry (a loader's check): stop early
+      if (prof) { const unsigned long long t = stamp(); p_wait += t - p_t; p_t = t; }
 #pragma unroll
       for (int k = 0; k < KS; ++k) {
         spc[k] = INFINITY;
@@ -235,7 +342,7 @@ lsap_kernel(const LsapArgs A) {
         T cv[KS];
         // row i < cur is still resident unless a loader may be overwriting it:
         // loaders write rows <= cur + LA - 1, evicting rows <= cur + LA - 1 - RB
-        if (i == cur || whole || i >= cur + LA - RB) {
+        if (i == cur || (i >= kpre && (whole || i >= cur + LA - RB))) {  // prefix rows never enter the ring
           const int slot = whole ? i : i % RB;
           const T* lrow = ring + (int64_t)slot * nc;
 #pragma unroll
@@ -277,8 +384,10 @@ lsap_kernel(const LsapArgs A) {
           alive[k] = alive[k] && !me;
         }
         --nrem;
+        if (prof) ++p_iter;
       }
       if (status) break;
+      if (prof) { const unsigned long long t = stamp(); p_scan += t - p_t; p_t = t; }
       // dual update (scipy order: u[cur], the other visited rows, the columns)
       if (lane == 0) u[cur] += minVal;
       wave_sync();
@@ -290,6 +399,7 @@ lsap_kernel(const LsapArgs A) {
         v[k] -= d;
       }
       wave_sync();
+      if (prof) { const unsigned long long t = stamp(); p_dual += t - p_t; p_t = t; }
       // augment along path (serial; one owner lane per step)
       int j = sink;
       for (;;) {
@@ -308,6 +418,12 @@ lsap_kernel(const LsapArgs A) {
         if (r == cur) break;
       }
       if (lane == 0) st_release(&ctl[0], cur + 1);  // slot cur % RB may be refilled
+      if (prof) { const unsigned long long t = stamp(); p_aug += t - p_t; p_t = t; }
+    }
+    if (prof && lane == 0) {
+      unsigned long long* o = A.prof + (int64_t)f * 8;
+      o[0] = p_wait; o[1] = p_scan; o[2] = p_dual; o[3] = p_aug; o[4] = p_iter;
+      o[5] = p_t - p_t0; o[6] = (unsigned long long)nr; o[7] = (unsigned long long)nc;
     }
     if (lane == 0) {
       ctl[2] = status;
@@ -323,11 +439,12 @@ lsap_kernel(const LsapArgs A) {
   }
   __syncthreads();
   int status = ctl[2];
+  if (ctl[4]) status = -3;  // a loader stalled: not a property of the matrix
   if (ctl[1]) status = -1;  // an invalid entry anywhere -> scipy raises (checked first)
   if (status) {
     if (assign)
       for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
-    if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = status == -3 ? -2 : status; }
+    if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = status; }
     return;
   }
   if (!tr) {
@@ -438,6 +555,7 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
+    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 8 : nullptr;
     int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                              : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
@@ -491,9 +609,17 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
+    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 8 : nullptr;
     int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                              : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
   }
+  return TRK_OK;
+}
+
+/* diagnostics: per-matrix solver cycle breakdown of later trk_lsap / trk_lsap_dev launches
+ * into buf [F][8] u64 (wait, scan, dual, augment, iterations, total, nr, nc); NULL = off */
+extern "C" int trk_lsap_set_prof(unsigned long long* buf) {
+  g_lsap_prof = buf;
   return TRK_OK;
 }

@@ -11,7 +11,7 @@ from typing import List, Tuple
 import numpy as np
 import torch
 
-from .ops import _device, lsap_batched
+from .ops import _device, lsap_batched, lsap_check_status
 
 
 def hungarian_assign(C_total, cost_max: float = 1e9
@@ -38,11 +38,7 @@ def hungarian_assign(C_total, cost_max: float = 1e9
     if not t.is_cuda:
         t = t.to(_device())
     res = lsap_batched(t.reshape(1, M, N), [M], [N], cost_max=float(cost_max))
-    status = int(res["status"][0].item())
-    if status == -1:
-        raise ValueError("matrix contains invalid numeric entries")
-    if status == -2:
-        raise ValueError("cost matrix is infeasible")
+    lsap_check_status(int(res["status"][0].item()), "hungarian_assign")
     assign = res["assign"][0, :M].cpu().numpy()
     matches = [(i, int(assign[i])) for i in range(M) if assign[i] >= 0]
     matched_dets = {j for _, j in matches}

@@ -410,6 +410,20 @@ def lsap_batched(C: torch.Tensor, nr: Sequence[int], nc: Sequence[int], *,
     return out
 
 
+def lsap_check_status(status: int, what: str = "lsap"):
+    """Raise like scipy for a trk_lsap status (-1 invalid entries, -2 infeasible);
+    -3 (internal solver stall) and -4 (launch bound) are library errors."""
+    if status == 0:
+        return
+    if status == -1:
+        raise ValueError("matrix contains invalid numeric entries")
+    if status == -2:
+        raise ValueError("cost matrix is infeasible")
+    if status == -3:
+        raise _lib.TrkError(f"{what}: the solver stalled (a bounded wait expired); the result is not valid")
+    raise _lib.TrkError(f"{what}: failed with status {status}")
+
+
 def _device():
     if not torch.cuda.is_available():
         raise RuntimeError("linear_sum_assignment: no ROCm device (this package has no CPU fallback)")
@@ -440,9 +454,6 @@ def linear_sum_assignment(cost_matrix, maximize: bool = False):
     t = t.to(_device(), non_blocking=False)
     res = lsap_batched(t.reshape(1, nr, nc), [nr], [nc])
     status = int(res["status"][0].item())
-    if status == -1:
-        raise ValueError("matrix contains invalid numeric entries")
-    if status == -2:
-        raise ValueError("cost matrix is infeasible")
+    lsap_check_status(status)
     k = int(res["count"][0].item())
     return res["rows"][0, :k].cpu().numpy(), res["cols"][0, :k].cpu().numpy()

@@ -345,6 +345,7 @@ class MultiStreamTracker:
         if len(self._pending) >= self.max_inflight:
             self._consume_through(self._pending[0])
         Mb = int(min(self.cap, max(1, self._live_ub().max())))
+        self.last_Mb = Mb  # row stride of this frame's stage cost matrices (tools, tests)
         if Mb > TRK_LSAP_MAX_DIM:
             raise NotImplementedError(f"more than {TRK_LSAP_MAX_DIM} live tracks in one stream")
         fid = np.asarray(list(frame_ids) if frame_ids is not None else [0] * S, np.int64)

@@ -102,7 +102,7 @@ class Pipeline:
         # consecutive frames' embeddings alternate between two side streams, so the
         # low-occupancy tail of frame f's encoder (SE / head: 128 workgroups) runs
         # beside frame f+1's ROI Align and first GEMM instead of before them
-        n_side = int(os.environ.get("TRK_EMBED_STREAMS", "2"))
+        n_side = int(os.environ.get("TRK_EMBED_STREAMS", "1"))
         self.sides = [torch.cuda.Stream(device=sc["feat"].device) for _ in range(n_side)]
         self.side = self.sides[0]
         self.pending = {}  # frame -> (embeddings, ready event)
@@ -113,6 +113,10 @@ class Pipeline:
         # serialising between consecutive encoder runs
         self.prefetch_early = os.environ.get("TRK_PREFETCH_EARLY", "1") == "1"
         self.depth = int(os.environ.get("TRK_PREFETCH_DEPTH", "1"))  # frames embedded ahead
+        # the tracker's launches (mostly few-workgroup kernels) on a high-priority stream so
+        # they dispatch as soon as CUs free up beside the encoder's full-GPU grids
+        prio = int(os.environ.get("TRK_TRACK_PRIO", "0"))
+        self.track_stream = torch.cuda.Stream(device=sc["feat"].device, priority=-1) if prio else None
 
     def capture(self):
         """Capture roi_align + encoder as two hipGraphs (static ROI / embedding
@@ -152,10 +156,11 @@ class Pipeline:
             return
         main = torch.cuda.current_stream()
         side = self.sides[f % len(self.sides)]
-        if len(self.sides) == 1 or self.graphs is not None:
+        if self.graphs is not None:
             side.wait_stream(main)  # graph replays reuse per-parity buffers main may still read
-        # (with two side streams no wait on main: an embedding reads only the frame's
-        # static map / boxes and writes buffers of its own; main waits on `ev`)
+        # (eager: no wait on main -- an embedding reads only the frame's static map / boxes
+        # and writes buffers of its own (kept alive for main by record_stream); main waits on
+        # `ev`.  So the encoder runs back to back on its stream while the tracker overlaps it)
         with torch.cuda.stream(side):
             if self.graphs is not None:
                 g, rois, emb = self.graphs[f & 1]
@@ -169,6 +174,12 @@ class Pipeline:
         self.pending[f] = (emb, ev)
 
     def step(self, f):
+        if self.track_stream is not None:
+            with torch.cuda.stream(self.track_stream):
+                return self._step(f)
+        return self._step(f)
+
+    def _step(self, f):
         sc = self.sc
         self.embed_async(f)
         emb, ev = self.pending.pop(f)

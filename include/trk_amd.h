@@ -134,7 +134,8 @@ int trk_cost_combine(int64_t M, int64_t N, const float* C_app, const float* pbox
  *           stride ld >= nc[f]; matrix f starts at C + f*batch_stride elements.
  *   rows,cols [f][kmax] int64 (kmax >= min(nr,nc)); count [f] int32 = min(nr,nc)
  *   status  [f] int32: 0 ok, -1 invalid numeric entries (NaN / -inf),
- *           -2 infeasible
+ *           -2 infeasible, -3 internal stall (a bounded wait expired: not a
+ *           property of the matrix), -4 (trk_lsap_dev) shape above the launch bound
  *   If assign != NULL: assign[f][nr_max] int32 = column of row i if matched and
  *           C[i,col] <= cost_max, else -1 (hung.py:35-40's cost gate).
  *   nr, nc are HOST arrays (shapes are decided on the host).
@@ -145,6 +146,11 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
              const int32_t* host_nr, const int32_t* host_nc, int64_t kmax,
              int64_t* rows, int64_t* cols, int32_t* count, int32_t* status,
              int32_t* assign, int64_t nr_max, double cost_max, void* stream);
+
+/* Diagnostics: later trk_lsap / trk_lsap_dev launches write a per-matrix solver
+ * cycle breakdown into buf [F][8] u64 (shader clocks: waiting for rows, scans +
+ * argmin, dual updates, augmentation; iterations, total, nr, nc).  NULL = off. */
+int trk_lsap_set_prof(unsigned long long* buf);
 
 /* ------------------------------------------------------------------------
  * Encoder helpers (the non-GEMM parts of encoderAndHead.Model's eval graph,

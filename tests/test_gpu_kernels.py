@@ -578,3 +578,43 @@ def test_act_mean_and_scale_rows(trk, gpu, act):
     ops.scale_rows(blk, s, act=None)
     assert torch.equal(blk, y) and torch.equal(wide[:, :, :256], w0[:, :, :256])
     assert torch.equal(wide[:, :, 768:], w0[:, :, 768:])
+
+
+def test_lsap_prefix_shortcut_vs_oracle(trk, oracle, gpu):
+    """The solver's exact shortcut (leading rows with a unique finite minimum in a
+    column no earlier row's minimum took) against the oracle on matrices where
+    the prefix is whole, cut by a duplicated minimum, by a tied row, by an
+    all-gated row, on a tall (transposed) problem and in f64."""
+    rng = np.random.default_rng(31)
+
+    def perm_like(nr, nc, lo=0.05, hi=5.0):
+        C = rng.uniform(1.0, hi, (nr, nc)).astype(np.float32)
+        cols = rng.permutation(nc)[:nr]
+        C[np.arange(nr), cols] = rng.uniform(0.0, lo, nr).astype(np.float32)
+        return C, cols
+
+    cases = []
+    C, _ = perm_like(256, 256); cases.append(C)                        # whole prefix
+    C, cols = perm_like(256, 256); C[100, cols[40]] = 0.0; cases.append(C)   # row 100 wants row 40's column
+    C, cols = perm_like(256, 256); C[50, :] = 2.0; cases.append(C)           # tied row
+    C, _ = perm_like(200, 256); C[7, :] = np.float32(1e9); cases.append(C)   # gated row early
+    C, _ = perm_like(256, 300); C[255, :] = np.float32(1e9); cases.append(C)  # gated last row
+    C, _ = perm_like(256, 180); cases.append(C.T.copy())                      # tall: transposed problem
+    C = rng.integers(0, 4, (128, 128)).astype(np.float32); cases.append(C)    # tie-heavy: prefix of ~0
+    for C in cases:
+        for dt in (np.float32, np.float64):
+            r, c = trk.linear_sum_assignment(C.astype(dt))
+            er, ec = oracle.lsap(C)
+            assert np.array_equal(r, er) and np.array_equal(c, ec), (C.shape, dt)
+    # batched: frames with different prefixes in one launch
+    F = len(cases[:5])
+    buf = np.zeros((F, 256, 300), np.float32)
+    for k, C in enumerate(cases[:5]):
+        buf[k, :C.shape[0], :C.shape[1]] = C
+    res = trk.lsap_batched(torch.from_numpy(buf).to(gpu), [C.shape[0] for C in cases[:5]],
+                           [C.shape[1] for C in cases[:5]])
+    for k, C in enumerate(cases[:5]):
+        er, ec = oracle.lsap(C)
+        n = int(res["count"][k])
+        assert np.array_equal(res["rows"][k, :n].cpu().numpy(), er)
+        assert np.array_equal(res["cols"][k, :n].cpu().numpy(), ec)

@@ -20,3 +20,29 @@ def test_tracker_conf_from_yaml(trk, tmp_path):
     import pytest
     with pytest.raises(KeyError, match="tracker"):
         trk.tracker_conf(conf_path=str(bad))
+
+
+def test_lsap_status_mapping():
+    """LSAP statuses: -1 / -2 raise ValueError like scipy; -3 (an internal solver
+    stall) and the tracker step's launch-bound / capacity statuses are library
+    errors, never reported as an infeasible matrix."""
+    import pytest
+    from conftest import pkg
+    trk = pkg()
+    ops = __import__(trk.__name__ + ".ops", fromlist=["x"])
+    tracking = __import__(trk.__name__ + ".tracking", fromlist=["x"])
+    ops.lsap_check_status(0)
+    with pytest.raises(ValueError, match="invalid numeric"):
+        ops.lsap_check_status(-1)
+    with pytest.raises(ValueError, match="infeasible"):
+        ops.lsap_check_status(-2)
+    with pytest.raises(trk.TrkError, match="stalled"):
+        ops.lsap_check_status(-3)
+    with pytest.raises(tracking.SolverStallError):
+        tracking._raise_status(-3, 0)
+    for st in (-4, -5):
+        with pytest.raises(trk.TrkError) as ei:
+            tracking._raise_status(st, 2)
+        assert not isinstance(ei.value, ValueError)
+    with pytest.raises(ValueError, match="infeasible"):
+        tracking._raise_status(-2, 0)
