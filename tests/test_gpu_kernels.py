@@ -599,7 +599,7 @@ def test_lsap_prefix_shortcut_vs_oracle(trk, oracle, gpu):
     C, cols = perm_like(256, 256); C[50, :] = 2.0; cases.append(C)           # tied row
     C, _ = perm_like(200, 256); C[7, :] = np.float32(1e9); cases.append(C)   # gated row early
     C, _ = perm_like(256, 300); C[255, :] = np.float32(1e9); cases.append(C)  # gated last row
-    C, _ = perm_like(256, 180); cases.append(C.T.copy())                      # tall: transposed problem
+    C, _ = perm_like(180, 256); cases.append(C.T.copy())                      # tall: transposed problem
     C = rng.integers(0, 4, (128, 128)).astype(np.float32); cases.append(C)    # tie-heavy: prefix of ~0
     for C in cases:
         for dt in (np.float32, np.float64):
