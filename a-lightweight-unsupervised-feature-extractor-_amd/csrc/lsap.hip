@@ -99,6 +99,27 @@ __device__ __forceinline__ void argmin_step(double& v, int& key, int& col) {
   col = take ? oc : col;
 }
 
+// min over the wave of a double (DPP row shifts + row broadcasts; +inf identity),
+// returned wave-uniform
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_min_step(double v) {
+  const int olo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWMASK, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(0x7ff00000, __double2hiint(v), CTRL, ROWMASK, 0xF, false);
+  const double o = __hiloint2double(ohi, olo);
+  return o < v ? o : v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+  v = dpp_min_step<0x111, 0xF>(v);
+  v = dpp_min_step<0x112, 0xF>(v);
+  v = dpp_min_step<0x114, 0xF>(v);
+  v = dpp_min_step<0x118, 0xF>(v);
+  v = dpp_min_step<0x142, 0xA>(v);
+  v = dpp_min_step<0x143, 0xC>(v);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
+}
+
 // lexicographic min over the wave; the result is returned wave-uniform
 // (row_shr 1/2/4/8 inside each row of 16, then row_bcast15 / row_bcast31,
 // total in lane 63).  (value, key) pairs are unique per column, so the order
@@ -187,7 +208,7 @@ lsap_kernel(const LsapArgs A) {
   if (threadIdx.x == 0) ctl[3] = nr;
   __syncthreads();
   {
-    constexpr int R = KS >= 16 ? 1 : (KS >= 8 ? 2 : (KS >= 4 ? 4 : 8));  // rows in flight per wave
+    constexpr int R = KS >= 16 ? 2 : (KS >= 8 ? 4 : 8);  // rows in flight per wave
     int bad = 0;
     for (int i0 = wave * R; i0 < nr; i0 += 4 * R) {
       T x[R][KS];
@@ -202,31 +223,32 @@ lsap_kernel(const LsapArgs A) {
       for (int r = 0; r < R; ++r) {
         const int i = i0 + r;
         if (i < nr) {
-          double best = INFINITY;
-          int bcol = 0x7fffffff, cnt = 0;
+          double lm = INFINITY;  // this lane's minimum (invalid slots hold +inf)
 #pragma unroll
           for (int k = 0; k < KS; ++k) {
-            const int c = lane + 64 * k;
             const T e = x[r][k];
-            if (k < ks && c < nc) {
-              if (e != e || e == (T)-INFINITY) bad = 1;
-              const double d = (double)e;
-              if (d < best) { best = d; bcol = c; cnt = 1; }
-              else if (d == best) ++cnt;
-            }
+            if (e != e || e == (T)-INFINITY) bad = 1;
+            const double d = (double)e;
+            lm = d < lm ? d : lm;
           }
+          const double m = wave_min(lm);
+          // entries equal to the minimum: unique iff one lane holds exactly one
+          int cnt = 0, col = 0;
 #pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const double ob = __shfl_xor(best, o);
-            const int oc = __shfl_xor(bcol, o), on = __shfl_xor(cnt, o);
-            if (ob < best) { best = ob; bcol = oc; cnt = on; }
-            else if (ob == best) { cnt += on; bcol = min(bcol, oc); }
+          for (int k = 0; k < KS; ++k) {
+            const bool eq = (double)x[r][k] == m;
+            col = (eq && cnt == 0) ? lane + 64 * k : col;
+            cnt += eq ? 1 : 0;
           }
+          const uint64_t holders = __ballot(cnt > 0);
+          const int hl = (int)__builtin_ctzll(holders | (1ull << 63));
+          const int hcnt = __builtin_amdgcn_readlane(cnt, hl);
+          const int hcol = __builtin_amdgcn_readlane(col, hl);
+          const bool uniq = m < INFINITY && __popcll(holders) == 1 && hcnt == 1;
           if (lane == 0) {
-            const bool uniq = cnt == 1 && best < INFINITY;
-            u[i] = best;
-            col4row[i] = uniq ? bcol : -1;
-            if (uniq) atomicMin(&firstrow[bcol], i);
+            u[i] = m;
+            col4row[i] = uniq ? hcol : -1;
+            if (uniq) atomicMin(&firstrow[hcol], i);
             else atomicMin(&ctl[3], i);
           }
         }

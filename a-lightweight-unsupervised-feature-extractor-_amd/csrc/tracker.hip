@@ -147,55 +147,69 @@ struct UpdArgs {
 };
 
 // update_matched for one (slot s, detection d) pair, one wavefront (all 64
-// lanes active): lane 0 runs the 8-D filter, the wave does the 128-D
-// appearance update (2 dims per lane).  conf: the detection's confidence as
-// the caller's float (the appearance gate compares it in double, :416);
-// has_cost / costv: the matched cost entry (gate :418).
+// lanes active; the workgroup is that one wave): the 8-D filter runs with one
+// lane per element of the 8x8 products (LDS-shared operands, each element
+// accumulated in the serial order, so the results equal a one-lane filter bit
+// for bit), then the wave does the 128-D appearance update (2 dims per lane).
+// conf: the detection's confidence as the caller's float (the appearance gate
+// compares it in double, :416); has_cost / costv: the matched cost entry (:418).
 __device__ void track_update_wave(const UpdArgs& A, int64_t s, int64_t d, double conf, bool has_cost,
                                   float costv, double conf_update_min, double cost_update_max,
                                   double maha_thr) {
+  __shared__ double sP[64], sK[32], sIKH[64], sT1[64], sX[8];
   const int lane = threadIdx.x & 63;
+  const int r = lane >> 3, c = lane & 7;
+  double* x = A.X + s * 8;
+  double* P = A.P + s * 64;
+  sP[lane] = P[lane];
+  if (lane < 8) sX[lane] = x[lane];
+  double z[4];
+  box_to_z(A.dbox + d * 4, z);
+  __syncthreads();
+  // filterpy KalmanFilter.update (R = I, H = [I4 | 0]): y, S = H P H^T + R, S^-1 (every lane)
+  double y[4], S[16], SI[16];
+  for (int q = 0; q < 4; ++q) y[q] = z[q] - sX[q];
+  for (int q = 0; q < 4; ++q)
+    for (int k = 0; k < 4; ++k) S[q * 4 + k] = sP[q * 8 + k] + (q == k ? 1.0 : 0.0);
+  inv4(S, SI);
+  if (lane < 32) {  // K = P H^T S^-1, element (lane / 4, lane % 4)
+    const int kr = lane >> 2, kc = lane & 3;
+    double v = 0.0;
+    for (int k = 0; k < 4; ++k) v += sP[kr * 8 + k] * SI[k * 4 + kc];
+    sK[lane] = v;
+  }
+  __syncthreads();
+  double xn = 0.0;
+  if (lane < 8) {  // x = x + K y
+    double v = 0.0;
+    for (int k = 0; k < 4; ++k) v += sK[lane * 4 + k] * y[k];
+    xn = sX[lane] + v;
+    x[lane] = xn;
+  }
+  // P = (I - K H) P (I - K H)^T + K R K^T, element (r, c) per lane
+  sIKH[lane] = (r == c ? 1.0 : 0.0) - (c < 4 ? sK[r * 4 + c] : 0.0);
+  __syncthreads();
+  {
+    double v = 0.0;
+    for (int k = 0; k < 8; ++k) v += sIKH[r * 8 + k] * sP[k * 8 + c];
+    sT1[lane] = v;
+  }
+  __syncthreads();
+  double pn;
+  {
+    double v = 0.0;
+    for (int k = 0; k < 8; ++k) v += sT1[r * 8 + k] * sIKH[c * 8 + k];
+    double kk = 0.0;
+    for (int k = 0; k < 4; ++k) kk += sK[r * 4 + k] * sK[c * 4 + k];
+    pn = v + kk;
+  }
+  P[lane] = pn;
+  __syncthreads();  // every read of the old P is done
+  sP[lane] = pn;
+  if (lane < 8) sX[lane] = xn;
+  __syncthreads();
   int push = 0;
   if (lane == 0) {
-    double* x = A.X + s * 8;
-    double* P = A.P + s * 64;
-    double z[4];
-    box_to_z(A.dbox + d * 4, z);
-    // filterpy KalmanFilter.update (R = I, H = [I4 | 0]):
-    double y[4], S[16], SI[16], K[32];
-    for (int r = 0; r < 4; ++r) y[r] = z[r] - x[r];
-    for (int r = 0; r < 4; ++r)
-      for (int c = 0; c < 4; ++c) S[r * 4 + c] = P[r * 8 + c] + (r == c ? 1.0 : 0.0);
-    inv4(S, SI);
-    for (int r = 0; r < 8; ++r)  // K = P H^T S^-1
-      for (int c = 0; c < 4; ++c) {
-        double v = 0.0;
-        for (int k = 0; k < 4; ++k) v += P[r * 8 + k] * SI[k * 4 + c];
-        K[r * 4 + c] = v;
-      }
-    for (int r = 0; r < 8; ++r) {
-      double v = 0.0;
-      for (int k = 0; k < 4; ++k) v += K[r * 4 + k] * y[k];
-      x[r] = x[r] + v;
-    }
-    // P = (I - K H) P (I - K H)^T + K R K^T
-    double IKH[64], T1[64];
-    for (int r = 0; r < 8; ++r)
-      for (int c = 0; c < 8; ++c) IKH[r * 8 + c] = (r == c ? 1.0 : 0.0) - (c < 4 ? K[r * 4 + c] : 0.0);
-    for (int r = 0; r < 8; ++r)
-      for (int c = 0; c < 8; ++c) {
-        double v = 0.0;
-        for (int k = 0; k < 8; ++k) v += IKH[r * 8 + k] * P[k * 8 + c];
-        T1[r * 8 + c] = v;
-      }
-    for (int r = 0; r < 8; ++r)
-      for (int c = 0; c < 8; ++c) {
-        double v = 0.0;
-        for (int k = 0; k < 8; ++k) v += T1[r * 8 + k] * IKH[c * 8 + k];
-        double kk = 0.0;
-        for (int k = 0; k < 4; ++k) kk += K[r * 4 + k] * K[c * 4 + k];
-        P[r * 8 + c] = v + kk;
-      }
     // last_* fields (update_matched :402-405)
     const float* b = A.dbox + d * 4;
     float* pb = A.pbox + s * 4;
@@ -207,7 +221,7 @@ __device__ void track_update_wave(const UpdArgs& A, int64_t s, int64_t d, double
     if (push && has_cost && (double)costv > cost_update_max) push = 0;
     if (push) {
       double gm[4], gs[16];
-      gate_params(x, P, gm, gs);
+      gate_params(sX, sP, gm, gs);
       if (maha(z, gm, gs) > maha_thr) push = 0;
     }
   }
