@@ -115,7 +115,7 @@ class Pipeline:
         self.depth = int(os.environ.get("TRK_PREFETCH_DEPTH", "1"))  # frames embedded ahead
         # the tracker's launches (mostly few-workgroup kernels) on a high-priority stream so
         # they dispatch as soon as CUs free up beside the encoder's full-GPU grids
-        prio = int(os.environ.get("TRK_TRACK_PRIO", "0"))
+        prio = int(os.environ.get("TRK_TRACK_PRIO", "1"))
         self.track_stream = torch.cuda.Stream(device=sc["feat"].device, priority=-1) if prio else None
 
     def capture(self):
