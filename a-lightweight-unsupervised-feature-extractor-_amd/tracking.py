@@ -598,14 +598,16 @@ class Tracking:
         dev = self.device
         t = self._mst.table
         idx = self._i32(rows).long()
-        p = default_cost_params(dict(w_app=1.0, w_bbox=0.0, w_conf=0.0, maha_thr=maha_thr), gate=True)
-        p.inf_cost = float(INF)
-        out = cost_combine(torch.from_numpy(np.ascontiguousarray(C_total_np, np.float32)).to(dev),
-                           t.pbox.index_select(0, idx), t.last_conf.index_select(0, idx),
+        # the kernel's own gate decision (d2 > maha_thr): all weights 0 on a zero C_app, and a
+        # gated pair's "cost" 1 -- so the mask is exactly the gate, whatever C_total holds
+        p = default_cost_params(dict(w_app=0.0, w_bbox=0.0, w_conf=0.0, maha_thr=maha_thr), gate=True)
+        p.inf_cost = 1.0
+        out = cost_combine(torch.zeros((M, N), device=dev), t.pbox.index_select(0, idx),
+                           t.last_conf.index_select(0, idx),
                            torch.as_tensor(np.asarray(det_boxes, np.float32).reshape(N, 4)).to(dev),
                            torch.ones(N, device=dev), p, t.gmean.index_select(0, idx),
                            t.gsinv.index_select(0, idx), torch.ones(M, device=dev, dtype=torch.int32))
-        gated = out["C_total"].cpu().numpy() >= np.float32(INF)
+        gated = out["C_total"].cpu().numpy() == np.float32(1.0)
         C_total_np[gated] = INF
         return C_total_np
 

@@ -45,17 +45,20 @@ PREROLL = 30
 
 
 # ------------------------------------------------------------ workload ----
-def silu(x):
-    return x / (1 + np.exp(-x))
+MAP_POOL = 16  # frames' maps in the rotating pool: 16 x 26 MB > the 256 MB Infinity Cache
 
 
-def make_scenes(dev, streams, N, frames, seed, C=512, H=40):
+def make_scenes(dev, streams, N, frames, seed, C=512, H=40, pool=MAP_POOL):
     """Per stream: N objects with w, h ~ U(32, 320) px in a 1280x1280
     letterboxed frame (rows 280..1000 = a 1080p picture), velocities
     U(-2, 2) px/frame bouncing at the borders, 0.5 px detection jitter,
-    conf ~ U(0.55, 0.99); detection order shuffled every frame."""
+    conf ~ U(0.55, 0.99); detection order shuffled every frame.  Feature
+    maps: a pool of `pool` frames of [streams, 512, 40, 40] f32 NCHW maps
+    (SiLU(randn)), frame f reads slot f % pool, so every frame's map read comes
+    from HBM, not from a cache that held it since the previous frame."""
     rng = np.random.default_rng(seed)
-    feat = silu(rng.standard_normal((streams, C, H, H)).astype(np.float32)).astype(np.float32)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    feat = torch.nn.functional.silu(torch.randn((pool, streams, C, H, H), generator=g, device=dev))
     w = rng.uniform(32, 320, (streams, N)); h = rng.uniform(32, 320, (streams, N))
     lo = np.stack([np.zeros_like(w), np.full_like(h, 280.0)], -1)
     hi = np.stack([1280 - w, 1000 - h], -1)
@@ -81,8 +84,13 @@ def make_scenes(dev, streams, N, frames, seed, C=512, H=40):
         v[bounce] *= -1
         p = np.clip(p, lo, hi)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    return dict(feat=t(feat), rois=t(rois), dbox=t(dbox), dconf=t(dconf), confs_host=dconf,
-                obj=obj, streams=streams, N=N, np=dict(feat=feat, rois=rois, dbox=dbox, dconf=dconf))
+    return dict(feat=feat, rois=t(rois), dbox=t(dbox), dconf=t(dconf), confs_host=dconf,
+                obj=obj, streams=streams, N=N, np=dict(rois=rois, dbox=dbox, dconf=dconf))
+
+
+def frame_map(sc, f):
+    """[streams, 512, 40, 40] map batch of frame f (rotating pool slot)"""
+    return sc["feat"][f % sc["feat"].shape[0]]
 
 
 class Pipeline:
@@ -138,12 +146,12 @@ class Pipeline:
         torch.cuda.synchronize()
 
     def _embed_from(self, rois):
-        roi = trk.roi_align(self.sc["feat"], rois, (self.S, self.S), 40 / 1280.0, 2, True,
+        roi = trk.roi_align(frame_map(self.sc, 0), rois, (self.S, self.S), 40 / 1280.0, 2, True,
                             out_dtype=torch.bfloat16, channels_last=True)
         return self.stage_embed(roi)
 
     def stage_roi(self, f):
-        return trk.roi_align(self.sc["feat"], self.sc["rois"][f], (self.S, self.S), 40 / 1280.0, 2, True,
+        return trk.roi_align(frame_map(self.sc, f), self.sc["rois"][f], (self.S, self.S), 40 / 1280.0, 2, True,
                              out_dtype=torch.bfloat16, channels_last=True)
 
     def stage_embed(self, roi):
@@ -300,7 +308,7 @@ def kernel_pass(pipe, f, reps=10):
         out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
 
     # roi_align kernel alone (map already NHWC) and the stage (NCHW map: + transpose)
-    nhwc = sc["feat"].contiguous(memory_format=torch.channels_last)
+    nhwc = frame_map(sc, f).contiguous(memory_format=torch.channels_last)
     timed("roi_align", lambda: trk.roi_align(nhwc, sc["rois"][f], (pipe.S, pipe.S), 40 / 1280.0, 2, True,
                                              out_dtype=torch.bfloat16, channels_last=True))
     timed("roi_stage", lambda: pipe.stage_roi(f))
@@ -339,15 +347,38 @@ def kernel_pass(pipe, f, reps=10):
     return out, M
 
 
-def cpu_baseline(sc, sd, budget_s=20.0):
-    """The reference's CPU path, ported (oracle/): torchvision-semantics
-    roi_align (C), the fp32 encoder restated in plain torch, the bank top-k +
-    bbox + conf + Mahalanobis cost (C), and the reference's own solver
-    scipy.optimize.linear_sum_assignment.  Bounded sample: whole frames of one
-    stream at N=256 (tracks = the stream's objects, banks of 30) until
-    ~budget_s of CPU time."""
+def _cpu_info():
+    """host CPU model and physical cores (lscpu), and the threads torch uses"""
+    import subprocess
+    model, cores = None, None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {l.split(":", 1)[0].strip(): l.split(":", 1)[1].strip() for l in out.splitlines() if ":" in l}
+        model = kv.get("Model name")
+        cps, socks = kv.get("Core(s) per socket"), kv.get("Socket(s)")
+        cores = int(cps) * int(socks) if cps and socks else None
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    return model, cores
+
+
+def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
+    """The reference's CPU path on this box's host cores, two modes (SURVEY.md
+    8(d)), same inputs, 3 warm-up frames, per-frame medians:
+      vectorised        oracle roi_align (C restatement of torchvision's CPU
+                        kernel, 1 thread) + the fp32 encoder in plain torch
+                        (all torch threads) + the oracle's vectorised cost incl.
+                        gate (C, 1 thread) + scipy.optimize.linear_sum_assignment
+      reference_literal the same roi_align / encoder / LSAP with the cost as the
+                        reference's Python computes it: the per-track top-k loop
+                        (mainTracking.py:173-210) and the per-pair 4x4-inverse
+                        gating loop (:327-336) -- oracle/literal.py
+    One stream at N=256 (tracks = the stream's objects, banks of 30).  The
+    literal mode's loops take seconds per frame, so its cost stage is sampled on
+    frames_lit frames (the stages are timed separately and the medians added)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
+    import literal as LIT
     from scipy.optimize import linear_sum_assignment
     npw = sc["np"]
     N = sc["N"]
@@ -355,26 +386,51 @@ def cpu_baseline(sc, sd, budget_s=20.0):
     bank = rng.standard_normal((N, 30, 128)).astype(np.float32)
     bank /= np.linalg.norm(bank, axis=-1, keepdims=True)
     gm = np.zeros((N, 4)); gs = np.tile(np.eye(4).reshape(1, 16) / 11.0, (N, 1))
-    frames, t0 = 0, time.perf_counter()
-    while True:
-        f, s = PREROLL + frames, frames % sc["streams"]
-        rois = npw["rois"][f % len(npw["rois"]), s * N:(s + 1) * N].copy()
+    kf_x = [np.zeros(8) for _ in range(N)]
+    kf_P = [np.diag([10.0] * 4 + [1000.0] * 4) for _ in range(N)]
+    t_roi, t_enc, t_cost, t_lsap, t_lit = [], [], [], [], []
+    t_start = time.perf_counter()
+    for q in range(3 + frames_vec):
+        f = (PREROLL + q) % len(npw["rois"])
+        s = q % sc["streams"]
+        rois = npw["rois"][f, s * N:(s + 1) * N].copy()
         rois[:, 0] = 0
-        roi = O.roi_align(npw["feat"][s:s + 1], rois, (10, 10), 40 / 1280.0, 2, True)
+        fmap = frame_map(sc, f)[s:s + 1].cpu().numpy()
+        t0 = time.perf_counter()
+        roi = O.roi_align(fmap, rois, (10, 10), 40 / 1280.0, 2, True)
+        t1 = time.perf_counter()
         with torch.no_grad():
             emb = O.encoder_forward(sd, torch.from_numpy(roi)).numpy()
-        b = npw["dbox"][f % len(npw["dbox"]), s]
-        out = O.cost_build(bank, np.full(N, 30, np.int32), emb, b, b, npw["dconf"][f % len(npw["dconf"]), s],
-                           npw["dconf"][f % len(npw["dconf"]), s], gm, gs, np.ones(N, np.int32))
+        t2 = time.perf_counter()
+        b, c = npw["dbox"][f, s], npw["dconf"][f, s]
+        out = O.cost_build(bank, np.full(N, 30, np.int32), emb, b, b, c, c, gm, gs, np.ones(N, np.int32))
+        t3 = time.perf_counter()
         linear_sum_assignment(out["C_total"])
-        frames += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or frames >= 64:
+        t4 = time.perf_counter()
+        if q < frames_lit + 1:  # literal cost: 1 warm-up + frames_lit timed
+            capp = LIT.build_c_app_topk_literal([list(bank[i]) for i in range(N)], list(emb))
+            tot = O.cost_combine(capp, b, b, c, c)["C_total"]
+            LIT.kalman_gating_literal(tot, kf_x, kf_P, b.tolist())
+            if q >= 1:
+                t_lit.append(time.perf_counter() - t4)
+        if q >= 3:
+            t_roi.append(t1 - t0); t_enc.append(t2 - t1); t_cost.append(t3 - t2); t_lsap.append(t4 - t3)
+        if time.perf_counter() - t_start > 3 * budget_s:
             break
-    return dict(value=round(frames * N / el, 2), unit="ROIs/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{frames} frames x N={N} of one stream in {el:.1f}s: oracle roi_align (C, 1 thread) + "
-                       f"fp32 encoder (plain torch CPU, {torch.get_num_threads()} threads) + oracle cost incl. "
-                       f"gate (C, 1 thread) + scipy linear_sum_assignment")
+    med = lambda v: float(np.median(v))
+    vec = med(t_roi) + med(t_enc) + med(t_cost) + med(t_lsap)
+    lit = med(t_roi) + med(t_enc) + med(t_lit) + med(t_lsap)
+    model, cores = _cpu_info()
+    thr = torch.get_num_threads()
+    return dict(value=round(N / vec, 2), unit="ROIs/s", cores=thr, kind="port",
+                sample=f"one stream, N={N}, 3 warm-up frames, medians over {len(t_roi)} frames "
+                       f"(literal cost stage: {len(t_lit)} frames): roi_align {med(t_roi) * 1e3:.0f} ms (C, 1 thread) + "
+                       f"fp32 encoder {med(t_enc) * 1e3:.0f} ms (torch CPU, {thr} threads) + cost "
+                       f"{med(t_cost) * 1e3:.1f} ms (C, 1 thread) + scipy LSAP {med(t_lsap) * 1e3:.1f} ms",
+                cpu_model=model, physical_cores=cores,
+                modes={"vectorised": {"ms_per_frame": round(vec * 1e3, 1), "rois_per_s": round(N / vec, 2)},
+                       "reference_literal": {"ms_per_frame": round(lit * 1e3, 1), "rois_per_s": round(N / lit, 2),
+                                             "cost_ms": round(med(t_lit) * 1e3, 1)}})
 
 
 def timed_region(step, steps, dist, sync, red_dev, finish=None):
