@@ -35,7 +35,11 @@
 
 #include <type_traits>
 
-unsigned long long* g_lsap_prof = nullptr;  // trk_set_tuning("lsap_prof", ...) via trk_lsap_set_prof
+unsigned long long* g_lsap_prof = nullptr;  // trk_lsap_set_prof (diagnostics)
+int g_lsap_dev_lds_kb = 24;  // trk_set_tuning("lsap_dev_lds_kb"): LDS budget of trk_lsap_dev workgroups.  Small
+                             // enough to be placed beside the encoder's workgroups (a CU's whole LDS would wait for
+                             // a CU free of them); the leading-row shortcut needs no ring, the sequential rows re-read
+                             // revisited rows from L2 when the ring is short
 
 namespace {
 
@@ -53,6 +57,7 @@ struct LsapArgs {
   int32_t* assign;
   double cost_max;
   int ring_rows;  // RB (ring capacity in rows) for the largest working nc of the batch
+  int lds_bytes;  // > 0: the launch's whole LDS budget; RB is then sized for each matrix's own nc
   unsigned long long* prof;  // trk_set_tuning("lsap_prof"): per-matrix solver cycle breakdown, else null
   const int32_t* dev_nr;  // trk_lsap_dev: shapes in device memory, bounded by nr_bound / nc_bound
   const int32_t* dev_nc;
@@ -169,7 +174,9 @@ lsap_kernel(const LsapArgs A) {
   const bool tr = nc0 < nr0;
   const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;  // working problem: nr <= nc
   const int64_t ld = A.ld;
-  const int RB = min(A.ring_rows, nr);
+  const int RB = A.lds_bytes > 0
+                     ? min(max((A.lds_bytes - 12 * nr - 48) / (nc * (int)sizeof(T) + 4), 2), nr)
+                     : min(A.ring_rows, nr);
   const bool whole = RB >= nr;
   // loaders run at most LA rows ahead of the solver, so the RB - LA most
   // recently solved rows stay resident for revisits (rows on augmenting paths)
@@ -608,14 +615,15 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
   const size_t fixed = 12 * (size_t)wr_max + 64;
   const size_t row_bytes = esz * (size_t)wc_max + 4;
   TRK_REQUIRE(fixed + 2 * row_bytes <= lds_limit, "lsap_dev: matrix too wide for the LDS ring");
-  int rb = (int)std::min<size_t>((lds_limit - fixed) / row_bytes, (size_t)wr_max);
-  rb = std::max(rb, 2);
-  const size_t lds = fixed + (size_t)rb * row_bytes + 16;
+  // the budget, raised to what two ring rows of the widest bound need
+  const size_t lds = std::min(lds_limit, std::max((size_t)g_lsap_dev_lds_kb * 1024, fixed + 2 * row_bytes + 16));
+  const int rb = 2;  // unused: the kernel sizes RB per matrix from lds (a.lds_bytes)
   for (int64_t f0 = 0; f0 < F; f0 += kMaxBatch) {
     const int nf = (int)std::min<int64_t>(kMaxBatch, F - f0);
     LsapArgs a;
     memset(&a, 0, sizeof a);
     a.ring_rows = rb;
+    a.lds_bytes = (int)lds;
     a.dev_nr = dev_nr + f0;
     a.dev_nc = dev_nc + f0;
     a.nr_bound = (int)nr_bound;

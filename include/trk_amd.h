@@ -51,7 +51,9 @@ const char* trk_last_error(void);
  *                    2 interleaved, 4 dedicated DMA waves, 5 256-channel tiles
  *   "g1dw_persist"   0 (default); > 0: persistent tile queue; 66: depthwise interleaved into the
  *                    next tile's K loop
- *   "cost_v2"        0 (default): detection-tile cost kernel; 1: bank-resident kernel */
+ *   "cost_v2"        0 (default): detection-tile cost kernel; 1: bank-resident kernel
+ *   "lsap_dev_lds_kb" LDS budget of trk_lsap_dev workgroups (default 24: they fit beside the
+ *                    encoder's workgroups instead of waiting for a whole CU) */
 int trk_set_tuning(const char* key, int value);
 
 /* ------------------------------------------------------------------------
