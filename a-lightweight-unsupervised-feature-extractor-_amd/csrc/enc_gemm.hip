@@ -465,6 +465,70 @@ constexpr size_t G1_TILE = (size_t)2 * G1_P * (G1_BN / 2) * 4;   // bf16 pairs [
 constexpr size_t G1_W = (size_t)25 * (G1_BN / 2) * 8;            // f32 pairs [25][64]
 constexpr size_t G1_LDS = NSTAGE * G1_STAGE > G1_TILE + G1_W ? NSTAGE * G1_STAGE : G1_TILE + G1_W;
 
+// Depthwise 5x5 of output rows [OY0, OY1) x columns [X0, X0 + 5) of a 10x10
+// ROI for the lane's channel pair: input rows / columns clipped to the ROI (the
+// zero padding's taps are skipped at compile time), weights read from LDS.  Each
+// output accumulates its taps in ascending input row, then ascending kx --
+// dwconv5_rows2_kernel's order, so Y2 is bit-identical.
+template <int OY0, int OY1, int X0>
+__device__ __forceinline__ void dw5_block(const uint32_t* __restrict__ src, const dw_pair_t* __restrict__ w,
+                                          uint32_t* __restrict__ dst, int ldd) {
+  constexpr int NY = OY1 - OY0;
+  constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY1 + 1 > G1_S - 1 ? G1_S - 1 : OY1 + 1;
+  constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
+  constexpr int NX = IX1 - IX0 + 1;
+  dw_pair_t acc[NY][5];
+#pragma unroll
+  for (int oy = 0; oy < NY; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) acc[oy][ox] = dw_pair_t{0.f, 0.f};
+  // input rows are software-pipelined: row iy + 1 is read from LDS while row iy is used
+  uint32_t nxt[NX];
+#pragma unroll
+  for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(IY0 * G1_S + IX0 + ix) * (G1_BN / 2)];
+#pragma unroll 1
+  for (int iy = IY0; iy <= IY1; ++iy) {  // rolled: one input row's values live at a time
+    dw_pair_t in[NX];
+#pragma unroll
+    for (int ix = 0; ix < NX; ++ix) in[ix] = dw_pair_t{__uint_as_float(nxt[ix] << 16), __uint_as_float(nxt[ix] & 0xffff0000u)};
+    const int iyn = iy < IY1 ? iy + 1 : iy;
+#pragma unroll
+    for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(iyn * G1_S + IX0 + ix) * (G1_BN / 2)];
+#pragma unroll
+    for (int oy = 0; oy < NY; ++oy) {
+      const int ky = iy - (OY0 + oy) + 2;
+      if (ky < 0 || ky > 4) continue;
+      dw_pair_t wr[5];  // weight row ky (LDS)
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx) wr[kx] = w[(ky * 5 + kx) * (G1_BN / 2)];
+#pragma unroll
+      for (int ox = 0; ox < 5; ++ox)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) {
+          const int ix = X0 + ox + kx - 2;
+          if (ix >= IX0 && ix <= IX1)
+            acc[oy][ox] = __builtin_elementwise_fma(wr[kx], in[ix - IX0], acc[oy][ox]);
+        }
+    }
+  }
+#pragma unroll
+  for (int oy = 0; oy < NY; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) {
+      const uint32_t v = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
+      if (ldd > 0) dst[((OY0 + oy) * G1_S + X0 + ox) * ldd] = v;
+      else asm volatile("" ::"v"(v));  // experiment (enc_gemm_dbg 256): no Y2 stores
+    }
+}
+
+// one 5x5 output quadrant (QY, QX), in two row blocks (fewer live accumulators)
+template <int QY, int QX>
+__device__ __forceinline__ void dw5_quadrant(const uint32_t* __restrict__ src, const dw_pair_t* __restrict__ w,
+                                             uint32_t* __restrict__ dst, int ldd) {
+  dw5_block<5 * QY, 5 * QY + 3, 5 * QX>(src, w, dst, ldd);
+  dw5_block<5 * QY + 3, 5 * QY + 5, 5 * QX>(src, w, dst, ldd);
+}
+
 template <int MODE>
 __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
                                           const float* __restrict__ wdw, uint16_t* __restrict__ Y2, int M, int N,
@@ -567,9 +631,19 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
   }
   __syncthreads();
 
+  const int cp = lane;
+  // depthwise weights [25][64 channel pairs] of the tile: global loads issued now,
+  // written to LDS after Y1 (their latency hides behind the Y1 writes)
+  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G1_TILE);
+  constexpr int NWQ = (25 * (G1_BN / 2) + 511) / 512;
+  dw_pair_t wreg[NWQ];
+#pragma unroll
+  for (int j = 0; j < NWQ; ++j) {
+    const int q = min(j * 512 + tid, 25 * (G1_BN / 2) - 1), k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
+    wreg[j] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
+  }
   // Y1 (bf16-rounded, rows < 200 of the tile) -> LDS [200][64 channel pairs]
   uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
-  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G1_TILE);
   {
     const int cl = wn * 32 + (lane & 31);  // channel within the tile
 #pragma unroll
@@ -584,59 +658,27 @@ __device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const 
       }
     }
   }
-  for (int q = tid; q < 25 * (G1_BN / 2); q += 512) {
-    const int k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
-    wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
-  }
+#pragma unroll
+  for (int j = 0; j < NWQ; ++j)
+    if (j * 512 + tid < 25 * (G1_BN / 2)) wl[j * 512 + tid] = wreg[j];
   __syncthreads();
 
-  // depthwise 5x5: task = (ROI, output row pair), lane = channel pair
-  const int cp = lane;
-  for (int task = (dbg & 16) ? 1 << 20 : wave; task < 2 * (G1_S / 2); task += 8) {
-    const int roi = task / (G1_S / 2), y0 = 2 * (task % (G1_S / 2));
+  // depthwise 5x5: wave = (ROI, 5x5 output quadrant): 8 equal tasks, lane = channel pair
+  if (dbg & 16) return;
+  {
+    const int roi = wave >> 2, quad = wave & 3;
     const int64_t rbase = m0 + roi * G1_P;
-    if (rbase >= M) continue;
-    const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2);
-    dw_pair_t a0[G1_S], a1[G1_S];
-#pragma unroll
-    for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const int yy = y0 - 2 + r;
-      if (yy < 0 || yy >= G1_S) continue;
-      dw_pair_t rr[G1_S];
-#pragma unroll
-      for (int x = 0; x < G1_S; ++x) {
-        const uint32_t v = src[(yy * G1_S + x) * (G1_BN / 2) + cp];
-        rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+    if (rbase < M) {
+      const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2) + cp;
+      const dw_pair_t* wq = wl + cp;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0) + cp;
+      const int ldd = (dbg & 256) ? 0 : N / 2;
+      switch (quad) {
+        case 0: dw5_quadrant<0, 0>(src, wq, dst, ldd); break;
+        case 1: dw5_quadrant<0, 1>(src, wq, dst, ldd); break;
+        case 2: dw5_quadrant<1, 0>(src, wq, dst, ldd); break;
+        default: dw5_quadrant<1, 1>(src, wq, dst, ldd); break;
       }
-      // taps in the zero padding (x + kx - 2 outside the ROI) are skipped
-      if (r <= 4) {
-        dw_pair_t wv[5];
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G1_BN / 2) + cp];
-#pragma unroll
-        for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx)
-            if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
-      }
-      if (r >= 1) {
-        dw_pair_t wv[5];
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G1_BN / 2) + cp];
-#pragma unroll
-        for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx)
-            if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
-      }
-    }
-    uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
-#pragma unroll
-    for (int x = 0; x < G1_S; ++x) {
-      dst[(y0 * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a0[x].x, a0[x].y);
-      dst[((y0 + 1) * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a1[x].x, a1[x].y);
     }
   }
 }

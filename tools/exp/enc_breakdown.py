@@ -1,6 +1,6 @@
 """Encoder GEMM time breakdown at the bench shape (M = 204800 rows, 2048 ROIs of
 10x10): each fused kernel with parts of its work switched off through the
-enc_gemm_dbg knob.  g1dw: 16 = no depthwise phase, 32 = K loop of 2 steps.
+enc_gemm_dbg knob.  g1dw: 16 = no depthwise phase, 32 = K loop of 2 steps, 256 = depthwise without the Y2 stores.
 gemm4: 1 = no epilogue, 2 = no stores, 4 = no ROI sums.  One JSON line each."""
 import importlib, json, os, sys
 import torch
@@ -36,7 +36,8 @@ def timeit(fn, reps=10):
 
 
 items = {
-    "g1dw": (lambda: ops.enc_g1_dwconv(X, W1, wdw), [0, 16, 32, 48, 16 | 64, 16 | 128, 16 | 64 | 128], 2 * M * 512 * 1024),
+    "g1dw": (lambda: ops.enc_g1_dwconv(X, W1, wdw), [0, 256, 16, 32, 48, 16 | 64, 16 | 128, 16 | 64 | 128],
+             2 * M * 512 * 1024),
     "plain256": (lambda: ops.enc_gemm(X, W1), [0], 2 * M * 512 * 1024),
     "dsc": (lambda: ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True), [0, 1, 2, 4], 2 * M * 1024 * 512),
     "trans": (lambda: ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True), [0, 1, 4], 2 * M * 1024 * 512),
