@@ -1586,6 +1586,215 @@ __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t nt
   tq.finish();
 }
 
+// ---------------------------------------------------------------------------
+// gemm8: 256 x 256 tiles, BK = 64, one 8-wave workgroup per CU (waves 2 (M) x 4
+// (N), wave tile 128 x 64 = 8 x 4 MFMA 16x16x32 tiles: 0.375 KB of fragment
+// reads per MFMA).  Both operands are staged by LDS-DMA into two 64 KiB K-tile
+// buffers: tile kt + 1's 8 loads per thread are issued at the top of step kt
+// and have the whole step's MFMAs to land; one vmcnt(0) + barrier per step.
+// The LDS image of a 256 x 64 operand is 16-B chunk c of row r at r * 8 + (c ^
+// ((r >> 1) & 7)) -- the 16-lane groups of every ds_read_b128 hit 16 distinct
+// bank groups -- laid down lane-linearly by the DMA (the XOR is applied to the
+// per-lane source address).  The SE scale of the transition is applied in LDS by
+// the thread that staged each chunk (its own vmcnt(0) orders it), before the
+// step's barrier.  Epilogue (transition): bias + SiLU + per-ROI column sums; a
+// wave's 128 rows are exactly one 128-row partial tile of the ROI sums.
+constexpr int G8_BM = 256, G8_BN = 256, G8_BK = 64, G8_CH = G8_BK / 8;
+constexpr int G8_POS = G8_BM * G8_CH;                          // 16-B slots of one operand image (2048)
+constexpr size_t G8_BUF = (size_t)2 * G8_POS * 16;             // A + B images of one K tile: 64 KiB
+constexpr int G8_SROI = 4;                                      // ROIs a 256-row tile spans (P >= 86)
+constexpr size_t G8_STILE = (size_t)G8_SROI * 512 * 4;          // s rows of those ROIs (kscale <= 512)
+constexpr size_t G8_LDS = 2 * G8_BUF + G8_STILE;               // 136 KiB
+
+__device__ __forceinline__ int g8_swz(int r, int c) { return r * G8_CH + (c ^ ((r >> 1) & 7)); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntiles) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* bufs = reinterpret_cast<uint4*>(smem);                // [2][A 2048 | B 2048] uint4
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t lb = xcd_remap(blockIdx.x, ntiles);
+  const int ntile_n = a.N / G8_BN;
+  const int ntl = (int)(lb % (ntile_n * a.groups));
+  const int64_t mt = lb / (ntile_n * a.groups);
+  const int g = ntl / ntile_n, n0 = (ntl % ntile_n) * G8_BN;
+  const int64_t m0 = mt * G8_BM;
+  const uint16_t* Ag = a.A + (int64_t)g * a.K;
+  const uint16_t* Bg = a.B + (int64_t)g * a.N * a.K;
+  const int nk = a.K / G8_BK;
+  const int64_t roi_base = m0 / a.P;
+
+  // DMA sources: slot p = q * 512 + tid of each image (row p >> 3, data chunk by the swizzle)
+  const uint16_t* asrc[4];
+  const uint16_t* bsrc[4];
+  int achunk[4], arow[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = q * 512 + tid, r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
+    arow[q] = r;
+    achunk[q] = c;
+    asrc[q] = Ag + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
+    bsrc[q] = Bg + (int64_t)(n0 + r) * a.K + c * 8;
+  }
+  auto issue = [&](int kt) {
+    uint4* d = bufs + (kt & 1) * (2 * G8_POS) + wave * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * G8_BK), LPTR(d + q * 512), 16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + kt * G8_BK), LPTR(d + G8_POS + q * 512), 16, 0, 0);
+  };
+
+  // transition: the SE scales of the tile's ROIs (LDS, [G8_SROI][kscale] f32) and, per staged
+  // chunk, the s row it is scaled with
+  const float* stile = reinterpret_cast<const float*>(smem + 2 * G8_BUF);
+  int srow[4];
+  if constexpr (EPI == EPI_TRANS) {
+    const int per = a.kscale / 4;                       // 16-B pieces per s row
+    const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
+    for (int p = tid; p < G8_SROI * per; p += 512) {
+      const int slot = p / per;
+      const int64_t roi = min(roi_base + slot, nroi - 1);
+      reinterpret_cast<float4*>(smem + 2 * G8_BUF)[p] =
+          *reinterpret_cast<const float4*>(a.scale + roi * a.kscale + (p % per) * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = min(m0 + arow[q], (int64_t)a.M - 1);
+      srow[q] = (int)(row / a.P - roi_base) * a.kscale + achunk[q] * 8;
+    }
+  }
+  auto transform = [&](int kt) {  // x_f columns of K tile kt: bf16(x * s[roi][k])
+    if constexpr (EPI == EPI_TRANS) {
+      if (kt * G8_BK < a.kscale) {
+        uint4* d = bufs + (kt & 1) * (2 * G8_POS);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint4 v = d[q * 512 + tid];
+          const float4 s0 = *reinterpret_cast<const float4*>(stile + srow[q] + kt * G8_BK);
+          const float4 s1 = *reinterpret_cast<const float4*>(stile + srow[q] + kt * G8_BK + 4);
+          const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            w[e] = pack_bf16x2(__uint_as_float(w[e] << 16) * sv[2 * e], __uint_as_float(w[e] & 0xffff0000u) * sv[2 * e + 1]);
+          d[q * 512 + tid] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    }
+  };
+
+  f4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // s tile (plain stores) visible before the first transform
+  transform(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue(kt + 1);
+    const uint4* ab = bufs + (kt & 1) * (2 * G8_POS);
+    const uint4* bb = ab + G8_POS;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = h * 4 + fc;
+      bf8v bfr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bfr[t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf8v afr = *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + i * 16 + fr, c));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[t], acc[i][t], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    if (kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      transform(kt + 1);
+    }
+    __syncthreads();
+  }
+
+  if constexpr (EPI == EPI_TRANS) {
+    // bias + SiLU + per-ROI column sums over this wave's 128 rows (one partial tile)
+    const int64_t r0 = m0 + wr * 128;
+    const int P = a.P;
+    const int64_t roi0 = r0 / P;
+    const int nxt = P - (int)(r0 - roi0 * P);   // first row (within the 128) of ROI roi0 + 1
+    const bool full = r0 + 128 <= (int64_t)a.M;
+    float bias4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bias4[t] = a.bias[n0 + wc * 64 + t * 16 + fr];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float sm[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        f4v v = acc[i][t];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e] + bias4[t]);
+        const int lo = i * 16;
+        if (full && lo + 16 <= nxt) {
+          sm[0] += (v[0] + v[1]) + (v[2] + v[3]);
+        } else if (full && lo >= nxt && lo + 16 <= nxt + P) {
+          sm[1] += (v[0] + v[1]) + (v[2] + v[3]);
+        } else if (full && lo >= nxt + P) {
+          sm[2] += (v[0] + v[1]) + (v[2] + v[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int ro = lo + fc * 4 + e;
+            const float x = (r0 + ro < a.M) ? v[e] : 0.f;
+            sm[0] += ro < nxt ? x : 0.f;
+            sm[1] += (ro >= nxt && ro < nxt + P) ? x : 0.f;
+            sm[2] += ro >= nxt + P ? x : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) sm[q] = sum_xor32(sum_xor16(sm[q]));
+      if (fc == 0) {
+        const int64_t last = min(r0 + 128, (int64_t)a.M) - 1;
+        const int nslot = (int)(last / P - roi0) + 1;
+        const int64_t th = r0 / kPartRows;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          if (q < nslot) {
+            const int64_t roi = roi0 + q;
+            const int j = (int)(th - roi * P / kPartRows);
+            a.sums[(roi * kPart + j) * a.ld_sums + (int64_t)g * a.N + n0 + wc * 64 + t * 16 + fr] =
+                llrintf(sm[q] * kFix);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int EPI>
+int launch8(const EncGemmArgs& a, hipStream_t st) {
+  const int64_t nwg = ((int64_t)a.M + G8_BM - 1) / G8_BM * (a.N / G8_BN) * a.groups;
+  TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm8: too many workgroups");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm8_kernel<EPI>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg);
+  return trk::check_launch("gemm8_kernel");
+}
+
 int cu_count() {
   static int n = 0;
   if (!n) {
@@ -1692,7 +1901,8 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  if (g_enc_gemm == 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
+  if (g_enc_gemm == 2 && P >= 86 && K % 64 == 0 && kscale % 64 == 0 && kscale <= 512) return launch8<EPI_TRANS>(a, st);
+  if (g_enc_gemm >= 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
   return launch<EPI_TRANS, 128, 256>(a, st);
 }
 

@@ -401,6 +401,17 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     assert (st0 - st).abs().max().item() <= 1e-3 * st.abs().max().item()
     st2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
     assert torch.equal(st, st2)
+    # the 256 x 256 / BK 64 kernel (enc_gemm 2; P >= 86): same math, another f32 summation order
+    if P >= 86:
+        try:
+            assert L.trk_set_tuning(b"enc_gemm", 2) == 0
+            st8 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+            st8b = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+        finally:
+            assert L.trk_set_tuning(b"enc_gemm", 1) == 0
+        assert (st8 - st).abs().max().item() <= 1e-3 * st.abs().max().item()
+        assert (st8 - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item()
+        assert torch.equal(st8, st8b)
     # plain GEMM (the first 1x1 convs), strided A rows
     W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
     A = Y2[:, :512]
