@@ -121,6 +121,8 @@ def _declare(L):
     L.trk_lsap_dev.restype = i32
     L.trk_lsap_set_prof.argtypes = [P]
     L.trk_lsap_set_prof.restype = i32
+    L.trk_enc_set_prof.argtypes = [P]
+    L.trk_enc_set_prof.restype = i32
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

@@ -1608,8 +1608,19 @@ constexpr size_t G8_LDS = 2 * G8_BUF + G8_STILE;               // 136 KiB
 
 __device__ __forceinline__ int g8_swz(int r, int c) { return r * G8_CH + (c ^ ((r >> 1) & 7)); }
 
-template <int EPI>
-__global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntiles) {
+__device__ __forceinline__ unsigned long long g8_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// PROF (trk_enc_set_prof, diagnostics only): waves 0 and 4 of each workgroup record
+// [start, prologue done, K loop done, end, sum of the per-step vmcnt waits, sum of
+// the per-step barrier waits, hw id, 0] at prof[(wg * 2 + wave / 4) * 8]
+template <int EPI, bool PROF>
+__global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntiles, unsigned long long* prof) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint4* bufs = reinterpret_cast<uint4*>(smem);                // [2][A 2048 | B 2048] uint4
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1694,36 +1705,64 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
     for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fc = lane >> 4;
+  unsigned long long p_t0 = 0, p_t1 = 0, p_t2 = 0, p_w = 0, p_b = 0;
+  if constexpr (PROF) p_t0 = g8_stamp();
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // s tile (plain stores) visible before the first transform
   transform(0);
   __syncthreads();
+  if constexpr (PROF) p_t1 = g8_stamp();
+  // K step: 16 MFMA groups s = (k half h, row tile i), 4 MFMAs each; the A fragment of
+  // group s + 1 (and the next half's B fragments) are read while group s runs, and the
+  // next K tile's 8 LDS-DMA pieces are issued one per odd group, between MFMAs
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue(kt + 1);
+    const bool pf = kt + 1 < nk;
     const uint4* ab = bufs + (kt & 1) * (2 * G8_POS);
     const uint4* bb = ab + G8_POS;
+    uint4* dn = bufs + ((kt + 1) & 1) * (2 * G8_POS) + wave * 64;
+    auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 7) * 16 + fr, (s >> 3) * 4 + fc)); };
+    bf8v bfr[2][4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = h * 4 + fc;
-      bf8v bfr[4];
+    for (int t = 0; t < 4; ++t) bfr[0][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, fc));
+    bf8v afr = rd_a(0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bfr[t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, c));
+    for (int s = 0; s < 16; ++s) {
+      const int h = s >> 3, i = s & 7;
+      bf8v anext = afr;
+      if (s < 15) anext = rd_a(s + 1);
+      if (s == 4) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf8v afr = *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + i * 16 + fr, c));
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[t], acc[i][t], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        for (int t = 0; t < 4; ++t) bfr[1][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, 4 + fc));
       }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[h][t], acc[i][t], 0, 0, 0);
+      if (pf && (s & 1)) {
+        const int q = s >> 1;  // piece q: A slots q*512.. (q < 4), B slots (q - 4)*512..
+        if (q < 4)
+          __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + (kt + 1) * G8_BK), LPTR(dn + q * 512), 16, 0, 0);
+        else
+          __builtin_amdgcn_global_load_lds(GPTR(bsrc[q - 4] + (kt + 1) * G8_BK), LPTR(dn + G8_POS + (q - 4) * 512), 16, 0, 0);
+      }
+      afr = anext;
     }
+    unsigned long long pa = 0, pb = 0;
+    if constexpr (PROF) pa = g8_stamp();
     if (kt + 1 < nk) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (PROF) pb = g8_stamp();
       transform(kt + 1);
+    } else if constexpr (PROF) {
+      pb = pa;
     }
     __syncthreads();
+    if constexpr (PROF) {
+      const unsigned long long pc = g8_stamp();
+      p_w += pb - pa;
+      p_b += pc - pb;
+    }
   }
+  if constexpr (PROF) p_t2 = g8_stamp();
 
   if constexpr (EPI == EPI_TRANS) {
     // bias + SiLU + per-ROI column sums over this wave's 128 rows (one partial tile)
@@ -1779,7 +1818,18 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
       }
     }
   }
+  if constexpr (PROF) {
+    const unsigned long long p_t3 = g8_stamp();
+    if ((wave & 3) == 0 && lane == 0) {
+      unsigned long long* o = prof + ((int64_t)blockIdx.x * 2 + (wave >> 2)) * 8;
+      unsigned hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      o[0] = p_t0; o[1] = p_t1; o[2] = p_t2; o[3] = p_t3; o[4] = p_w; o[5] = p_b; o[6] = hw; o[7] = 0;
+    }
+  }
 }
+
+unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics)
 
 template <int EPI>
 int launch8(const EncGemmArgs& a, hipStream_t st) {
@@ -1787,11 +1837,16 @@ int launch8(const EncGemmArgs& a, hipStream_t st) {
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm8: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm8_kernel<EPI>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg);
+  if (g_enc_prof)
+    hipLaunchKernelGGL((gemm8_kernel<EPI, true>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, g_enc_prof);
+  else
+    hipLaunchKernelGGL((gemm8_kernel<EPI, false>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, nullptr);
   return trk::check_launch("gemm8_kernel");
 }
 
@@ -1975,4 +2030,11 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
                      (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
   return trk::check_launch("g1dw_kernel");
+}
+
+// diagnostics: gemm8 per-workgroup timestamps (PROF variant above); buf holds
+// >= 16 * workgroups u64, nullptr switches back to the plain kernel
+extern "C" int trk_enc_set_prof(unsigned long long* buf) {
+  g_enc_prof = buf;
+  return TRK_OK;
 }

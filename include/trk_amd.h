@@ -153,6 +153,9 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
  * cycle breakdown into buf [F][8] u64 (shader clocks: waiting for rows, scans +
  * argmin, dual updates, augmentation; iterations, total, nr, nc).  NULL = off. */
 int trk_lsap_set_prof(unsigned long long* buf);
+/* diagnostics: per-workgroup timestamps of the 256x256 encoder GEMM (enc_gemm=2);
+ * buf >= 16 u64 per workgroup, NULL = off */
+int trk_enc_set_prof(unsigned long long* buf);
 
 /* ------------------------------------------------------------------------
  * Encoder helpers (the non-GEMM parts of encoderAndHead.Model's eval graph,
