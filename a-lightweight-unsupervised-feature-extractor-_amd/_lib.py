@@ -115,14 +115,18 @@ def _declare(L):
     for n in ("trk_step_begin", "trk_step_mid", "trk_step_end", "trk_step_apply"):
         getattr(L, n).restype = i32
     L.trk_build_cost_dev.argtypes = [i64, i64, i64, P, P, P, i64, i64, P, P, P, P, P, P, P, P, P, P,
-                                     ctypes.POINTER(CostParams), P, P, P]
+                                     ctypes.POINTER(CostParams), P, P, P, P]
     L.trk_build_cost_dev.restype = i32
+    L.trk_cost_work_bytes.argtypes = [i64, i64]
+    L.trk_cost_work_bytes.restype = i64
     L.trk_lsap_dev.argtypes = [i64, P, i32, i64, i64, P, P, i64, i64, i64, P, P, P, P, P, i64, f64, P]
     L.trk_lsap_dev.restype = i32
     L.trk_lsap_set_prof.argtypes = [P]
     L.trk_lsap_set_prof.restype = i32
     L.trk_enc_set_prof.argtypes = [P]
     L.trk_enc_set_prof.restype = i32
+    L.trk_cost_set_prof.argtypes = [P]
+    L.trk_cost_set_prof.restype = i32
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

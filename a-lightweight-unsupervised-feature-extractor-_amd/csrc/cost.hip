@@ -22,8 +22,11 @@
 // the one FMA torch's CPU norm performs is written as an explicit fmaf.
 #include "trk_common.h"
 
-int g_cost_v2 = 0;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel (Nmax <= 272; its 147 KiB LDS
-                    // workgroups stall behind the encoder in the pipeline: 1.23M vs 1.51M ROIs/s), 0 = cost_kernel
+int g_cost_v2 = 0;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel on trk_build_cost (Nmax <= 272;
+                    // its 147 KiB LDS workgroups stall behind the encoder in the pipeline: 1.23M vs 1.51M ROIs/s),
+                    // and cost_kernel instead of cost3 on trk_build_cost_dev (A/B); 0 = default
+
+unsigned long long* g_cost_prof = nullptr;  // trk_cost_set_prof (diagnostics)
 
 namespace {
 
@@ -347,6 +350,189 @@ __global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// cost3 (trk_build_cost_dev with a workspace): the track's bank is the resident
+// MFMA A operand, the detections stream -- with no LDS, so its workgroups are
+// placed beside the encoder's (cost2's 147 KiB LDS image of the frame's
+// detections made them wait for a CU of their own).
+//   det_prep_kernel  once per frame: the renormalised detection rows (thread pair
+//                    2j, 2j + 1 = the halves of row j; the same double
+//                    sum-of-squares and f32 divide as cost_kernel, so every B
+//                    fragment is bit-identical) and their box / conf / KF terms,
+//                    into the workspace
+//   cost3_kernel     one wave per track row: its <=30x128 bank is read from HBM
+//                    once into registers; the 32-detection tiles' B fragments come
+//                    from the workspace (L2-resident), the next tile's prefetched
+//                    while the MFMA chain runs.  MFMA chain, top-k and epilogue are
+//                    cost_kernel's: identical outputs.
+// HBM bytes per launch: the live banks (M x T x 512 B) + the detections twice
+// (N x 512 B) + the cost rows, against cost_kernel's bank read per 32-column tile.
+struct Cost3Work {
+  float* dn;       // [F][Nmax][D] renormalised detections
+  DetTerms* dt;    // [F][Nmax]
+  unsigned long long* prof;  // trk_cost_set_prof (diagnostics): per wave [start, bank, chain+top-k, epilogue]
+};
+__device__ __forceinline__ unsigned long long c3_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+inline Cost3Work cost3_work(void* work, int64_t F, int64_t Nmax) {
+  Cost3Work w;
+  w.dn = reinterpret_cast<float*>(work);
+  w.dt = reinterpret_cast<DetTerms*>(reinterpret_cast<unsigned char*>(work) + (size_t)F * Nmax * D * 4);
+  w.prof = nullptr;
+  return w;
+}
+
+__global__ void __launch_bounds__(256) det_prep_kernel(const CostArgs A, Cost3Work w) {
+  const int f = blockIdx.y;
+  const int N = A.dev_N ? min(A.dev_N[f], A.Nmax) : A.N[f];
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  const int j = q >> 1, h = q & 1;
+  if (j >= N) return;  // both threads of a pair leave together (N is per frame)
+  float b[64];
+  load_a_frag(A.det_emb + ((int64_t)f * A.Nmax + j) * D + 64 * h, true, b);
+  double ss = 0.0;
+#pragma unroll
+  for (int s = 0; s < 64; ++s) ss += (double)b[s] * (double)b[s];
+  ss += __shfl_xor(ss, 1);
+  const float nrm = (float)sqrt(ss) + 1e-12f;
+  float* o = w.dn + ((int64_t)f * A.Nmax + j) * D + 64 * h;
+#pragma unroll
+  for (int s = 0; s < 64; s += 4)
+    *reinterpret_cast<float4*>(o + s) = make_float4(b[s] / nrm, b[s + 1] / nrm, b[s + 2] / nrm, b[s + 3] / nrm);
+  if (h == 0) {
+    DetTerms t;
+    det_terms(A.dbox + ((int64_t)f * A.Nmax + j) * 4, A.conf_cur[(int64_t)f * A.Nmax + j], t.ccx, t.ccy, t.Ac, t.ccv,
+              t.z0, t.z1, t.z2, t.z3);
+    w.dt[(int64_t)f * A.Nmax + j] = t;
+  }
+}
+
+// B fragment of detection row j (columns past N read row N - 1: their sims are
+// never stored, and an unconditional load keeps the compiler's vmcnt counting exact
+// so the next tile's loads stay in flight across the current MFMA chain)
+__device__ __forceinline__ void load_b_tile(const float* dnf, int j, int N, int h, float (&b)[64]) {
+  const float* p = dnf + (int64_t)min(j, N - 1) * D + 64 * h;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
+    b[4 * q + 0] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const Cost3Work w) {
+  const int f = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // track terms below: scalar loads
+  const int M = A.dev_M ? min(A.dev_M[f], A.Mmax) : A.M[f];
+  const int N = A.dev_N ? min(A.dev_N[f], A.Nmax) : A.N[f];
+  const int i = blockIdx.x * 4 + wave;
+  if (i >= M || N == 0) return;  // no barriers below
+  const int col = lane & 31, h = lane >> 5;
+  const int64_t slot = A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.rs_ld + i] : (int64_t)f * A.Mmax + i;
+  const int T = min(A.bank_len[slot], A.Tmax);
+  unsigned long long p0 = 0, p1 = 0, pc = 0, pe = 0, pt = 0;
+  if (w.prof) p0 = c3_stamp();
+  float a[64];
+  load_a_frag(A.bank + (slot * A.Tmax + col) * D + 64 * h, col < T, a);
+  if (w.prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    p1 = pt = c3_stamp();
+  }
+  const int topk = A.p.topk;
+  const bool gate = A.p.gate && A.gate_on[slot];
+  // the track's box / conf / gate terms, hoisted out of the tile loop into scalar
+  // registers (wave-uniform; readfirstlane tells the compiler so)
+  auto uni_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+  auto uni_d = [](double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  };
+  float tb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tb[q] = uni_f(A.pbox[slot * 4 + q]);
+  const float tconf = uni_f(A.conf_prev[slot]);
+  double tg[4] = {0.0, 0.0, 0.0, 0.0}, tS[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) tS[q] = 0.0;
+  if (gate) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tg[q] = uni_d(A.gmean[slot * 4 + q]);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tS[q] = uni_d(A.gsinv[slot * 16 + q]);
+  }
+  const float* dnf = w.dn + (int64_t)f * A.Nmax * D;
+  const DetTerms* dtf = w.dt + (int64_t)f * A.Nmax;
+  float* Ct = A.C_total ? A.C_total + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
+  float* Ca = A.C_app ? A.C_app + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
+  // one 32-detection tile, straight-line: the tile's detection terms are loaded first,
+  // then the next tile's B fragments (into the other buffer), then the MFMA chain, so
+  // the epilogue's wait for the terms leaves the prefetch in flight
+  auto tile = [&](int j0, const float (&b)[64], float (&bn)[64]) {
+    const int j = j0 + col;
+    const DetTerms t = dtf[min(j, N - 1)];
+    load_b_tile(dnf, j + 32, N, h, bn);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
+    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    float tk[kMaxTopk];
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
+      topk_insert(tk, tr < T ? acc[r] : -INFINITY);
+    }
+    float other[kMaxTopk];
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) other[q] = __shfl_xor(tk[q], 32);
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q) topk_insert(tk, other[q]);
+    const int k = min(topk, T);
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < kMaxTopk; ++q)
+      if (q < k) sum = sum + tk[q];
+    const float app = k <= 0 ? 1.0f : 1.0f - sum / (float)k;
+    if (w.prof) {
+      asm volatile("" ::"v"(app));
+      const unsigned long long t1 = c3_stamp();
+      pc += t1 - pt;
+      pt = t1;
+    }
+    float cen, scl, cf;
+    const float tot = combine(A.p, app, tb, tconf, t.ccx, t.ccy, t.Ac, t.ccv, gate, tg, tS, t.z0, t.z1, t.z2, t.z3,
+                              cen, scl, cf);
+    if (h == 0 && j < N) {
+      if (Ct) Ct[j] = tot;
+      if (Ca) Ca[j] = app;
+    }
+  };
+  float b0[64], b1[64];
+  load_b_tile(dnf, col, N, h, b0);
+  for (int j0 = 0; j0 < N; j0 += 64) {
+    tile(j0, b0, b1);
+    if (j0 + 32 >= N) break;
+    tile(j0 + 32, b1, b0);
+  }
+  if (w.prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t1 = c3_stamp();
+    pe = t1 - p1 - pc;
+    if (lane == 0) {
+      unsigned long long* o = w.prof + ((int64_t)(f * gridDim.x + blockIdx.x) * 4 + wave) * 4;
+      o[0] = p0; o[1] = p1 - p0; o[2] = pc; o[3] = pe;
+    }
+  }
+}
+
 // C_app given (costCard.cal_cost API): elementwise combine over [M, N].
 __global__ void __launch_bounds__(256)
 combine_kernel(int M, int N, const float* __restrict__ C_app, const float* __restrict__ pbox,
@@ -470,12 +656,18 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
   return TRK_OK;
 }
 
+extern "C" int64_t trk_cost_work_bytes(int64_t F, int64_t Nmax) {
+  if (F <= 0 || Nmax <= 0) return 0;
+  return F * Nmax * (int64_t)(D * 4 + sizeof(DetTerms));
+}
+
 extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* dev_M, const int32_t* dev_N,
                                   const int32_t* row_slot, int64_t rs_ld, int64_t Tmax, const float* bank,
                                   const int32_t* bank_len, const float* pbox, const float* conf_prev,
                                   const double* gmean, const double* gsinv, const int32_t* gate_on,
                                   const float* det_emb, const float* dbox, const float* conf_cur,
-                                  const trk_cost_params* host_params, float* C_total, float* C_app, void* stream) {
+                                  const trk_cost_params* host_params, float* C_total, float* C_app, void* work,
+                                  void* stream) {
   TRK_REQUIRE(F >= 0 && Mmax >= 0 && Nmax >= 0, "build_cost_dev: negative shape");
   TRK_REQUIRE(host_params, "build_cost_dev: null params");
   TRK_REQUIRE(Tmax >= 1 && Tmax <= 32, "build_cost_dev: Tmax (hist_max) must be in [1, 32], got %lld",
@@ -505,9 +697,28 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
     a.C_total = C_total ? C_total + co : nullptr;
     a.C_app = C_app ? C_app + co : nullptr;
     a.p = *host_params;
+    if (work && !g_cost_v2) {
+      // the workspace holds all F frames; this chunk's rows start at frame f0
+      Cost3Work w = cost3_work(work, F, Nmax);
+      w.prof = g_cost_prof ? g_cost_prof + f0 * ((Mmax + 3) / 4) * 16 : nullptr;
+      w.dn += f0 * Nmax * D;
+      w.dt += f0 * Nmax;
+      hipLaunchKernelGGL(det_prep_kernel, dim3((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf), dim3(256), 0, st, a, w);
+      if (int e = trk::check_launch("det_prep_kernel")) return e;
+      hipLaunchKernelGGL(cost3_kernel, dim3((unsigned)((Mmax + 3) / 4), (unsigned)nf), dim3(256), 0, st, a, w);
+      if (int e = trk::check_launch("cost3_kernel")) return e;
+      continue;
+    }
     dim3 grid((unsigned)((Nmax + 31) / 32), (unsigned)((Mmax + kRowsPerWG - 1) / kRowsPerWG), (unsigned)nf);
     hipLaunchKernelGGL(cost_kernel, grid, dim3(256), 0, st, a);
     if (int e = trk::check_launch("cost_kernel")) return e;
   }
+  return TRK_OK;
+}
+
+// diagnostics: cost3 per-wave s_memtime breakdown [start, bank load, MFMA chain +
+// top-k, epilogue] (u64 x 4 per wave, 4 waves per (frame, row block)); NULL = off
+extern "C" int trk_cost_set_prof(unsigned long long* buf) {
+  g_cost_prof = buf;
   return TRK_OK;
 }

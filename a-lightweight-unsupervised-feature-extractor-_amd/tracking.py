@@ -261,6 +261,7 @@ class MultiStreamTracker:
                            count=torch.empty(S, device=dev, dtype=torch.int32),
                            assign=torch.empty((S, cap), device=dev, dtype=torch.int32)) for _ in range(2)]
         self._C = [torch.empty(S * cap * Nm, device=dev, dtype=torch.float32) for _ in range(2)]
+        self._cost_work = torch.empty(int(lib().trk_cost_work_bytes(S, Nm)), device=dev, dtype=torch.uint8)
         self._pool = []  # result buffers of the old layout
         t = self.table
         self._state = StepState(*[_ptr(getattr(t, n)) if hasattr(t, n) and n not in self._scr else
@@ -367,7 +368,8 @@ class MultiStreamTracker:
         check(L.trk_build_cost_dev(S, Mb, Nm, _ptr(sc["m1"]), _ptr(sc["ndet"]), _ptr(sc["row1"]), self.cap, self.T,
                                    _ptr(t.bank), _ptr(t.bank_len), _ptr(t.pbox), _ptr(t.last_conf), _ptr(t.gmean),
                                    _ptr(t.gsinv), _ptr(t.gate_on), _ptr(det_emb), _ptr(dbox), _ptr(dconf),
-                                   p(self.params), _ptr(C1), None, stream), "build_cost (stage 1)")
+                                   p(self.params), _ptr(C1), None, _ptr(self._cost_work), stream),
+              "build_cost (stage 1)")
         check(L.trk_lsap_dev(S, _ptr(C1), TRK_F32, Nm, Mb * Nm, _ptr(sc["m1"]), _ptr(sc["ndet"]), Mb, Nm,
                              min(self.cap, Nm), _ptr(l1["rows"]), _ptr(l1["cols"]), _ptr(l1["count"]),
                              _ptr(sc["lsap_status"][0]), _ptr(l1["assign"]), Mb, float(self.cfg["cost_max"]), stream),
@@ -377,7 +379,7 @@ class MultiStreamTracker:
         check(L.trk_build_cost_dev(S, Mb, Nm, _ptr(sc["m2"]), _ptr(sc["n2"]), _ptr(sc["row2"]), self.cap, self.T,
                                    _ptr(t.bank), _ptr(t.bank_len), _ptr(t.pbox), _ptr(t.last_conf), None, None, None,
                                    _ptr(sc["e2"]), _ptr(sc["b2"]), _ptr(sc["c2"]), p(self.params_nogate), None,
-                                   _ptr(C2), stream), "build_cost (stage 2)")
+                                   _ptr(C2), _ptr(self._cost_work), stream), "build_cost (stage 2)")
         check(L.trk_lsap_dev(S, _ptr(C2), TRK_F32, Nm, Mb * Nm, _ptr(sc["m2"]), _ptr(sc["n2"]), Mb, Nm,
                              min(self.cap, Nm), _ptr(l2["rows"]), _ptr(l2["cols"]), _ptr(l2["count"]),
                              _ptr(sc["lsap_status"][1]), _ptr(l2["assign"]), Mb,

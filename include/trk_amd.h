@@ -156,6 +156,8 @@ int trk_lsap_set_prof(unsigned long long* buf);
 /* diagnostics: per-workgroup timestamps of the 256x256 encoder GEMM (enc_gemm=2);
  * buf >= 16 u64 per workgroup, NULL = off */
 int trk_enc_set_prof(unsigned long long* buf);
+/* diagnostics: per-wave timestamps of the bank-resident cost kernel; NULL = off */
+int trk_cost_set_prof(unsigned long long* buf);
 
 /* ------------------------------------------------------------------------
  * Encoder helpers (the non-GEMM parts of encoderAndHead.Model's eval graph,
@@ -351,13 +353,16 @@ int trk_step_apply(const trk_step_state* st, const trk_step_config* cfg, const f
  * (dev_M / dev_N, dev_nr / dev_nc); Mmax / nr_bound / nc_bound are host upper
  * bounds that size the launch (a larger device size is an error: status -4 for
  * the solver, rows past Mmax are not computed by the cost).  row_slot has row
- * stride rs_ld. */
+ * stride rs_ld.  work: device scratch of trk_cost_work_bytes(F, Nmax) bytes, 16-B
+ * aligned (the renormalised detections; the bank then is read once per launch
+ * instead of once per 32-detection tile), or NULL. */
+int64_t trk_cost_work_bytes(int64_t F, int64_t Nmax);
 int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* dev_M, const int32_t* dev_N,
                        const int32_t* row_slot, int64_t rs_ld, int64_t Tmax, const float* bank,
                        const int32_t* bank_len, const float* pbox, const float* conf_prev, const double* gmean,
                        const double* gsinv, const int32_t* gate_on, const float* det_emb, const float* dbox,
                        const float* conf_cur, const trk_cost_params* host_params, float* C_total, float* C_app,
-                       void* stream);
+                       void* work, void* stream);
 int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stride, const int32_t* dev_nr,
                  const int32_t* dev_nc, int64_t nr_bound, int64_t nc_bound, int64_t kmax, int64_t* rows,
                  int64_t* cols, int32_t* count, int32_t* status, int32_t* assign, int64_t nr_max, double cost_max,

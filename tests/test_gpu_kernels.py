@@ -245,6 +245,67 @@ def test_cost_batched_frames_with_row_slots(trk, oracle, gpu):
         assert np.max(np.abs(out["C_total"][f, :M, :N].cpu().numpy() - exp["C_total"])) <= 2e-6
 
 
+def test_cost_dev_bank_resident_vs_det_tile(trk, oracle, gpu):
+    """trk_build_cost_dev with a workspace (det_prep + cost3: the bank read once
+    per launch) against the same call without one (cost_kernel): bit-identical,
+    and against the oracle; ragged N (not a multiple of 32), row slots, gate on,
+    device-side sizes, an empty frame."""
+    import ctypes
+    from importlib import import_module
+    ops = import_module(trk.__name__ + ".ops")
+    rng = np.random.default_rng(23)
+    F, Mmax, Nmax, S, T = 3, 40, 70, 200, 30
+    bank = _renorm(rng.standard_normal((S, T, 128)))
+    blen = rng.integers(0, 31, S).astype(np.int32)
+    bank[np.arange(T)[None, :] >= blen[:, None]] = 0
+    pbox = _boxes(rng, S)
+    lconf = rng.uniform(0.3, 1, S).astype(np.float32)
+    x = np.zeros((S, 8)); x[:, :4] = np.stack([(pbox[:, 0] + pbox[:, 2]) / 2, (pbox[:, 1] + pbox[:, 3]) / 2,
+                                               (pbox[:, 2] - pbox[:, 0]) / (pbox[:, 3] - pbox[:, 1]),
+                                               pbox[:, 3] - pbox[:, 1]], 1)
+    gm, gs = oracle.gate_params(x, np.tile(np.diag([10., 10, 10, 10, 1000, 1000, 1000, 1000]), (S, 1, 1)))
+    gate_on = (rng.random(S) < 0.8).astype(np.int32)
+    Ms, Ns = np.array([40, 17, 0], np.int32), np.array([70, 5, 9], np.int32)
+    slots = np.stack([rng.permutation(S)[:Mmax] for _ in range(F)]).astype(np.int32)
+    det = rng.standard_normal((F, Nmax, 128)).astype(np.float32)   # not normalised: the kernel renormalises
+    dbox = np.stack([_boxes(rng, Nmax) for _ in range(F)])
+    dconf = rng.uniform(0.3, 1, (F, Nmax)).astype(np.float32)
+    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(gpu, dt)
+    dev = dict(bank=t(bank), blen=t(blen, torch.int32), pbox=t(pbox), lconf=t(lconf), gm=t(gm, torch.float64),
+               gs=t(gs, torch.float64), gon=t(gate_on, torch.int32), det=t(det), dbox=t(dbox), dconf=t(dconf),
+               M=t(Ms, torch.int32), N=t(Ns, torch.int32), slots=t(slots, torch.int32))
+    L = trk.lib()
+    params = trk.default_cost_params(gate=True)
+    P = ops._ptr
+
+    def run(work):
+        Ct = torch.full((F, Mmax, Nmax), -7.0, device=gpu)
+        Ca = torch.full((F, Mmax, Nmax), -7.0, device=gpu)
+        rc = L.trk_build_cost_dev(F, Mmax, Nmax, P(dev["M"]), P(dev["N"]), P(dev["slots"]), Mmax, T, P(dev["bank"]),
+                                  P(dev["blen"]), P(dev["pbox"]), P(dev["lconf"]), P(dev["gm"]), P(dev["gs"]),
+                                  P(dev["gon"]), P(dev["det"]), P(dev["dbox"]), P(dev["dconf"]), ctypes.byref(params),
+                                  P(Ct), P(Ca), P(work), ops._stream(gpu))
+        assert rc == 0
+        torch.cuda.synchronize()
+        return Ct.cpu().numpy(), Ca.cpu().numpy()
+
+    work = torch.empty(int(L.trk_cost_work_bytes(F, Nmax)), device=gpu, dtype=torch.uint8)
+    Ct3, Ca3 = run(work)
+    Ct1, Ca1 = run(None)
+    assert np.array_equal(Ct3, Ct1) and np.array_equal(Ca3, Ca1)
+    for f in range(F):
+        M, N = int(Ms[f]), int(Ns[f])
+        assert (Ct3[f, M:] == -7.0).all() and (Ct3[f, :, N:] == -7.0).all()  # nothing written outside M x N
+        if M == 0:
+            continue
+        s = slots[f, :M]
+        exp = oracle.cost_build(bank[s], blen[s], det[f, :N], pbox[s], dbox[f, :N], lconf[s], dconf[f, :N],
+                                gm[s], gs[s], gate_on[s])
+        assert np.max(np.abs(Ca3[f, :M, :N] - exp["C_app"])) <= 2e-6
+        assert np.array_equal(Ct3[f, :M, :N] >= 1e9, exp["C_total"] >= 1e9)
+        assert np.max(np.abs(Ct3[f, :M, :N] - exp["C_total"])) <= 2e-6
+
+
 def test_costcard_api_vs_reference_golden(trk, gpu):
     d = np.load(os.path.join(GOLDEN, "costcard_golden.npz"))
     for tag in "abc":
