@@ -1619,7 +1619,11 @@ __device__ __forceinline__ unsigned long long g8_stamp() {
 // PROF (trk_enc_set_prof, diagnostics only): waves 0 and 4 of each workgroup record
 // [start, prologue done, K loop done, end, sum of the per-step vmcnt waits, sum of
 // the per-step barrier waits, hw id, 0] at prof[(wg * 2 + wave / 4) * 8]
-template <int EPI, bool PROF>
+// MF = 0: v_mfma_f32_16x16x32_bf16, wave tile 8 x 4 MFMA tiles; MF = 1:
+// v_mfma_f32_32x32x16_bf16, 4 x 2 tiles (half the MFMA instructions; at two waves
+// per SIMD a 32x32x16 retires 33 % more flops per cycle than two 16x16x32 --
+// tools/exp/clock_probe.hip).  Same LDS images and fragment bytes.
+template <int EPI, bool PROF, int MF>
 __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntiles, unsigned long long* prof) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint4* bufs = reinterpret_cast<uint4*>(smem);                // [2][A 2048 | B 2048] uint4
@@ -1698,13 +1702,23 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
     }
   };
 
-  f4v acc[8][4];
+  typename std::conditional<MF == 0, f4v[8][4], f16_t[4][2]>::type acc;
+  if constexpr (MF == 0) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][t][e] = 0.f;
+  }
 
   const int fr = lane & 15, fc = lane >> 4;
+  const int f32r = lane & 31, f32h = lane >> 5;
   unsigned long long p_t0 = 0, p_t1 = 0, p_t2 = 0, p_w = 0, p_b = 0;
   if constexpr (PROF) p_t0 = g8_stamp();
   issue(0);
@@ -1721,30 +1735,55 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
     const uint4* ab = bufs + (kt & 1) * (2 * G8_POS);
     const uint4* bb = ab + G8_POS;
     uint4* dn = bufs + ((kt + 1) & 1) * (2 * G8_POS) + wave * 64;
-    auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 7) * 16 + fr, (s >> 3) * 4 + fc)); };
-    bf8v bfr[2][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bfr[0][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, fc));
-    bf8v afr = rd_a(0);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int h = s >> 3, i = s & 7;
-      bf8v anext = afr;
-      if (s < 15) anext = rd_a(s + 1);
-      if (s == 4) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bfr[1][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, 4 + fc));
+    auto issue_piece = [&](int q) {  // piece q: A slots q*512.. (q < 4), B slots (q - 4)*512..
+      if (q < 4)
+        __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + (kt + 1) * G8_BK), LPTR(dn + q * 512), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(GPTR(bsrc[q - 4] + (kt + 1) * G8_BK), LPTR(dn + G8_POS + (q - 4) * 512), 16, 0, 0);
+    };
+    if constexpr (MF == 0) {
+      auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 7) * 16 + fr, (s >> 3) * 4 + fc)); };
+      bf8v bfr[2][4];
+  #pragma unroll
+      for (int t = 0; t < 4; ++t) bfr[0][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, fc));
+      bf8v afr = rd_a(0);
+  #pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int h = s >> 3, i = s & 7;
+        bf8v anext = afr;
+        if (s < 15) anext = rd_a(s + 1);
+        if (s == 4) {
+  #pragma unroll
+          for (int t = 0; t < 4; ++t) bfr[1][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, 4 + fc));
+        }
+  #pragma unroll
+        for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[h][t], acc[i][t], 0, 0, 0);
+        if (pf && (s & 1)) issue_piece(s >> 1);
+        afr = anext;
       }
+    } else {
+      // 16 groups s = (k step ks = s >> 2, row tile i = s & 3), 2 MFMAs each; lane (r, h)
+      // reads 16 B of row r at chunk 2 ks + h
+      auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 3) * 32 + f32r, (s >> 2) * 2 + f32h)); };
+      auto rd_b = [&](int ks, int t) { return *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 32 + f32r, ks * 2 + f32h)); };
+      bf8v bfr[2][2];
+      bfr[0][0] = rd_b(0, 0);
+      bfr[0][1] = rd_b(0, 1);
+      bf8v afr = rd_a(0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[h][t], acc[i][t], 0, 0, 0);
-      if (pf && (s & 1)) {
-        const int q = s >> 1;  // piece q: A slots q*512.. (q < 4), B slots (q - 4)*512..
-        if (q < 4)
-          __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + (kt + 1) * G8_BK), LPTR(dn + q * 512), 16, 0, 0);
-        else
-          __builtin_amdgcn_global_load_lds(GPTR(bsrc[q - 4] + (kt + 1) * G8_BK), LPTR(dn + G8_POS + (q - 4) * 512), 16, 0, 0);
+      for (int s = 0; s < 16; ++s) {
+        const int ks = s >> 2, i = s & 3;
+        bf8v anext = afr;
+        if (s < 15) anext = rd_a(s + 1);
+        if (i == 1 && ks < 3) {
+          bfr[(ks + 1) & 1][0] = rd_b(ks + 1, 0);
+          bfr[(ks + 1) & 1][1] = rd_b(ks + 1, 1);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[ks & 1][t], acc[i][t], 0, 0, 0);
+        if (pf && (s & 1)) issue_piece(s >> 1);
+        afr = anext;
       }
-      afr = anext;
     }
     unsigned long long pa = 0, pb = 0;
     if constexpr (PROF) pa = g8_stamp();
@@ -1771,48 +1810,96 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
     const int64_t roi0 = r0 / P;
     const int nxt = P - (int)(r0 - roi0 * P);   // first row (within the 128) of ROI roi0 + 1
     const bool full = r0 + 128 <= (int64_t)a.M;
-    float bias4[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bias4[t] = a.bias[n0 + wc * 64 + t * 16 + fr];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float sm[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        f4v v = acc[i][t];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e] + bias4[t]);
-        const int lo = i * 16;
-        if (full && lo + 16 <= nxt) {
-          sm[0] += (v[0] + v[1]) + (v[2] + v[3]);
-        } else if (full && lo >= nxt && lo + 16 <= nxt + P) {
-          sm[1] += (v[0] + v[1]) + (v[2] + v[3]);
-        } else if (full && lo >= nxt + P) {
-          sm[2] += (v[0] + v[1]) + (v[2] + v[3]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int ro = lo + fc * 4 + e;
-            const float x = (r0 + ro < a.M) ? v[e] : 0.f;
-            sm[0] += ro < nxt ? x : 0.f;
-            sm[1] += (ro >= nxt && ro < nxt + P) ? x : 0.f;
-            sm[2] += ro >= nxt + P ? x : 0.f;
+    const int64_t last = min(r0 + 128, (int64_t)a.M) - 1;
+    const int nslot = (int)(last / P - roi0) + 1;
+    const int64_t th = r0 / kPartRows;
+    if constexpr (MF == 0) {
+      float bias4[4];
+  #pragma unroll
+      for (int t = 0; t < 4; ++t) bias4[t] = a.bias[n0 + wc * 64 + t * 16 + fr];
+  #pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float sm[3] = {0.f, 0.f, 0.f};
+  #pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          f4v v = acc[i][t];
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e] + bias4[t]);
+          const int lo = i * 16;
+          if (full && lo + 16 <= nxt) {
+            sm[0] += (v[0] + v[1]) + (v[2] + v[3]);
+          } else if (full && lo >= nxt && lo + 16 <= nxt + P) {
+            sm[1] += (v[0] + v[1]) + (v[2] + v[3]);
+          } else if (full && lo >= nxt + P) {
+            sm[2] += (v[0] + v[1]) + (v[2] + v[3]);
+          } else {
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int ro = lo + fc * 4 + e;
+              const float x = (r0 + ro < a.M) ? v[e] : 0.f;
+              sm[0] += ro < nxt ? x : 0.f;
+              sm[1] += (ro >= nxt && ro < nxt + P) ? x : 0.f;
+              sm[2] += ro >= nxt + P ? x : 0.f;
+            }
+          }
+        }
+  #pragma unroll
+        for (int q = 0; q < 3; ++q) sm[q] = sum_xor32(sum_xor16(sm[q]));
+        if (fc == 0) {
+  #pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            if (q < nslot) {
+              const int64_t roi = roi0 + q;
+              const int j = (int)(th - roi * P / kPartRows);
+              a.sums[(roi * kPart + j) * a.ld_sums + (int64_t)g * a.N + n0 + wc * 64 + t * 16 + fr] =
+                  llrintf(sm[q] * kFix);
+            }
           }
         }
       }
+    } else {
+      // 32x32 tiles: lane (c = lane & 31, h) holds rows (r & 3) + 8 (r >> 2) + 4 h of
+      // column c in register r
 #pragma unroll
-      for (int q = 0; q < 3; ++q) sm[q] = sum_xor32(sum_xor16(sm[q]));
-      if (fc == 0) {
-        const int64_t last = min(r0 + 128, (int64_t)a.M) - 1;
-        const int nslot = (int)(last / P - roi0) + 1;
-        const int64_t th = r0 / kPartRows;
+      for (int t = 0; t < 2; ++t) {
+        const int col = n0 + wc * 64 + t * 32 + f32r;
+        const float bias = a.bias[col];
+        float sm[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          if (q < nslot) {
-            const int64_t roi = roi0 + q;
-            const int j = (int)(th - roi * P / kPartRows);
-            a.sums[(roi * kPart + j) * a.ld_sums + (int64_t)g * a.N + n0 + wc * 64 + t * 16 + fr] =
-                llrintf(sm[q] * kFix);
+        for (int i = 0; i < 4; ++i) {
+          f16_t v = acc[i][t];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) v[e] = silu_f(v[e] + bias);
+          const int lo = i * 32;
+          if (full && (lo + 32 <= nxt || (lo >= nxt && lo + 32 <= nxt + P) || lo >= nxt + P)) {
+            float x = 0.f;
+#pragma unroll
+            for (int e = 0; e < 16; e += 4) x += (v[e] + v[e + 1]) + (v[e + 2] + v[e + 3]);
+            const int q = lo + 32 <= nxt ? 0 : lo + 32 <= nxt + P ? 1 : 2;
+            sm[0] += q == 0 ? x : 0.f;
+            sm[1] += q == 1 ? x : 0.f;
+            sm[2] += q == 2 ? x : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int ro = lo + (e & 3) + 8 * (e >> 2) + 4 * f32h;
+              const float x = (r0 + ro < a.M) ? v[e] : 0.f;
+              sm[0] += ro < nxt ? x : 0.f;
+              sm[1] += (ro >= nxt && ro < nxt + P) ? x : 0.f;
+              sm[2] += ro >= nxt + P ? x : 0.f;
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) sm[q] = sum_xor32(sm[q]);
+        if (f32h == 0) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            if (q < nslot) {
+              const int64_t roi = roi0 + q;
+              const int j = (int)(th - roi * P / kPartRows);
+              a.sums[(roi * kPart + j) * a.ld_sums + (int64_t)g * a.N + col] = llrintf(sm[q] * kFix);
+            }
           }
         }
       }
@@ -1831,22 +1918,22 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics)
 
-template <int EPI>
+template <int EPI, int MF>
 int launch8(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + G8_BM - 1) / G8_BM * (a.N / G8_BN) * a.groups;
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm8: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, false, MF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, true, MF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
     attr = true;
   }
   if (g_enc_prof)
-    hipLaunchKernelGGL((gemm8_kernel<EPI, true>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, g_enc_prof);
+    hipLaunchKernelGGL((gemm8_kernel<EPI, true, MF>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, g_enc_prof);
   else
-    hipLaunchKernelGGL((gemm8_kernel<EPI, false>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, nullptr);
+    hipLaunchKernelGGL((gemm8_kernel<EPI, false, MF>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, nullptr);
   return trk::check_launch("gemm8_kernel");
 }
 
@@ -1956,7 +2043,8 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  if (g_enc_gemm == 2 && P >= 86 && K % 64 == 0 && kscale % 64 == 0 && kscale <= 512) return launch8<EPI_TRANS>(a, st);
+  if (g_enc_gemm >= 2 && P >= 86 && K % 64 == 0 && kscale % 64 == 0 && kscale <= 512)
+    return g_enc_gemm == 2 ? launch8<EPI_TRANS, 0>(a, st) : launch8<EPI_TRANS, 1>(a, st);
   if (g_enc_gemm >= 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
   return launch<EPI_TRANS, 128, 256>(a, st);
 }

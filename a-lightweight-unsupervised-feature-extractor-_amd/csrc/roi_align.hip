@@ -715,7 +715,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "g1dw_mode")) { extern int g_g1dw_mode; TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 5, "g1dw_mode in {0, 1, 2, 4, 5}"); g_g1dw_mode = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm_dbg")) { extern int g_enc_gemm_dbg; g_enc_gemm_dbg = value; return TRK_OK; }
-  if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value >= 0 && value <= 2, "enc_gemm in {0,1,2}"); g_enc_gemm = value; return TRK_OK; }
+  if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value >= 0 && value <= 3, "enc_gemm in {0,1,2,3}"); g_enc_gemm = value; return TRK_OK; }
   if (!strcmp(key, "dw_fast")) { extern int g_dw_fast; TRK_REQUIRE(value == 0 || value == 1, "dw_fast in {0,1}"); g_dw_fast = value; return TRK_OK; }
   if (!strcmp(key, "lsap_dev_lds_kb")) { extern int g_lsap_dev_lds_kb; TRK_REQUIRE(value >= 8 && value <= 156, "lsap_dev_lds_kb in [8, 156]"); g_lsap_dev_lds_kb = value; return TRK_OK; }
   if (!strcmp(key, "roi_vec")) { TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "roi_vec in {0,1,2,4}"); g_roi_vec = value; return TRK_OK; }

@@ -333,10 +333,12 @@ def build_cost(*, M: Sequence[int], N: Sequence[int], bank: torch.Tensor, bank_l
                gmean: Optional[torch.Tensor] = None, gsinv: Optional[torch.Tensor] = None,
                gate_on: Optional[torch.Tensor] = None, row_slot: Optional[torch.Tensor] = None,
                out: Optional[dict] = None, want=("C_total",)) -> dict:
-    """Batched fused cost (trk_build_cost).  Shapes: det_emb [F, Nmax, 128],
-    dbox [F, Nmax, 4], conf_cur [F, Nmax]; track arrays indexed by slot
-    (bank [S, Tmax, 128] ...), rows mapped through row_slot [F, Mmax] if given,
-    else slot = f*Mmax + i.  Returns {name: [F, Mmax, Nmax] f32}."""
+    """Batched fused cost.  Shapes: det_emb [F, Nmax, 128], dbox [F, Nmax, 4],
+    conf_cur [F, Nmax]; track arrays indexed by slot (bank [S, Tmax, 128] ...),
+    rows mapped through row_slot [F, Mmax] if given, else slot = f*Mmax + i.
+    Returns {name: [F, Mmax, Nmax] f32}.  C_total / C_app only: the bank-resident
+    kernel (trk_build_cost_dev with a workspace); any of C_center / C_scale /
+    C_conf: the det-tile kernel (trk_build_cost).  Bit-identical outputs."""
     _need_gpu(det_emb, "build_cost")
     F, Nmax, D = det_emb.shape
     if D != 128:
@@ -346,6 +348,22 @@ def build_cost(*, M: Sequence[int], N: Sequence[int], bank: torch.Tensor, bank_l
     dev = det_emb.device
     if out is None:
         out = {k: torch.empty((F, Mmax, Nmax), device=dev, dtype=torch.float32) for k in want}
+    if set(out) <= {"C_total", "C_app"} and F > 0 and Mmax > 0 and Nmax > 0:
+        Mi, Ni = [int(m) for m in M], [int(n) for n in N]
+        if len(Mi) != F or len(Ni) != F or any(not 0 <= m <= Mmax for m in Mi) or any(not 0 <= n <= Nmax for n in Ni):
+            raise ValueError("build_cost: frame M/N outside [0, Mmax/Nmax]")
+        if row_slot is None:
+            row_slot = torch.arange(F * Mmax, device=dev, dtype=torch.int32).view(F, Mmax)
+        dM = torch.tensor(Mi, dtype=torch.int32).to(dev, non_blocking=True)
+        dN = torch.tensor(Ni, dtype=torch.int32).to(dev, non_blocking=True)
+        work = torch.empty(int(lib().trk_cost_work_bytes(F, Nmax)), device=dev, dtype=torch.uint8)
+        rc = lib().trk_build_cost_dev(F, Mmax, Nmax, _ptr(dM), _ptr(dN), _ptr(row_slot), row_slot.shape[1], Tmax,
+                                      _ptr(bank), _ptr(bank_len), _ptr(pbox), _ptr(conf_prev), _ptr(gmean),
+                                      _ptr(gsinv), _ptr(gate_on), _ptr(det_emb), _ptr(dbox), _ptr(conf_cur),
+                                      ctypes.byref(params), _ptr(out.get("C_total")), _ptr(out.get("C_app")),
+                                      _ptr(work), _stream(dev))
+        check(rc, "build_cost")
+        return out
     hM = (ctypes.c_int32 * max(F, 1))(*[int(m) for m in M])
     hN = (ctypes.c_int32 * max(F, 1))(*[int(n) for n in N])
     rc = lib().trk_build_cost(F, Mmax, Nmax, hM, hN, _ptr(row_slot), Tmax, _ptr(bank), _ptr(bank_len),

@@ -157,7 +157,16 @@ def _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf, gate=
                          gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
                          gate_on=t(np.ones(M, np.int32), torch.int32),
                          want=("C_total", "C_app", "C_center", "C_scale", "C_conf"))
-    return {k: v[0].cpu().numpy() for k, v in out.items()}
+    res = {k: v[0].cpu().numpy() for k, v in out.items()}
+    # C_total / C_app only: the bank-resident kernel (det_prep + cost3), bit-identical
+    out3 = trk.build_cost(M=[M], N=[N], bank=t(_renorm(bank)), bank_len=t(blen, torch.int32), pbox=t(pbox),
+                          conf_prev=t(lconf), det_emb=t(det[None]), dbox=t(dbox[None]),
+                          conf_cur=t(dconf[None]), params=trk.default_cost_params(gate=gate),
+                          gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
+                          gate_on=t(np.ones(M, np.int32), torch.int32), want=("C_total", "C_app"))
+    for k in ("C_total", "C_app"):
+        assert np.array_equal(out3[k][0].cpu().numpy(), res[k]), k
+    return res
 
 
 @pytest.mark.parametrize("name", ["s16", "s64", "reid"])
@@ -462,17 +471,18 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     assert (st0 - st).abs().max().item() <= 1e-3 * st.abs().max().item()
     st2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
     assert torch.equal(st, st2)
-    # the 256 x 256 / BK 64 kernel (enc_gemm 2; P >= 86): same math, another f32 summation order
-    if P >= 86:
+    # the 256 x 256 / BK 64 kernels (enc_gemm 2: 16x16x32 MFMA, 3: 32x32x16; P >= 86):
+    # same math, another f32 summation order
+    for mode in ((2, 3) if P >= 86 else ()):
         try:
-            assert L.trk_set_tuning(b"enc_gemm", 2) == 0
+            assert L.trk_set_tuning(b"enc_gemm", mode) == 0
             st8 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
             st8b = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
         finally:
             assert L.trk_set_tuning(b"enc_gemm", 1) == 0
-        assert (st8 - st).abs().max().item() <= 1e-3 * st.abs().max().item()
-        assert (st8 - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item()
-        assert torch.equal(st8, st8b)
+        assert (st8 - st).abs().max().item() <= 1e-3 * st.abs().max().item(), mode
+        assert (st8 - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item(), mode
+        assert torch.equal(st8, st8b), mode
     # plain GEMM (the first 1x1 convs), strided A rows
     W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
     A = Y2[:, :512]

@@ -11,7 +11,7 @@ typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 template <int KIND>
 __global__ void __launch_bounds__(256) probe(unsigned long long* out, int iters, float seed) {
   unsigned long long t0, r0, t1, r1;
-  f32x16 acc = {};
+  f32x16 acc = {}, acc2 = {}, acc3 = {}, acc4 = {};
   float a = seed + threadIdx.x, b = seed * 2.f;
   bf8v ab, bb;
   for (int q = 0; q < 8; ++q) { ab[q] = (__bf16)(a + q); bb[q] = (__bf16)(b - q); }
@@ -20,12 +20,22 @@ __global__ void __launch_bounds__(256) probe(unsigned long long* out, int iters,
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       if constexpr (KIND == 0) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bb, acc, 0, 0, 0);
+      else if constexpr (KIND == 1) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bb, acc, 0, 0, 0);
+      else if constexpr (KIND == 2) {  // 4 independent accumulators
+        if ((u & 3) == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bb, acc, 0, 0, 0);
+        if ((u & 3) == 1) acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bb, acc2, 0, 0, 0);
+        if ((u & 3) == 2) acc3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bb, acc3, 0, 0, 0);
+        if ((u & 3) == 3) acc4 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, bb, acc4, 0, 0, 0);
+      } else {  // 4 independent 16x16x32 accumulators (4 regs each)
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        f4* p = reinterpret_cast<f4*>(&acc);
+        p[u & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, p[u & 3], 0, 0, 0);
+      }
     }
   }
   asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1)::"memory");
   float s = 0.f;
-  for (int q = 0; q < 16; ++q) s += acc[q];
+  for (int q = 0; q < 16; ++q) s += acc[q] + acc2[q] + acc3[q] + acc4[q];
   if ((threadIdx.x & 63) == 0) {
     unsigned long long* o = out + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
     o[0] = t1 - t0; o[1] = r1 - r0; o[2] = (unsigned long long)(s != 12345.f); o[3] = 0;
@@ -40,11 +50,13 @@ int main() {
   hipMalloc(&d, (size_t)maxwg * 4 * 4 * 8);
   std::vector<unsigned long long> h((size_t)maxwg * 16);
   const int iters = 4000;
-  for (int kind = 0; kind < 2; ++kind)
+  for (int kind = 0; kind < 4; ++kind)
     for (int wg : {1, ncu, 2 * ncu}) {
       for (int rep = 0; rep < 2; ++rep) {
         if (kind == 0) hipLaunchKernelGGL(probe<0>, dim3(wg), dim3(256), 0, 0, d, iters, 1.f);
-        else hipLaunchKernelGGL(probe<1>, dim3(wg), dim3(256), 0, 0, d, iters, 1.f);
+        else if (kind == 1) hipLaunchKernelGGL(probe<1>, dim3(wg), dim3(256), 0, 0, d, iters, 1.f);
+        else if (kind == 2) hipLaunchKernelGGL(probe<2>, dim3(wg), dim3(256), 0, 0, d, iters, 1.f);
+        else hipLaunchKernelGGL(probe<3>, dim3(wg), dim3(256), 0, 0, d, iters, 1.f);
         hipDeviceSynchronize();
       }
       hipMemcpy(h.data(), d, (size_t)wg * 16 * 8, hipMemcpyDeviceToHost);
@@ -52,12 +64,11 @@ int main() {
       for (int w = 0; w < wg * 4; ++w) { tk += h[w * 4]; rt += h[w * 4 + 1]; }
       tk /= wg * 4; rt /= wg * 4;
       const double n = (double)iters * 16;
-      const double cyc = kind == 0 ? 64.0 : 32.0;   // per-SIMD issue cycles per MFMA (guide)
-      const double waves_per_simd = wg <= ncu ? 1.0 : 2.0;
-      printf("{\"mfma\": \"%s\", \"workgroups\": %d, \"ticks_per_mfma\": %.2f, \"realtime_us\": %.1f, "
-             "\"tick_GHz\": %.3f, \"clock_GHz_if_busy\": %.3f}\n",
-             kind == 0 ? "f32_32x32x2" : "bf16_32x32x16", wg, tk / n, rt / 100.0, tk / (rt * 10.0),
-             n * cyc * waves_per_simd / (rt * 10.0) / 1e3);
+      const char* nm[4] = {"f32_32x32x2 chain", "bf16_32x32x16 chain", "bf16_32x32x16 x4 acc", "bf16_16x16x32 x4 acc"};
+      const double flop = kind == 0 ? 4096.0 : kind == 3 ? 16384.0 : 32768.0;
+      printf("{\"mfma\": \"%s\", \"workgroups\": %d, \"ticks_per_mfma_per_wave\": %.2f, \"realtime_us\": %.1f, "
+             "\"tick_GHz\": %.3f, \"chip_TFLOPs\": %.1f}\n",
+             nm[kind], wg, tk / n, rt / 100.0, tk / (rt * 10.0), n * flop * wg * 4 / (rt * 10.0) / 1e6);
     }
   hipFree(d);
   return 0;

@@ -39,7 +39,7 @@ def main():
     print("JSON " + json.dumps(out))
     if len(sys.argv) > 3:  # short-name traffic table for bench.py (profiles/pmc_traffic.json)
         short_names = {"roi_sweep_kernel": "roi_align", "dwconv5_rows2_kernel": "dwconv5",
-                       "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost",
+                       "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost", "cost3_kernel": "cost", "det_prep_kernel": "cost_prep",
                        "enc_gemm_kernel<0": "enc_gemm_dsc", "enc_gemm_kernel<1": "enc_gemm_trans",
                        "enc_gemm_kernel<2": "enc_gemm_plain", "g1dw_kernel": "enc_g1_dwconv",
                        "g1dw_il_kernel": "enc_g1_dwconv", "g1dw_persist_kernel": "enc_g1_dwconv",
