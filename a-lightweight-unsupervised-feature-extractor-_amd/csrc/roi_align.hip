@@ -466,7 +466,7 @@ __device__ __forceinline__ void cache_load(f2_t (&v0)[NH][2], f2_t (&v1)[NH][2],
   }
 }
 
-template <int NH, bool OUT_BF16, int PW>
+template <int NH, bool OUT_BF16, int PW, bool g_sweep_wlds>
 __global__ void __launch_bounds__(256)
 roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
                  int C, int H, int W, const float* __restrict__ rois, float spatial_scale,
@@ -474,8 +474,11 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
   constexpr int CPW = 256 * NH, NS = 2 * PW;
   static_assert(NS <= 64, "one x sample per lane");
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // per-wave sample weight table: [x sample][y sample] = {w1, w2, w3, w4}, read back
+  // with a wave-uniform address (an LDS broadcast instead of four readlanes)
+  __shared__ float4 wtab[4][NS][2];
   const int64_t item = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-  if (item >= nitems) return;  // wave-uniform
+  if (item >= nitems) return;  // wave-uniform (no barriers below)
   const int chunk = (int)(item % nchunks);
   const int64_t t_ = item / nchunks;
   const int ph = (int)(t_ % PH);
@@ -526,6 +529,7 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
     for (int iy = 0; iy < 2; ++iy) {
       wq[iy][0] = yh[iy] * a.h; wq[iy][1] = yh[iy] * a.l;
       wq[iy][2] = yl[iy] * a.h; wq[iy][3] = yl[iy] * a.l;
+      if (g_sweep_wlds && lane < NS) wtab[wave][lane][iy] = make_float4(wq[iy][0], wq[iy][1], wq[iy][2], wq[iy][3]);
     }
   }
 
@@ -588,10 +592,16 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
           }
           k.cb = hi;
         }
-        const float w1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][0]), j));
-        const float w2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][1]), j));
-        const float w3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][2]), j));
-        const float w4 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][3]), j));
+        float w1, w2, w3, w4;
+        if (g_sweep_wlds) {
+          const float4 w = wtab[wave][j][iy];
+          w1 = w.x; w2 = w.y; w3 = w.z; w4 = w.w;
+        } else {
+          w1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][0]), j));
+          w2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][1]), j));
+          w3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][2]), j));
+          w4 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][3]), j));
+        }
         sample4<NH>(t[iy], w1, w2, w3, w4, k.a0, k.b0, k.a1, k.b1);
       } else {
         sample4<NH>(t[iy], 0.f, 0.f, 0.f, 0.f, zero, zero, zero, zero);
@@ -628,6 +638,7 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
 int g_roi_window_kb = 0;   // measured r01: direct L2 taps beat LDS window staging (229 vs 300+ us)
 int g_roi_vec = 0;  // 0 = auto
 int g_roi_sweep = 1;  // NHWC output: row-sweep kernel, 256 (1) or 512 (2) channels per wave
+int g_roi_wlds = 1;   // row sweep: sample weights from an LDS table (1: r02 A/B 97 vs 104 us) or readlanes (0)
 
 template <int VEC, bool OUT_BF16, bool OUT_NHWC>
 int launch_roi(const float* nhwc, int B, int C, int H, int W, const float* rois, int K,
@@ -680,8 +691,12 @@ int launch_sweep(const float* nhwc, int C, int H, int W, const float* rois, int 
     trk::set_error("roi_align: too many workgroups");
     return TRK_EUNSUPPORTED;
   }
-  hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, C, H, W,
-                     rois, scale, PH, aligned, out, nchunks, nitems);
+  if (g_roi_wlds)
+    hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW, true>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, C, H,
+                       W, rois, scale, PH, aligned, out, nchunks, nitems);
+  else
+    hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW, false>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, C, H,
+                       W, rois, scale, PH, aligned, out, nchunks, nitems);
   return trk::check_launch("roi_sweep_kernel");
 }
 
@@ -713,6 +728,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "enc_gemm_offset")) { extern int g_enc_gemm_offset; TRK_REQUIRE(value >= 0 && value <= 64, "enc_gemm_offset in [0, 64]"); g_enc_gemm_offset = value; return TRK_OK; }
   if (!strcmp(key, "g1dw_persist")) { extern int g_g1dw_persist; TRK_REQUIRE(value >= 0 && value <= 66, "g1dw_persist in [0, 66]"); g_g1dw_persist = value; return TRK_OK; }
   if (!strcmp(key, "g1dw_mode")) { extern int g_g1dw_mode; TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 5, "g1dw_mode in {0, 1, 2, 4, 5}"); g_g1dw_mode = value; return TRK_OK; }
+  if (!strcmp(key, "roi_wlds")) { TRK_REQUIRE(value == 0 || value == 1, "roi_wlds in {0, 1}"); g_roi_wlds = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm_dbg")) { extern int g_enc_gemm_dbg; g_enc_gemm_dbg = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value >= 0 && value <= 3, "enc_gemm in {0,1,2,3}"); g_enc_gemm = value; return TRK_OK; }

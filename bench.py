@@ -46,6 +46,10 @@ PREROLL = 30
 
 # ------------------------------------------------------------ workload ----
 MAP_POOL = 16  # frames' maps in the rotating pool: 16 x 26 MB > the 256 MB Infinity Cache
+# map layout the detector hands over: "nhwc" (channels_last, what an NHWC backbone on
+# MI355X emits; roi_align reads it directly) or "nchw" (the reference's YOLOv7 layout;
+# roi_align then transposes each frame's map once, +17 us per 8-stream frame)
+MAP_LAYOUT = os.environ.get("TRK_MAP_LAYOUT", "nhwc")
 
 
 def make_scenes(dev, streams, N, frames, seed, C=512, H=40, pool=MAP_POOL):
@@ -53,12 +57,17 @@ def make_scenes(dev, streams, N, frames, seed, C=512, H=40, pool=MAP_POOL):
     letterboxed frame (rows 280..1000 = a 1080p picture), velocities
     U(-2, 2) px/frame bouncing at the borders, 0.5 px detection jitter,
     conf ~ U(0.55, 0.99); detection order shuffled every frame.  Feature
-    maps: a pool of `pool` frames of [streams, 512, 40, 40] f32 NCHW maps
-    (SiLU(randn)), frame f reads slot f % pool, so every frame's map read comes
-    from HBM, not from a cache that held it since the previous frame."""
+    maps: a pool of `pool` frames of [streams, 512, 40, 40] f32 maps (SiLU(randn);
+    channels_last unless TRK_MAP_LAYOUT=nchw), frame f reads slot f % pool, so every
+    frame's map read comes from HBM, not from a cache that held it since the
+    previous frame."""
     rng = np.random.default_rng(seed)
     g = torch.Generator(device=dev).manual_seed(seed)
     feat = torch.nn.functional.silu(torch.randn((pool, streams, C, H, H), generator=g, device=dev))
+    if MAP_LAYOUT == "nhwc":  # per-frame [streams, C, H, W] slices with channels_last strides
+        feat = feat.permute(0, 1, 3, 4, 2).contiguous().permute(0, 1, 4, 2, 3)
+    elif MAP_LAYOUT != "nchw":
+        raise ValueError(f"TRK_MAP_LAYOUT must be nhwc or nchw, got {MAP_LAYOUT!r}")
     w = rng.uniform(32, 320, (streams, N)); h = rng.uniform(32, 320, (streams, N))
     lo = np.stack([np.zeros_like(w), np.full_like(h, 280.0)], -1)
     hi = np.stack([1280 - w, 1000 - h], -1)
@@ -620,9 +629,11 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16 encoder / f32 roi+cost / f64 KF+LSAP duals",
         "data": "synthetic (SiLU(randn) maps, moving boxes; seeded random encoder weights)",
-        "config": {"workload": f"c3: {Fs} streams x N={N} detections/frame per GPU, [{Fs},512,40,40] maps, "
-                               f"10x10 ROIs, full tracker step (bank T=30, KF, 2-stage assign)",
-                   "streams_per_gpu": Fs, "N": N, "roi": S, "parallelism": f"replicas{world}"},
+        "config": {"workload": f"c3: {Fs} streams x N={N} detections/frame per GPU, [{Fs},512,40,40] "
+                               f"{MAP_LAYOUT.upper()} maps, 10x10 ROIs, full tracker step (bank T=30, KF, "
+                               f"2-stage assign)",
+                   "streams_per_gpu": Fs, "N": N, "roi": S, "map_layout": MAP_LAYOUT,
+                   "parallelism": f"replicas{world}"},
         "roofline": rf, "identity_rate": round(ident, 5),
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,43 @@
+"""ROI Align at the bench shape (8 frames x 256 ROIs, 512x40x40 maps, 10x10
+bins, NHWC bf16 out) under tuning-knob variants, interleaved rounds, median.
+usage: python tools/exp/roi_ab.py "roi_wlds=0" "roi_wlds=1" ..."""
+import importlib, json, os, statistics, sys
+import torch
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
+trk = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd")
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(0)
+F, K = 8, 256
+feat = torch.randn(F, 512, 40, 40, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+xy = torch.rand(F * K, 2, device=dev, generator=g) * 1100
+wh = 20 + torch.rand(F * K, 2, device=dev, generator=g) * 300
+rois = torch.cat([torch.arange(F, device=dev).repeat_interleave(K)[:, None].float(), xy, xy + wh], 1)
+L = trk.lib()
+variants = sys.argv[1:] or ["roi_wlds=0", "roi_wlds=1"]
+
+
+def setv(v, reset=False):
+    for kv in v.split(","):
+        k, x = kv.split("=")
+        L.trk_set_tuning(k.encode(), 0 if reset and k == "roi_wlds" else (1 if reset else int(x)))
+
+
+def run():
+    return trk.roi_align(feat, rois, (10, 10), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+
+
+ref = run()
+res = {v: [] for v in variants}
+for _ in range(8):
+    for v in variants:
+        setv(v)
+        out = run(); torch.cuda.synchronize()
+        assert torch.equal(out, ref), v
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10): run()
+        e1.record(); torch.cuda.synchronize()
+        res[v].append(e0.elapsed_time(e1) / 10 * 1e3)
+        setv(v, reset=True)
+for v in variants:
+    print(json.dumps({"variant": v, "median_us": round(statistics.median(res[v]), 1), "min_us": round(min(res[v]), 1)}))
