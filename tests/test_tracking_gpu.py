@@ -216,3 +216,86 @@ def test_track_table_grows_past_capacity(trk, gpu):
         assert _same(rd, rh), f
     assert dev.cap >= 2048
     assert len(dev.live_slots(0)) == len(host.streams[0].live_sorted()) > 1024
+
+
+def _ref_kf(oracle, box):
+    """KalmanFilter.init_kf_from_bbox (reference KalmanFilter.py:36-99) on the
+    oracle's filterpy restatement: float32 F, H, x, P, Q, R"""
+    kf = oracle.KalmanFilterRestated(8, 4)
+    F = np.eye(8, dtype=np.float32)
+    F[np.arange(4), np.arange(4) + 4] = 1.0
+    kf.F = F
+    H = np.zeros((4, 8), np.float32)
+    H[np.arange(4), np.arange(4)] = 1.0
+    kf.H = H
+    kf.x = np.zeros((8, 1), np.float32)
+    kf.x[0:4, 0] = _ref_z(box)
+    kf.P = np.diag(np.array([10] * 4 + [1000] * 4, np.float32))
+    q = np.array([1.0] * 4 + [10.0] * 4, np.float32)
+    kf.Q = np.diag(q * q)
+    r = np.ones(4, np.float32)
+    kf.R = np.diag(r * r)
+    return kf
+
+
+def _ref_z(box):
+    """bbox_xyxy_to_z (KalmanFilter.py:5-16)"""
+    x1, y1, x2, y2 = map(float, box)
+    w, h = max(1.0, x2 - x1), max(1.0, y2 - y1)
+    return np.array([x1 + 0.5 * w, y1 + 0.5 * h, w / h, h], dtype=np.float32)
+
+
+def _ref_d2(kf, box):
+    """gating_distance_maha (KalmanFilter.py:105-116), numpy dtypes as in the reference"""
+    z = _ref_z(box).reshape(4, 1).astype(np.float32)
+    y = z - (kf.H @ kf.x)
+    S = kf.H @ kf.P @ kf.H.T + kf.R
+    Sinv = np.linalg.inv(S + 1e-9 * np.eye(4, dtype=np.float32))
+    return float((y.T @ Sinv @ y)[0, 0])
+
+
+def _box_at_d2(kf, box, target):
+    """the box shifted in x so that the reference's d2 equals target (bisection)"""
+    lo, hi = 0.0, 2000.0
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        b = [box[0] + mid, box[1], box[2] + mid, box[3]]
+        if _ref_d2(kf, b) < target:
+            lo = mid
+        else:
+            hi = mid
+    return [box[0] + lo, box[1], box[2] + lo, box[3]]
+
+
+def test_kalman_gate_decisions_at_threshold(trk, oracle, gpu):
+    """KAT for the Kalman gate near maha_thr on a track's second and third frames.
+    filterpy keeps a new track's x / P in float32 through the first predict and
+    update (x until the second update); the device state is float64 from birth, so
+    d2 differs from the reference's by ~1e-7 relative there (Kalman
+    state).  Detections at d2_ref = thr * (1 -+ 1e-4) -- far outside that band --
+    must be matched / gated exactly as the reference decides."""
+    thr = 9.49
+    box0 = [500.0, 400.0, 600.0, 600.0]
+    emb = np.random.default_rng(3).standard_normal((1, 128)).astype(np.float32)
+    for nupd in (0, 1):  # gate on the 2nd frame (no update yet) / on the 3rd (one update)
+        kf = _ref_kf(oracle, box0)
+        frames = [box0]
+        if nupd:
+            kf.predict()
+            kf.update(_ref_z(box0).reshape(4, 1))
+            frames.append(box0)
+        kf.predict()
+        inside = _box_at_d2(kf, box0, thr * (1 - 1e-4))
+        outside = _box_at_d2(kf, box0, thr * (1 + 1e-4))
+        assert _ref_d2(kf, inside) <= thr < _ref_d2(kf, outside)
+        mst = trk.MultiStreamTracker(2, device=gpu)
+        E = torch.from_numpy(np.stack([emb, emb]))[:, :, :].to(gpu)
+        C = torch.full((2, 1), 0.9, device=gpu)
+        for f, b in enumerate(frames):
+            B = torch.tensor([[b], [b]], dtype=torch.float32, device=gpu)
+            res = mst.step(E, B, C, [1, 1], [[0.9], [0.9]], [f, f])
+        B = torch.tensor([[inside], [outside]], dtype=torch.float32, device=gpu)
+        res = mst.step(E, B, C, [1, 1], [[0.9], [0.9]], [len(frames)] * 2)
+        assert res[0].matches.reshape(-1, 2).shape[0] == 1, (nupd, res[0])   # inside: matched
+        assert res[1].matches.reshape(-1, 2).shape[0] == 0, (nupd, res[1])   # outside: gated
+        assert len(res[1].unmatched_dets) == 1
