@@ -127,6 +127,8 @@ def _declare(L):
     L.trk_enc_set_prof.restype = i32
     L.trk_cost_set_prof.argtypes = [P]
     L.trk_cost_set_prof.restype = i32
+    L.trk_head_set_prof.argtypes = [P]
+    L.trk_head_set_prof.restype = i32
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

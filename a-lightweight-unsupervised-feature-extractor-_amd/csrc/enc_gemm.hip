@@ -1766,6 +1766,11 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
       // reads 16 B of row r at chunk 2 ks + h
       auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 3) * 32 + f32r, (s >> 2) * 2 + f32h)); };
       auto rd_b = [&](int ks, int t) { return *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 32 + f32r, ks * 2 + f32h)); };
+      const bool top = a.dbg & 512;  // experiment: the next K tile's 8 DMA pieces all before the MFMAs
+      if (pf && top) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) issue_piece(q);
+      }
       bf8v bfr[2][2];
       bfr[0][0] = rd_b(0, 0);
       bfr[0][1] = rd_b(0, 1);
@@ -1781,7 +1786,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[ks & 1][t], acc[i][t], 0, 0, 0);
-        if (pf && (s & 1)) issue_piece(s >> 1);
+        if (pf && !top && (s & 1)) issue_piece(s >> 1);
         afr = anext;
       }
     }

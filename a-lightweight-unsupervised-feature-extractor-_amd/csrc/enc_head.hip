@@ -18,66 +18,100 @@
 // weight row (the sum's order is permuted, not its terms).
 #include "trk_common.h"
 
+unsigned long long* g_head_prof = nullptr;  // trk_head_set_prof (diagnostics)
+int g_head_waves = 16;  // trk_set_tuning("head_waves"): enc_head workgroup of 8 or 16 waves
+
 namespace {
 
 typedef float f4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned long long hd_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 constexpr int RB = 16;        // ROIs per workgroup
 constexpr int NWAVE = 8;
 constexpr int MAXC = 1024;    // channel bound (LDS sizing)
 
 // acc[t] (t < NT) += X[16][K] . W[n0 + 16 t .. + 15][K]^T.  K is walked in
-// chunks of U blocks of 16 whose weight loads (NT x U 16-B loads per lane) are
-// all issued before the chunk's first MFMA: one L2 round trip per chunk
-// instead of one per block (the loop is latency-bound otherwise).  NT and U are
-// compile-time so the loads / MFMAs are straight-line code.
+// chunks of U blocks of 16; chunk c + 1's weight and activation loads (NT x U + U
+// 16-B loads per lane, into the other register buffer) are issued before chunk c's
+// MFMAs, so each L2 round trip runs under the previous chunk's MFMAs instead of
+// between them.  NT and U are compile-time so loads / MFMAs are straight-line code.
 template <int NT, int U>
-__device__ __forceinline__ void rb_chunk(const float* xp, const float* const (&wp)[NT], int kb0, f4_t (&acc)[NT]) {
+struct RbBuf {
   float4 a[U], b[U][NT];
+};
+
+template <int NT, int U>
+__device__ __forceinline__ void rb_load(const float* xp, const float* const (&wp)[NT], int kb0, RbBuf<NT, U>& d) {
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b[u][t] = *reinterpret_cast<const float4*>(wp[t] + kb0 + 16 * u);
+    for (int t = 0; t < NT; ++t) d.b[u][t] = *reinterpret_cast<const float4*>(wp[t] + kb0 + 16 * u);
 #pragma unroll
-  for (int u = 0; u < U; ++u) a[u] = *reinterpret_cast<const float4*>(xp + kb0 + 16 * u);
-  // keep every load of the chunk ahead of its MFMAs (the scheduler would otherwise
-  // interleave them to save registers and re-serialise the round trips)
-  __builtin_amdgcn_sched_barrier(0);
+  for (int u = 0; u < U; ++u) d.a[u] = *reinterpret_cast<const float4*>(xp + kb0 + 16 * u);
+}
+
+template <int NT, int U>
+__device__ __forceinline__ void rb_mfma(const RbBuf<NT, U>& d, f4_t (&acc)[NT]) {
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, b[u][t].x, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, b[u][t].y, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, b[u][t].z, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, b[u][t].w, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(d.a[u].x, d.b[u][t].x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(d.a[u].y, d.b[u][t].y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(d.a[u].z, d.b[u][t].z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(d.a[u].w, d.b[u][t].w, acc[t], 0, 0, 0);
     }
 }
 
-template <int NT>
+template <int NT, int U>
 __device__ __forceinline__ void rb_gemm(const float* __restrict__ Xs, int ldx, const float* __restrict__ W,
                                         int64_t ldw, int n0, int K, f4_t (&acc)[NT]) {
-  constexpr int U = NT >= 4 ? 8 : 16;  // <= 32 weight loads in flight per lane
+  constexpr int KC = 16 * U;
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const float* wp[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) wp[t] = W + (int64_t)(n0 + 16 * t + r) * ldw + 4 * g;
   const float* xp = Xs + r * ldx + 4 * g;
-  int kb = 0;
-  for (; kb + 16 * U <= K; kb += 16 * U) rb_chunk<NT, U>(xp, wp, kb, acc);
-  for (; kb < K; kb += 16) rb_chunk<NT, 1>(xp, wp, kb, acc);
+  const int nch = K / KC;
+  if (nch > 0) {
+    RbBuf<NT, U> b0, b1;
+    rb_load<NT, U>(xp, wp, 0, b0);
+    int c = 0;
+    for (;;) {
+      if (c + 1 < nch) rb_load<NT, U>(xp, wp, (c + 1) * KC, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      rb_mfma<NT, U>(b0, acc);
+      if (++c == nch) break;
+      if (c + 1 < nch) rb_load<NT, U>(xp, wp, (c + 1) * KC, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      rb_mfma<NT, U>(b1, acc);
+      if (++c == nch) break;
+    }
+  }
+  for (int kb = nch * KC; kb < K; kb += 16) {
+    RbBuf<NT, 1> t1;
+    rb_load<NT, 1>(xp, wp, kb, t1);
+    rb_mfma<NT, 1>(t1, acc);
+  }
 }
 
 // Y[16][N] = epi(col, X[16][K] . W[N][K]^T + bias) -> per-element store
 // callback, column tiles of 16 spread over the 8 waves (runs of 4, then singles).
-template <int NT, class Store>
+template <int NT, int U, class Store>
 __device__ __forceinline__ void rb_tiles(const float* Xs, int ldx, const float* W, const float* bias, int K,
                                          int t0, Store store) {
   const int lane = threadIdx.x & 63;
   f4_t acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4_t{0.f, 0.f, 0.f, 0.f};
-  rb_gemm<NT>(Xs, ldx, W, K, t0 * 16, K, acc);
+  rb_gemm<NT, U>(Xs, ldx, W, K, t0 * 16, K, acc);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int col = (t0 + t) * 16 + (lane & 15);
@@ -87,16 +121,23 @@ __device__ __forceinline__ void rb_tiles(const float* Xs, int ldx, const float* 
   }
 }
 
-template <class Store>
+// column tiles spread over the NW waves: runs of 4 (8-wave workgroups) or 2 (16-wave
+// workgroups, 128 VGPRs), then singles; U = K blocks per double-buffered chunk
+template <int NW, class Store>
 __device__ __forceinline__ void rb_linear(const float* Xs, int ldx, const float* W, const float* bias, int N,
                                           int K, Store store) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntile = N / 16;
-  const int per = (ntile + NWAVE - 1) / NWAVE;
+  const int per = (ntile + NW - 1) / NW;
   const int t_begin = wave * per, t_end = min(ntile, t_begin + per);
   int t0 = t_begin;
-  for (; t0 + 4 <= t_end; t0 += 4) rb_tiles<4>(Xs, ldx, W, bias, K, t0, store);
-  for (; t0 < t_end; ++t0) rb_tiles<1>(Xs, ldx, W, bias, K, t0, store);
+  if constexpr (NW <= 8) {
+    for (; t0 + 4 <= t_end; t0 += 4) rb_tiles<4, 4>(Xs, ldx, W, bias, K, t0, store);
+    for (; t0 < t_end; ++t0) rb_tiles<1, 8>(Xs, ldx, W, bias, K, t0, store);
+  } else {
+    for (; t0 + 2 <= t_end; t0 += 2) rb_tiles<2, 2>(Xs, ldx, W, bias, K, t0, store);
+    for (; t0 < t_end; ++t0) rb_tiles<1, 4>(Xs, ldx, W, bias, K, t0, store);
+  }
 }
 
 // number of 128-row GEMM tiles covering ROI roi (its partial sums, trk_amd.h)
@@ -153,13 +194,61 @@ __global__ void __launch_bounds__(512) enc_se_kernel(const SeArgs a) {
     *reinterpret_cast<float4*>(Xs + rr * ldx + c) = mr;
   }
   __syncthreads();
-  rb_linear(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[row * ldh + col] = fmaxf(v, 0.f); });
+  rb_linear<NWAVE>(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[row * ldh + col] = fmaxf(v, 0.f); });
   __syncthreads();
   // hardsigmoid (torch: min(max(x + 3, 0), 6) / 6), straight to global
   float* __restrict__ sout = a.s;
-  rb_linear(Hs, ldh, a.w2, a.b2, C, H, [&](int row, int col, float v) {
+  rb_linear<NWAVE>(Hs, ldh, a.w2, a.b2, C, H, [&](int row, int col, float v) {
     if (row < nrow) sout[(r0 + row) * C + col] = fminf(fmaxf(v + 3.0f, 0.f), 6.0f) / 6.0f;
   });
+}
+
+// LayerNorm over C (biased variance, eps inside the sqrt) + SiLU of rows w, w + NW, ...
+// of Zs into Gs.  Lane-strided columns c = lane + 64 q (q < QL, QL * 64 >= C) held in
+// registers; the affine parameters are loaded once per wave, all in flight together.
+// Sums run in ascending q per lane, then the xor tree: the order of the plain loop.
+template <int NW, int QL>
+__device__ __forceinline__ void ln_silu_rows(const float* Zs, float* Gs, int ldx, int C, const float* ln_w,
+                                             const float* ln_b, float eps) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float lw[QL], lb[QL];
+#pragma unroll
+  for (int q = 0; q < QL; ++q) {
+    const int c = lane + 64 * q;
+    lw[q] = c < C ? ln_w[c] : 0.f;
+    lb[q] = c < C ? ln_b[c] : 0.f;
+  }
+  for (int rr = wave; rr < RB; rr += NW) {
+    const float* z = Zs + rr * ldx;
+    float zv[QL];
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < QL; ++q) {
+      const int c = lane + 64 * q;
+      zv[q] = c < C ? z[c] : 0.f;
+      if (c < C) sum += zv[q];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float mean = sum / (float)C;
+    float sq = 0.f;
+#pragma unroll
+    for (int q = 0; q < QL; ++q) {
+      const float d = zv[q] - mean;
+      if (lane + 64 * q < C) sq += d * d;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+    const float rstd = 1.0f / sqrtf(sq / (float)C + eps);
+#pragma unroll
+    for (int q = 0; q < QL; ++q) {
+      const int c = lane + 64 * q;
+      if (c < C) {
+        const float y = (zv[q] - mean) * rstd * lw[q] + lb[q];
+        Gs[rr * ldx + c] = y / (1.0f + expf(-y));
+      }
+    }
+  }
 }
 
 struct HeadArgs {
@@ -170,9 +259,11 @@ struct HeadArgs {
   int R, C, D, Pi;
   float P, eps;
   double alpha;
+  unsigned long long* prof;  // per wave [prologue, W0, LN, W4, normalize] (diagnostics)
 };
 
-__global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) enc_head_kernel(const HeadArgs a) {
   extern __shared__ __align__(16) float lds[];
   const int C = a.C, D = a.D, ldx = C + 4, ldd = D + 4;
   float* Gs = lds;                  // [16][C + 4] g, then silu(LN(z))
@@ -182,6 +273,8 @@ __global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
   const int nrow = (int)min<int64_t>(RB, a.R - r0);
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float al = (float)a.alpha, bl = (float)(1.0 - a.alpha);  // torch: a * (.), (1 - a) * (.)
+  unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+  if (a.prof) pt[0] = hd_stamp();
   const int C4 = C / 4;
 #pragma unroll 4
   for (int q = threadIdx.x; q < RB * C4; q += blockDim.x) {
@@ -213,34 +306,24 @@ __global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
     *reinterpret_cast<float4*>(Gs + rr * ldx + c) = make_float4(gv[0], gv[1], gv[2], gv[3]);
   }
   __syncthreads();
-  rb_linear(Gs, ldx, a.w0, nullptr, C, C, [&](int row, int col, float v) { Zs[row * ldx + col] = v; });
+  if (a.prof) pt[1] = hd_stamp();
+  rb_linear<NW>(Gs, ldx, a.w0, nullptr, C, C, [&](int row, int col, float v) { Zs[row * ldx + col] = v; });
   __syncthreads();
-  // LayerNorm over C (biased variance, eps inside the sqrt) + SiLU: wave w owns rows 2w, 2w + 1
-  for (int rr = 2 * wave; rr < 2 * wave + 2; ++rr) {
-    const float* z = Zs + rr * ldx;
-    float sum = 0.f;
-    for (int c = lane; c < C; c += 64) sum += z[c];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    const float mean = sum / (float)C;
-    float sq = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float d = z[c] - mean;
-      sq += d * d;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
-    const float rstd = 1.0f / sqrtf(sq / (float)C + a.eps);
-    for (int c = lane; c < C; c += 64) {
-      const float y = (z[c] - mean) * rstd * a.ln_w[c] + a.ln_b[c];
-      Gs[rr * ldx + c] = y / (1.0f + expf(-y));
-    }
+  if (a.prof) pt[2] = hd_stamp();
+  // LayerNorm over C (biased variance, eps inside the sqrt) + SiLU: wave w owns rows w, w + NW, ...
+  if constexpr (NW == 16) {  // launched for C <= 512 only (register budget)
+    ln_silu_rows<NW, 8>(Zs, Gs, ldx, C, a.ln_w, a.ln_b, a.eps);
+  } else {
+    if (C <= 512) ln_silu_rows<NW, 8>(Zs, Gs, ldx, C, a.ln_w, a.ln_b, a.eps);
+    else ln_silu_rows<NW, MAXC / 64>(Zs, Gs, ldx, C, a.ln_w, a.ln_b, a.eps);
   }
   __syncthreads();
-  rb_linear(Gs, ldx, a.w4, a.b4, D, C, [&](int row, int col, float v) { Ys[row * ldd + col] = v; });
+  if (a.prof) pt[3] = hd_stamp();
+  rb_linear<NW>(Gs, ldx, a.w4, a.b4, D, C, [&](int row, int col, float v) { Ys[row * ldd + col] = v; });
   __syncthreads();
+  if (a.prof) pt[4] = hd_stamp();
   // F.normalize(dim=1): y / max(||y||, 1e-12)
-  for (int rr = 2 * wave; rr < 2 * wave + 2; ++rr) {
+  for (int rr = wave; rr < RB; rr += NW) {
     const float* y = Ys + rr * ldd;
     float sq = 0.f;
     for (int c = lane; c < D; c += 64) sq += y[c] * y[c];
@@ -249,6 +332,15 @@ __global__ void __launch_bounds__(512) enc_head_kernel(const HeadArgs a) {
     const float nrm = fmaxf(sqrtf(sq), 1e-12f);
     if (rr < nrow)
       for (int c = lane; c < D; c += 64) a.out[(r0 + rr) * D + c] = y[c] / nrm;
+  }
+  if (a.prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pt[5] = hd_stamp();
+    if (lane == 0) {
+      unsigned long long* o = a.prof + ((int64_t)blockIdx.x * 16 + wave) * 5;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) o[q] = pt[q + 1] - pt[q];
+    }
   }
 }
 
@@ -290,15 +382,29 @@ extern "C" int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_
   TRK_REQUIRE(tsums && s && m_r && m_n && w0 && ln_w && ln_b && w4 && b4 && out, "enc_head: null pointer");
   TRK_REQUIRE(al16(tsums) && al16(s) && al16(m_r) && al16(m_n) && al16(w0) && al16(w4),
               "enc_head: operands must be 16-byte aligned");
-  HeadArgs a{tsums, s, m_r, m_n, w0, ln_w, ln_b, w4, b4, out, (int)R, (int)C, (int)D, (int)P, (float)P, ln_eps, alpha};
+  HeadArgs a{tsums, s, m_r, m_n, w0, ln_w, ln_b, w4, b4, out, (int)R, (int)C, (int)D, (int)P, (float)P, ln_eps, alpha,
+             g_head_prof};
   const size_t lds = (size_t)RB * (2 * (C + 4) + (D + 4)) * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_head_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_head_kernel<8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_head_kernel<16>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(enc_head_kernel, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * NWAVE), lds,
-                     reinterpret_cast<hipStream_t>(stream), a);
+  if (g_head_waves == 16 && C <= 512)
+    hipLaunchKernelGGL(enc_head_kernel<16>, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * 16), lds,
+                       reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(enc_head_kernel<8>, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * 8), lds,
+                       reinterpret_cast<hipStream_t>(stream), a);
   return trk::check_launch("enc_head_kernel");
+}
+
+// diagnostics: enc_head per-wave s_memtime phases (u64 x 5 per wave, 8 waves per
+// 16-ROI workgroup); NULL = off
+extern "C" int trk_head_set_prof(unsigned long long* buf) {
+  g_head_prof = buf;
+  return TRK_OK;
 }

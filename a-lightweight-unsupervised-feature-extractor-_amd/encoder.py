@@ -178,6 +178,7 @@ class Model(nn.Module):
     fused_gemm = True
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
+    tail_stream = None   # fused tail: a torch.cuda.Stream for enc_head (None: the current stream)
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
@@ -209,8 +210,21 @@ class Model(nn.Module):
                 # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
                 m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
                 tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
-                return enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
-                                self.head.net[1].eps, W["h4"], W["h4b"])
+                head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
+                                        self.head.net[1].eps, W["h4"], W["h4b"])
+                ts = self.tail_stream
+                if ts is None:
+                    return head()
+                # the head (128 workgroups, latency-bound) on its own stream, so the caller's
+                # next launches (the next frame's ROI Align / first GEMM) fill the rest of the
+                # GPU beside it; the result is ready on `tail_stream`, which the caller syncs
+                ev = torch.cuda.Event()
+                ev.record()
+                with torch.cuda.stream(ts):
+                    ts.wait_event(ev)
+                    for t in (tsums, s, m_r, m_n):
+                        t.record_stream(ts)
+                    return head()
             f = enc_sums_reduce(sums, ss)
             m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
             s = self._se(m_r)

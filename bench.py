@@ -134,6 +134,15 @@ class Pipeline:
         # they dispatch as soon as CUs free up beside the encoder's full-GPU grids
         prio = int(os.environ.get("TRK_TRACK_PRIO", "1"))
         self.track_stream = torch.cuda.Stream(device=sc["feat"].device, priority=-1) if prio else None
+        # the encoder's last kernel (projection head, 128 latency-bound workgroups) on a stream of
+        # its own: the next frame's ROI Align and first GEMM fill the GPU beside it
+        self.tail = (torch.cuda.Stream(device=sc["feat"].device)
+                     if os.environ.get("TRK_HEAD_STREAM", "1") == "1" else None)
+        # ROI Align of frame f+1 issued on its own stream when frame f's encoder is enqueued
+        # (TRK_ROI_STREAM=1: +0.7..2 % in r02 A/B runs, within run-to-run spread: off by default)
+        self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
+                           if os.environ.get("TRK_ROI_STREAM", "0") == "1" else None)
+        self.roi_pending = {}
 
     def capture(self):
         """Capture roi_align + encoder as two hipGraphs (static ROI / embedding
@@ -184,11 +193,38 @@ class Pipeline:
                 rois.copy_(self.sc["rois"][f], non_blocking=True)
                 g.replay()
             else:
-                emb = self.stage_embed(self.stage_roi(f))
+                roi = self._roi_for(f, side)
+                self.model.tail_stream = self.tail
+                try:
+                    emb = self.stage_embed(roi)
+                finally:
+                    self.model.tail_stream = None
+                self._roi_ahead(f + 1)
             ev = torch.cuda.Event()
-            ev.record(side)
+            ev.record(self.tail if (self.tail is not None and self.graphs is None) else side)
         emb.record_stream(main)
         self.pending[f] = (emb, ev)
+
+    def _roi_ahead(self, f):
+        """ROI Align of frame f on its own stream, now: it runs beside the encoder
+        launches already queued (VALU-bound next to MFMA-bound) instead of before the
+        frame's first GEMM on the encoder stream"""
+        if self.roi_stream is None or f in self.roi_pending or f >= len(self.sc["rois"]):
+            return
+        with torch.cuda.stream(self.roi_stream):
+            roi = self.stage_roi(f)
+            ev = torch.cuda.Event()
+            ev.record(self.roi_stream)
+        self.roi_pending[f] = (roi, ev)
+
+    def _roi_for(self, f, side):
+        if self.roi_stream is None:
+            return self.stage_roi(f)
+        self._roi_ahead(f)
+        roi, ev = self.roi_pending.pop(f)
+        side.wait_event(ev)
+        roi.record_stream(side)
+        return roi
 
     def step(self, f):
         if self.track_stream is not None:

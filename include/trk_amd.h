@@ -158,6 +158,8 @@ int trk_lsap_set_prof(unsigned long long* buf);
 int trk_enc_set_prof(unsigned long long* buf);
 /* diagnostics: per-wave timestamps of the bank-resident cost kernel; NULL = off */
 int trk_cost_set_prof(unsigned long long* buf);
+/* diagnostics: per-wave phase timestamps of enc_head; NULL = off */
+int trk_head_set_prof(unsigned long long* buf);
 
 /* ------------------------------------------------------------------------
  * Encoder helpers (the non-GEMM parts of encoderAndHead.Model's eval graph,

@@ -7,7 +7,7 @@ sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 ops = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
-modes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,2,3").split(",")]
+modes = (sys.argv[1] if len(sys.argv) > 1 else "1,2,3").split(",")  # enc_gemm[:enc_gemm_dbg]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 P, M = 100, 204800
 R = M // P
@@ -30,9 +30,12 @@ def timeit(fn, reps=10):
 res = {m: [] for m in modes}
 for _ in range(rounds):
     for m in modes:
-        L.trk_set_tuning(b"enc_gemm", m)
+        mm, _, dbg = m.partition(":")
+        L.trk_set_tuning(b"enc_gemm", int(mm))
+        L.trk_set_tuning(b"enc_gemm_dbg", int(dbg or 0))
         res[m].append(timeit(lambda: ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True)))
 L.trk_set_tuning(b"enc_gemm", 1)
+L.trk_set_tuning(b"enc_gemm_dbg", 0)
 for m in modes:
     med = statistics.median(res[m])
     print(json.dumps({"mode": m, "median_us": round(med, 1), "min_us": round(min(res[m]), 1),
