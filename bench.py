@@ -650,6 +650,10 @@ def main():
     rf["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL",
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
+    rf["streams"] = {"embed": len(pipe.sides), "head_stream": pipe.tail is not None,
+                     "roi_stream": pipe.roi_stream is not None, "track_prio": pipe.track_stream is not None,
+                     "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,
+                     "tuning": os.environ.get("TRK_TUNE") or None}
     step_us = el / args.steps * 1e6
     rf["step_breakdown"] = {
         "step_us": round(step_us, 1),
