@@ -34,6 +34,7 @@
 //   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
 #include "trk_common.h"
 
+unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
 int g_enc_gemm = 1;      // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
 int g_enc_gemm_dbg = 0;     // trk_set_tuning("enc_gemm_dbg"): experiments (1 skip epilogue, 2 stores, 4 sums, 8 sum
                             // writes; g1dw: 16 no depthwise, 32 two K steps only)
@@ -94,6 +95,7 @@ struct EncGemmArgs {
   const float* scale;      // EPI_TRANS: s [nroi][kscale]
   int M, N, K, P, groups, kscale;
   int dbg;                 // g_enc_gemm_dbg
+  unsigned long long* prof;  // trk_enc_set_prof (gemm4: per-workgroup phase stamps; diagnostics)
 };
 
 // bf16-path activations: hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32), a
@@ -103,6 +105,13 @@ __device__ __forceinline__ float silu_f(float v) {
 }
 __device__ __forceinline__ float hswish_f(float v) {
   return v * fminf(fmaxf(v + 3.0f, 0.0f), 6.0f) * (1.0f / 6.0f);
+}
+__device__ __forceinline__ unsigned long long eg_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
 }
 
 // cross-lane exchanges without the LDS pipe (ds_bpermute): DPP quad_perm for lane ^ 1,
@@ -1396,6 +1405,11 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
 
+  // diagnostics (trk_enc_set_prof): wave 0's [start, K loop, activation, ROI sums,
+  // staging + barrier, sums stores, output stores drained] per workgroup
+  unsigned long long pst[8];
+  const bool prof = a.prof != nullptr;
+  if (prof) pst[0] = eg_stamp();
   issue(0);
   if (nk > 1) {
     issue(1);
@@ -1435,6 +1449,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
     g4_barrier();
   }
 
+  if (prof) pst[1] = eg_stamp();
   if (a.dbg & 1) {
     if (tid == 0 && acc[0][0][0] == 12345.f) a.sums[0] = 1;
     return;
@@ -1457,6 +1472,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
         acc[i][t][2 * h] = v.x;
         acc[i][t][2 * h + 1] = v.y;
       }
+  }
+  if (prof) {
+    asm volatile("" ::"v"(acc[3][7][3]));
+    pst[2] = eg_stamp();
   }
   // per-ROI column sums: each row-half wave (wr) writes its f32 partials for every tile
   // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
@@ -1518,6 +1537,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       }
     }
   }
+  if (prof) pst[3] = eg_stamp();
   if (EPI == EPI_DSC && !(a.dbg & 2)) {
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
     const bool odd = fr & 1;
@@ -1535,6 +1555,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       }
   }
   __syncthreads();
+  if (prof) pst[4] = eg_stamp();
   {
     const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
     const int nslot = (int)(last_row / a.P - roi_base) + 1;
@@ -1547,6 +1568,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
             llrintf(part[slot * 256 + c] * kFix) + llrintf(part[(G4_SLOTS + slot) * 256 + c] * kFix);
       }
   }
+  if (prof) pst[5] = eg_stamp();
   if (EPI == EPI_DSC && !(a.dbg & 2)) {
     const uint32_t* stage = reinterpret_cast<const uint32_t*>(smem);
     const int64_t cbase = (int64_t)g * a.N + n0;
@@ -1557,6 +1579,16 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       if (row < a.M)
         *reinterpret_cast<uint4*>(a.C + row * a.ldc + cbase + c8) =
             *reinterpret_cast<const uint4*>(stage + rl * G4_SLD + c8 / 2);
+    }
+  }
+  if (prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pst[6] = eg_stamp();
+    if (tid == 0) {
+      unsigned long long* o = a.prof + lb * 8;
+      for (int q = 0; q < 6; ++q) o[q] = pst[q + 1] - pst[q];
+      o[6] = pst[6] - pst[0];
+      o[7] = 0;
     }
   }
 }
@@ -1921,7 +1953,6 @@ __global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntile
   }
 }
 
-unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics)
 
 template <int EPI, int MF>
 int launch8(const EncGemmArgs& a, hipStream_t st) {
@@ -1968,6 +1999,7 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   }
   EncGemmArgs b = a;
   b.dbg = g_enc_gemm_dbg;
+  b.prof = g_enc_prof;
   hipLaunchKernelGGL((gemm4_kernel<EPI>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg, g_enc_gemm_offset,
                      g_enc_gemm_offset > 0 ? next_queue_slot() : -1);
   return trk::check_launch("gemm4_kernel");
