@@ -35,6 +35,7 @@
 #include "trk_common.h"
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
+int g_enc_g4_narrow = 0;  // trk_set_tuning("enc_g4_narrow"): 1 = 3-slot ROI sums even for P >= 64 (A/B)
 int g_enc_gemm = 1;      // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
 int g_enc_gemm_dbg = 0;     // trk_set_tuning("enc_gemm_dbg"): experiments (1 skip epilogue, 2 stores, 4 sums, 8 sum
                             // writes; g1dw: 16 no depthwise, 32 two K steps only)
@@ -1300,7 +1301,9 @@ constexpr size_t G4_RED = (size_t)G4_SLOTS * 256 * 8;   // 8 KiB
 constexpr size_t G4_LDS = (G4_RING + G4_STILE) > (G4_STAGE + G4_RED) ? (G4_RING + G4_STILE) : (G4_STAGE + G4_RED);
 static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
 
-template <int EPI>
+// WIDE (P >= 64): a wave's 64 rows span at most 2 ROIs and a tile's 128 at most 3, so
+// the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions)
+template <int EPI, bool WIDE = false>
 __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, unsigned char* smem) {
   uint4* ring = reinterpret_cast<uint4*>(smem);
   // opaque per tile: keeps the compiler from hoisting lane-dependent addresses
@@ -1490,7 +1493,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
     const bool full = r0w + 64 <= (int64_t)a.M;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      float ssum[G4_WSLOTS] = {0.f, 0.f, 0.f};
+      constexpr int WS = WIDE ? 2 : G4_WSLOTS, TS = WIDE ? 3 : G4_SLOTS;
+      float ssum[WS];
+#pragma unroll
+      for (int q = 0; q < WS; ++q) ssum[q] = 0.f;
       int slot = 0, nxt = nxt0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1498,7 +1504,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
         if (full && nxt >= 16 * k + 16) {
           const float x = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
-          for (int q = 0; q < G4_WSLOTS; ++q)
+          for (int q = 0; q < WS; ++q)
             if (q == slot) ssum[q] += x;
         } else {
           float lo = 0.f, hi = 0.f;
@@ -1510,7 +1516,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
             else hi += x;
           }
 #pragma unroll
-          for (int q = 0; q < G4_WSLOTS; ++q) {
+          for (int q = 0; q < WS; ++q) {
             if (q == slot) ssum[q] += lo;
             if (q == slot + 1) ssum[q] += hi;
           }
@@ -1521,16 +1527,16 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
         }
       }
 #pragma unroll
-      for (int q = 0; q < G4_WSLOTS; ++q) {
+      for (int q = 0; q < WS; ++q) {
         ssum[q] = sum_xor16(ssum[q]);
         ssum[q] = sum_xor32(ssum[q]);
       }
       if (lane < 16) {
 #pragma unroll
-        for (int ts = 0; ts < G4_SLOTS; ++ts) {
+        for (int ts = 0; ts < TS; ++ts) {
           float v = 0.f;
 #pragma unroll
-          for (int q = 0; q < G4_WSLOTS; ++q)
+          for (int q = 0; q < WS; ++q)
             if (q <= slot && wslot0 + q == ts) v = ssum[q];
           part[(wr * G4_SLOTS + ts) * 256 + colq + t * 16] = v;
         }
@@ -1598,11 +1604,11 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 // 2048-cycle sleeps), so the two workgroups sharing a CU stay out of phase:
 // one's MFMA loop runs under the other's VALU / store epilogue instead of both
 // alternating between them in lockstep.
-template <int EPI>
+template <int EPI, bool WIDE>
 __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles, int offset, int qslot) {
   extern __shared__ __align__(16) unsigned char smem[];
   if (qslot < 0) {  // one workgroup per tile
-    gemm4_tile<EPI>(a, xcd_remap(blockIdx.x, ntiles), smem);
+    gemm4_tile<EPI, WIDE>(a, xcd_remap(blockIdx.x, ntiles), smem);
     return;
   }
   const TileQueue tq{g_tileq[qslot], ntiles};
@@ -1612,7 +1618,7 @@ __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t nt
   for (;;) {
     const int64_t t = tq.next(reinterpret_cast<int*>(smem), cur);  // LDS is free between tiles
     if (t < 0) break;
-    gemm4_tile<EPI>(a, t, smem);
+    gemm4_tile<EPI, WIDE>(a, t, smem);
     __syncthreads();  // the next tile's DMA reuses the LDS the epilogue read
   }
   tq.finish();
@@ -1993,15 +1999,22 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t grid = g_enc_gemm_offset > 0 ? std::min<int64_t>(nwg, 2 * (int64_t)cu_count()) : nwg;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
     attr = true;
   }
   EncGemmArgs b = a;
   b.dbg = g_enc_gemm_dbg;
   b.prof = g_enc_prof;
-  hipLaunchKernelGGL((gemm4_kernel<EPI>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg, g_enc_gemm_offset,
-                     g_enc_gemm_offset > 0 ? next_queue_slot() : -1);
+  const int qs = g_enc_gemm_offset > 0 ? next_queue_slot() : -1;
+  if (a.P >= 64 && !g_enc_g4_narrow)
+    hipLaunchKernelGGL((gemm4_kernel<EPI, true>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg,
+                       g_enc_gemm_offset, qs);
+  else
+    hipLaunchKernelGGL((gemm4_kernel<EPI, false>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg,
+                       g_enc_gemm_offset, qs);
   return trk::check_launch("gemm4_kernel");
 }
 
