@@ -285,27 +285,39 @@ class LiveProbe:
              "trk_step_begin": "step_begin", "trk_step_mid": "step_mid", "trk_step_end": "step_end",
              "trk_step_apply": "step_apply"}
 
-    def __init__(self):
+    def __init__(self, pool=4096):
         self.on = False
         self.ev = {v: [] for v in self.NAMES.values()}
+        # events made before the timed region (creating two per call inside it cost host
+        # time the pipeline then waited for), handed out in order
+        self.pool = [_ev() for _ in range(pool)]
+        self.pi = 0
         self._orig = ops.lib
         probe = self
 
         class _Proxy:
-            def __getattr__(self, name):
+            def __getattr__(self, name):  # first lookup of a name only: the result is cached
                 fn = getattr(probe._orig(), name)
                 key = probe.NAMES.get(name)
-                if not probe.on or key is None:
+                if key is None:
+                    setattr(self, name, fn)
                     return fn
 
                 def call(*a):
+                    if not probe.on:
+                        return fn(*a)
                     st = torch.cuda.current_stream()
-                    e0, e1 = _ev(), _ev()
+                    if probe.pi + 2 <= len(probe.pool):
+                        e0, e1 = probe.pool[probe.pi], probe.pool[probe.pi + 1]
+                        probe.pi += 2
+                    else:
+                        e0, e1 = _ev(), _ev()
                     e0.record(st)
                     rc = fn(*a)
                     e1.record(st)
                     probe.ev[key].append((e0, e1))
                     return rc
+                setattr(self, name, call)
                 return call
 
         self._proxy = _Proxy()
@@ -551,7 +563,7 @@ def main():
         pipe.step(f)
         f += 1
 
-    probe = LiveProbe()
+    probe = LiveProbe(pool=max(1024, 2 * 20 * (args.steps + 2)))
     probe.on = True
     pipe.tracker.sync_wait_s = 0.0
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
