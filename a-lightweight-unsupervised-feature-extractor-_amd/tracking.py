@@ -224,6 +224,8 @@ class MultiStreamTracker:
         self.table = TrackTable(n_streams, int(capacity), self.T, self.device)
         self.params = default_cost_params(self.cfg, gate=True)
         self.params_nogate = default_cost_params(self.cfg, gate=False)
+        self._cost_max = float(self.cfg["cost_max"])
+        self._reid_max = float(self.cfg["reid_only_cost_max"])
         self.max_inflight = max(1, int(max_inflight))
         self._nmax = 0
         self._pending: List[StepHandle] = []
@@ -270,6 +272,20 @@ class MultiStreamTracker:
                                 float(self.cfg["init_conf_min"]), float(self.cfg["conf_update_min"]),
                                 float(self.cfg["cost_update_max"]), float(self.cfg["reid_only_cost_max"]),
                                 float(self.cfg["maha_thr"]), float(self.cfg["ema_alpha"]))
+        # the launch arguments that only change with the scratch / table: converted once
+        # (a frame's ~60 pointer conversions were host time the pipeline waited for)
+        P = _ptr
+        t, l1, l2 = self.table, self._lsap[0], self._lsap[1]
+        self._fp = dict(
+            st=ctypes.byref(self._state), cf=ctypes.byref(self._conf), prm=ctypes.byref(self.params),
+            prm_ng=ctypes.byref(self.params_nogate), m1=P(self._scr["m1"]), ndet=P(self._scr["ndet"]),
+            row1=P(self._scr["row1"]), m2=P(self._scr["m2"]), n2=P(self._scr["n2"]), row2=P(self._scr["row2"]),
+            e2=P(self._scr["e2"]), b2=P(self._scr["b2"]), c2=P(self._scr["c2"]),
+            ls0=P(self._scr["lsap_status"][0]), ls1=P(self._scr["lsap_status"][1]),
+            bank=P(t.bank), bank_len=P(t.bank_len), pbox=P(t.pbox), last_conf=P(t.last_conf), gmean=P(t.gmean),
+            gsinv=P(t.gsinv), gate_on=P(t.gate_on), C1=P(self._C[0]), C2=P(self._C[1]), work=P(self._cost_work),
+            r1=P(l1["rows"]), c1=P(l1["cols"]), n1=P(l1["count"]), a1=P(l1["assign"]),
+            r2=P(l2["rows"]), cc2=P(l2["cols"]), nn2=P(l2["count"]), a2=P(l2["assign"]))
 
     _scr_cap = -1
 
@@ -361,37 +377,28 @@ class MultiStreamTracker:
         L = lib()
         hN = (ctypes.c_int32 * S)(*N.tolist())
         hF = (ctypes.c_int64 * S)(*fid.tolist())
-        check(L.trk_step_begin(ctypes.byref(st), ctypes.byref(cf), hN, hF, Mb, stream), "step_begin")
-        C1, C2 = self._C
-        l1, l2 = self._lsap
-        p = ctypes.byref
-        check(L.trk_build_cost_dev(S, Mb, Nm, _ptr(sc["m1"]), _ptr(sc["ndet"]), _ptr(sc["row1"]), self.cap, self.T,
-                                   _ptr(t.bank), _ptr(t.bank_len), _ptr(t.pbox), _ptr(t.last_conf), _ptr(t.gmean),
-                                   _ptr(t.gsinv), _ptr(t.gate_on), _ptr(det_emb), _ptr(dbox), _ptr(dconf),
-                                   p(self.params), _ptr(C1), None, _ptr(self._cost_work), stream),
+        fp = self._fp
+        pe, pb, pc, pc64 = _ptr(det_emb), _ptr(dbox), _ptr(dconf), _ptr(dconf64)
+        check(L.trk_step_begin(fp["st"], fp["cf"], hN, hF, Mb, stream), "step_begin")
+        kmax = min(self.cap, Nm)
+        check(L.trk_build_cost_dev(S, Mb, Nm, fp["m1"], fp["ndet"], fp["row1"], self.cap, self.T, fp["bank"],
+                                   fp["bank_len"], fp["pbox"], fp["last_conf"], fp["gmean"], fp["gsinv"],
+                                   fp["gate_on"], pe, pb, pc, fp["prm"], fp["C1"], None, fp["work"], stream),
               "build_cost (stage 1)")
-        check(L.trk_lsap_dev(S, _ptr(C1), TRK_F32, Nm, Mb * Nm, _ptr(sc["m1"]), _ptr(sc["ndet"]), Mb, Nm,
-                             min(self.cap, Nm), _ptr(l1["rows"]), _ptr(l1["cols"]), _ptr(l1["count"]),
-                             _ptr(sc["lsap_status"][0]), _ptr(l1["assign"]), Mb, float(self.cfg["cost_max"]), stream),
-              "lsap (stage 1)")
-        check(L.trk_step_mid(p(st), p(cf), Mb, _ptr(C1), _ptr(l1["assign"]), _ptr(det_emb), _ptr(dbox), _ptr(dconf),
-                             stream), "step_mid")
-        check(L.trk_build_cost_dev(S, Mb, Nm, _ptr(sc["m2"]), _ptr(sc["n2"]), _ptr(sc["row2"]), self.cap, self.T,
-                                   _ptr(t.bank), _ptr(t.bank_len), _ptr(t.pbox), _ptr(t.last_conf), None, None, None,
-                                   _ptr(sc["e2"]), _ptr(sc["b2"]), _ptr(sc["c2"]), p(self.params_nogate), None,
-                                   _ptr(C2), _ptr(self._cost_work), stream), "build_cost (stage 2)")
-        check(L.trk_lsap_dev(S, _ptr(C2), TRK_F32, Nm, Mb * Nm, _ptr(sc["m2"]), _ptr(sc["n2"]), Mb, Nm,
-                             min(self.cap, Nm), _ptr(l2["rows"]), _ptr(l2["cols"]), _ptr(l2["count"]),
-                             _ptr(sc["lsap_status"][1]), _ptr(l2["assign"]), Mb,
-                             float(self.cfg["reid_only_cost_max"]), stream), "lsap (stage 2)")
-        check(L.trk_step_end(p(st), p(cf), Mb, _ptr(C2), _ptr(l2["assign"]), _ptr(dconf64), _ptr(dconf), stream),
-              "step_end")
+        check(L.trk_lsap_dev(S, fp["C1"], TRK_F32, Nm, Mb * Nm, fp["m1"], fp["ndet"], Mb, Nm, kmax, fp["r1"], fp["c1"],
+                             fp["n1"], fp["ls0"], fp["a1"], Mb, self._cost_max, stream), "lsap (stage 1)")
+        check(L.trk_step_mid(fp["st"], fp["cf"], Mb, fp["C1"], fp["a1"], pe, pb, pc, stream), "step_mid")
+        check(L.trk_build_cost_dev(S, Mb, Nm, fp["m2"], fp["n2"], fp["row2"], self.cap, self.T, fp["bank"],
+                                   fp["bank_len"], fp["pbox"], fp["last_conf"], None, None, None, fp["e2"], fp["b2"],
+                                   fp["c2"], fp["prm_ng"], None, fp["C2"], fp["work"], stream), "build_cost (stage 2)")
+        check(L.trk_lsap_dev(S, fp["C2"], TRK_F32, Nm, Mb * Nm, fp["m2"], fp["n2"], Mb, Nm, kmax, fp["r2"], fp["cc2"],
+                             fp["nn2"], fp["ls1"], fp["a2"], Mb, self._reid_max, stream), "lsap (stage 2)")
+        check(L.trk_step_end(fp["st"], fp["cf"], Mb, fp["C2"], fp["a2"], pc64, pc, stream), "step_end")
         buf = self._result_buf()
         buf.copy_(sc["result"], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        check(L.trk_step_apply(p(st), p(cf), _ptr(det_emb), _ptr(dbox), _ptr(dconf), _ptr(dconf64), stream),
-              "step_apply")
+        check(L.trk_step_apply(fp["st"], fp["cf"], pe, pb, pc, pc64, stream), "step_apply")
         # the caller's detection tensors must outlive the frame's kernels
         for x in (det_emb, dbox, dconf, dconf64):
             if x is not None:
