@@ -89,6 +89,24 @@ class ProjectionHead(nn.Module):
         self.logit_bias = nn.Parameter(torch.tensor(0.0, dtype=torch.float32), requires_grad=False)
 
 
+class DeferredHead:
+    """The fused path's last kernel (enc_head), not yet launched.  `launch(stream)`
+    makes `stream` wait for everything enqueued on the producing stream so far and
+    launches the head there, returning the [R, 128] embeddings (valid on `stream`)."""
+
+    def __init__(self, fn, inputs):
+        self._fn, self._inputs = fn, inputs
+        self.ready = torch.cuda.Event()
+        self.ready.record()  # after the transition GEMM, on the producing stream
+
+    def launch(self, stream: torch.cuda.Stream) -> torch.Tensor:
+        with torch.cuda.stream(stream):
+            stream.wait_event(self.ready)
+            for t in self._inputs:
+                t.record_stream(stream)
+            return self._fn()
+
+
 class Model(nn.Module):
     """encoderAndHead.Model(in_channels, out_channels, warmup_epochs, proj_dim)."""
 
@@ -178,7 +196,7 @@ class Model(nn.Module):
     fused_gemm = True
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
-    tail_stream = None   # fused tail: a torch.cuda.Stream for enc_head (None: the current stream)
+    defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
@@ -212,19 +230,13 @@ class Model(nn.Module):
                 tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
                 head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                         self.head.net[1].eps, W["h4"], W["h4b"])
-                ts = self.tail_stream
-                if ts is None:
+                if not self.defer_head:
                     return head()
-                # the head (128 workgroups, latency-bound) on its own stream, so the caller's
-                # next launches (the next frame's ROI Align / first GEMM) fill the rest of the
-                # GPU beside it; the result is ready on `tail_stream`, which the caller syncs
-                ev = torch.cuda.Event()
-                ev.record()
-                with torch.cuda.stream(ts):
-                    ts.wait_event(ev)
-                    for t in (tsums, s, m_r, m_n):
-                        t.record_stream(ts)
-                    return head()
+                # the head (128 latency-bound workgroups) is left to the caller, who launches
+                # it on the stream that consumes the embeddings: the caller's next launches on
+                # this stream (the next frame's ROI Align / first GEMM) then fill the rest of
+                # the GPU beside it
+                return DeferredHead(head, (tsums, s, m_r, m_n))
             f = enc_sums_reduce(sums, ss)
             m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
             s = self._se(m_r)

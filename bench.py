@@ -134,10 +134,10 @@ class Pipeline:
         # they dispatch as soon as CUs free up beside the encoder's full-GPU grids
         prio = int(os.environ.get("TRK_TRACK_PRIO", "1"))
         self.track_stream = torch.cuda.Stream(device=sc["feat"].device, priority=-1) if prio else None
-        # the encoder's last kernel (projection head, 128 latency-bound workgroups) on a stream of
-        # its own: the next frame's ROI Align and first GEMM fill the GPU beside it
-        self.tail = (torch.cuda.Stream(device=sc["feat"].device)
-                     if os.environ.get("TRK_HEAD_STREAM", "1") == "1" else None)
+        # the encoder's last kernel (projection head, 128 latency-bound workgroups) launched
+        # on the tracker's stream right before the frame's tracker step, so the next frame's
+        # ROI Align and first GEMM (embedding stream) fill the GPU beside it; no extra stream
+        self.defer_head = os.environ.get("TRK_HEAD_STREAM", "1") == "1" and self.track_stream is not None
         # ROI Align of frame f+1 issued on its own stream when frame f's encoder is enqueued
         # (TRK_ROI_STREAM=1: +0.7..2 % in r02 A/B runs, within run-to-run spread: off by default)
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
@@ -194,14 +194,22 @@ class Pipeline:
                 g.replay()
             else:
                 roi = self._roi_for(f, side)
-                self.model.tail_stream = self.tail
+                self.model.defer_head = self.defer_head
                 try:
-                    emb = self.stage_embed(roi)
+                    if self.defer_head:
+                        with torch.no_grad():
+                            emb = self.model(roi)
+                    else:
+                        emb = self.stage_embed(roi)
                 finally:
-                    self.model.tail_stream = None
+                    self.model.defer_head = False
                 self._roi_ahead(f + 1)
+                if hasattr(emb, "launch"):  # deferred head: launched by _step on the tracker's stream
+                    self.pending[f] = (emb, None)
+                    return
+                emb = emb.view(self.sc["streams"], self.sc["N"], 128)
             ev = torch.cuda.Event()
-            ev.record(self.tail if (self.tail is not None and self.graphs is None) else side)
+            ev.record(side)
         emb.record_stream(main)
         self.pending[f] = (emb, ev)
 
@@ -236,7 +244,11 @@ class Pipeline:
         sc = self.sc
         self.embed_async(f)
         emb, ev = self.pending.pop(f)
-        torch.cuda.current_stream().wait_event(ev)
+        if ev is None:  # deferred head: launched here, on the tracker's stream, before the step
+            with torch.no_grad():
+                emb = emb.launch(torch.cuda.current_stream()).view(sc["streams"], sc["N"], 128)
+        else:
+            torch.cuda.current_stream().wait_event(ev)
         if self.prefetch_early:  # next frame's embedding before this frame's cost build
             for d in range(1, self.depth + 1):
                 self.embed_async(f + d)
@@ -662,7 +674,7 @@ def main():
     rf["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL",
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
-    rf["streams"] = {"embed": len(pipe.sides), "head_stream": pipe.tail is not None,
+    rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
                      "roi_stream": pipe.roi_stream is not None, "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,
                      "tuning": os.environ.get("TRK_TUNE") or None}
