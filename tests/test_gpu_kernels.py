@@ -594,6 +594,32 @@ def test_encoder_fused_tail_matches_torch_tail(trk, gpu):
     assert (z - zt).abs().max().item() <= 2e-5
 
 
+def test_encoder_deferred_head_on_another_stream(trk, gpu):
+    """defer_head: the encoder returns the projection head unlaunched; launched on
+    another stream (as the bench does, on the tracker's) it gives the same embeddings
+    bit for bit, with the producing stream already running the next input."""
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()})
+    m = m.to(gpu)
+    x = torch.from_numpy(G.encoder_input(7, 64, 10)).to(gpu).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    other = torch.cuda.Stream(device=gpu)
+    with torch.no_grad():
+        z = m(x)
+        try:
+            m.defer_head = True
+            dh = m(x)
+            assert hasattr(dh, "launch")
+            z_next = m(x.flip(0))  # the producing stream moves on
+        finally:
+            m.defer_head = False
+        zd = dh.launch(other)
+    other.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(z, zd)
+    assert torch.equal(z_next.launch(torch.cuda.current_stream()), m(x.flip(0)))
+
+
 # ----------------------------------------------------- encoder helpers ----
 @pytest.mark.parametrize("S", [7, 10])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
