@@ -20,6 +20,7 @@
 
 unsigned long long* g_head_prof = nullptr;  // trk_head_set_prof (diagnostics)
 int g_head_waves = 16;  // trk_set_tuning("head_waves"): enc_head workgroup of 8 or 16 waves
+int g_se_waves = 16;    // trk_set_tuning("se_waves"): enc_se workgroup of 8 or 16 waves (16: 26 vs 29 us)
 
 namespace {
 
@@ -34,7 +35,6 @@ __device__ __forceinline__ unsigned long long hd_stamp() {
 }
 
 constexpr int RB = 16;        // ROIs per workgroup
-constexpr int NWAVE = 8;
 constexpr int MAXC = 1024;    // channel bound (LDS sizing)
 
 // acc[t] (t < NT) += X[16][K] . W[n0 + 16 t .. + 15][K]^T.  K is walked in
@@ -159,7 +159,8 @@ struct SeArgs {
   float P;
 };
 
-__global__ void __launch_bounds__(512) enc_se_kernel(const SeArgs a) {
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) enc_se_kernel(const SeArgs a) {
   extern __shared__ __align__(16) float lds[];
   const int C = a.C, H = a.H, ldx = C + 4, ldh = H + 4;
   float* Xs = lds;                 // [16][C + 4] m_r
@@ -194,11 +195,11 @@ __global__ void __launch_bounds__(512) enc_se_kernel(const SeArgs a) {
     *reinterpret_cast<float4*>(Xs + rr * ldx + c) = mr;
   }
   __syncthreads();
-  rb_linear<NWAVE>(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[row * ldh + col] = fmaxf(v, 0.f); });
+  rb_linear<NW>(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[row * ldh + col] = fmaxf(v, 0.f); });
   __syncthreads();
   // hardsigmoid (torch: min(max(x + 3, 0), 6) / 6), straight to global
   float* __restrict__ sout = a.s;
-  rb_linear<NWAVE>(Hs, ldh, a.w2, a.b2, C, H, [&](int row, int col, float v) {
+  rb_linear<NW>(Hs, ldh, a.w2, a.b2, C, H, [&](int row, int col, float v) {
     if (row < nrow) sout[(r0 + row) * C + col] = fminf(fmaxf(v + 3.0f, 0.f), 6.0f) / 6.0f;
   });
 }
@@ -362,12 +363,18 @@ extern "C" int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int
   const size_t lds = (size_t)RB * ((C + 4) + (H + 4)) * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<16>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(enc_se_kernel, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * NWAVE), lds,
-                     reinterpret_cast<hipStream_t>(stream), a);
+  if (g_se_waves == 16)
+    hipLaunchKernelGGL(enc_se_kernel<16>, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * 16), lds,
+                       reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(enc_se_kernel<8>, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * 8), lds,
+                       reinterpret_cast<hipStream_t>(stream), a);
   return trk::check_launch("enc_se_kernel");
 }
 

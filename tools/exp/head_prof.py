@@ -31,7 +31,9 @@ def t(fn, n=20):
 L = trk.lib()
 for hw in (8, 16, 8, 16):
     L.trk_set_tuning(b"head_waves", hw)
-    print(json.dumps({"head_waves": hw, "enc_se_us": t(se), "enc_head_us": t(hd)}), flush=True)
+    L.trk_set_tuning(b"se_waves", hw)
+    print(json.dumps({"head_waves": hw, "se_waves": hw, "enc_se_us": t(se), "enc_head_us": t(hd)}), flush=True)
+L.trk_set_tuning(b"se_waves", 16)
 prof = torch.zeros(R // 16 * 16 * 5, dtype=torch.int64, device=dev)
 L.trk_head_set_prof(ops._ptr(prof)); hd(); torch.cuda.synchronize(); L.trk_head_set_prof(None)
 pr = prof.view(-1, 5).double()
