@@ -23,7 +23,7 @@ from .costcard import cal_cost, bbox_cost, conf_cost
 from .encoder import Model
 from .tracking import Tracking, MultiStreamTracker, TrackTable, tracker_conf, load_conf
 from .detect import (letterbox_geometry, scale_coords_params, non_max_suppression, det_nms_batched,
-                     YoloPostprocess, preprocess_roi, train_rois)
+                     YoloPostprocess, preprocess_roi, train_rois, SPPCSPCHook)
 
 __all__ = ["TrkError", "lib", "header_symbols", "roi_align", "roi_align_from_input_boxes",
            "build_cost", "cost_combine", "lsap_batched", "linear_sum_assignment",

@@ -2,9 +2,10 @@
 
 The YOLOv7 network itself is out of scope (weights absent, `.MISSING_LARGE_BLOBS`);
 what the tracker consumes from it is (i) the SPPCSPC feature map, captured by a
-forward hook (reference model/yolov7/yoloDetects2.py:27-34) -- here simply the
-``feat`` tensor the caller passes on -- and (ii) the post-processed detections.
-This module mirrors the post-processing the reference runs on the head output:
+forward hook (reference model/yolov7/yoloDetects2.py:27-34: ``SPPCSPCHook``
+registers it on a loaded model; the ``feat`` tensor otherwise comes from the
+caller) and (ii) the post-processed detections.  This module mirrors the
+post-processing the reference runs on the head output:
 
   letterbox_geometry      utils/datasets.py:984-1014 (ratio and padding only;
                           the image resize itself is the caller's)
@@ -32,7 +33,7 @@ from ._lib import check, lib
 from .ops import _need_gpu, _ptr, _stream, roi_align
 
 __all__ = ["letterbox_geometry", "scale_coords_params", "non_max_suppression", "det_nms_batched",
-           "YoloPostprocess", "preprocess_roi", "train_rois"]
+           "YoloPostprocess", "preprocess_roi", "train_rois", "SPPCSPCHook"]
 
 _P, _i32, _i64, _f32, _f64, _sz = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float,
                                    ctypes.c_double, ctypes.c_size_t)
@@ -44,6 +45,33 @@ _lib.register({
 })
 
 MAX_WH, MAX_DET, MAX_NMS = 4096, 300, 30000   # general.py:621-623
+
+
+class SPPCSPCHook:
+    """The backbone-feature capture of YoloDetects.__init__ (yoloDetects2.py:27-34): a
+    forward hook on the model's first module whose class is named ``SPPCSPC`` keeps
+    that module's output (the [B, C, Hf, Wf] map roi_align reads) in ``.feat`` after
+    every forward.  ``remove()`` detaches it.  Raises ValueError when the model has no
+    such module (the reference silently leaves ``backbone_feat`` None; a missing
+    map would only surface later as a roi_align input error)."""
+
+    def __init__(self, model: torch.nn.Module, class_name: str = "SPPCSPC"):
+        self.feat: Optional[torch.Tensor] = None
+        self._handle = None
+        for m in model.modules():
+            if m.__class__.__name__ == class_name:
+                self._handle = m.register_forward_hook(self._hook)
+                break
+        if self._handle is None:
+            raise ValueError(f"model has no {class_name} module to hook")
+
+    def _hook(self, module, inputs, output):
+        self.feat = output
+
+    def remove(self):
+        if self._handle is not None:
+            self._handle.remove()
+            self._handle = None
 
 
 def letterbox_geometry(shape_hw: Tuple[int, int], new_shape=1280, auto: bool = False,

@@ -125,6 +125,34 @@ def test_letterbox_and_scale_params(trk):
     assert gain == 1280 / 1920 and pad == (0.0, 280.0)
 
 
+def test_sppcspc_hook_captures_backbone_output(trk):
+    """SPPCSPCHook = YoloDetects.__init__'s hook (yoloDetects2.py:27-34): the first
+    module whose class is named SPPCSPC; its output is kept after each forward."""
+    import torch
+    from importlib import import_module
+    det = import_module(trk.__name__ + ".detect")
+
+    class SPPCSPC(torch.nn.Module):
+        def forward(self, x):
+            return x * 2
+
+    class Head(torch.nn.Module):
+        def forward(self, x):
+            return x.sum(1)
+
+    net = torch.nn.Sequential(torch.nn.Identity(), SPPCSPC(), SPPCSPC(), Head())
+    h = det.SPPCSPCHook(net)
+    x = torch.randn(2, 3, 5, 5)
+    y = net(x)
+    assert torch.equal(h.feat, x * 2) and y.shape == (2, 5, 5)  # the first SPPCSPC's output
+    h.remove()
+    h.feat = None
+    net(x)
+    assert h.feat is None
+    with pytest.raises(ValueError, match="no SPPCSPC"):
+        det.SPPCSPCHook(torch.nn.Sequential(torch.nn.Identity()))
+
+
 def test_det_wrappers_reject_host_tensors(trk):
     import torch
     with pytest.raises(RuntimeError, match="no CPU fallback"):
