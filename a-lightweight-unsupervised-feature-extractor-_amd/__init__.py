@@ -30,4 +30,4 @@ __all__ = ["TrkError", "lib", "header_symbols", "roi_align", "roi_align_from_inp
            "default_cost_params", "CostParams", "hungarian_assign", "cal_cost", "bbox_cost",
            "conf_cost", "Model", "Tracking", "MultiStreamTracker", "TrackTable", "tracker_conf",
            "load_conf", "letterbox_geometry", "scale_coords_params", "non_max_suppression",
-           "det_nms_batched", "YoloPostprocess", "preprocess_roi", "train_rois"]
+           "det_nms_batched", "YoloPostprocess", "preprocess_roi", "train_rois", "SPPCSPCHook"]
