@@ -181,7 +181,8 @@ cost_kernel(const CostArgs A) {
 
   float a[64];
   int iend = min(i0 + kRowsPerWave, M);
-  if (i0 < iend) {
+  const bool chunked = Tmax > 32;  // hist_max > 32: the bank in 32-row MFMA chunks
+  if (i0 < iend && !chunked) {
     const int64_t s0 = slot_of(i0);
     const int T0 = min(A.bank_len[s0], Tmax);
     load_a_frag(A.bank + (s0 * Tmax + col) * D + 64 * h, col < T0, a);
@@ -189,24 +190,29 @@ cost_kernel(const CostArgs A) {
   for (int i = i0; i < iend; ++i) {
     const int64_t slot = slot_of(i);
     const int T = min(A.bank_len[slot], Tmax);
-    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
-    // prefetch the next row's bank while the MFMA chain drains
-    if (i + 1 < iend) {
-      const int64_t sn = slot_of(i + 1);
-      const int Tn = min(A.bank_len[sn], Tmax);
-      load_a_frag(A.bank + (sn * Tmax + col) * D + 64 * h, col < Tn, a);
-    }
-    // ---- top-k over t for column j (torch.topk(dim=0) + mean, :201-203)
+    // ---- top-k over t for column j (torch.topk(dim=0) + mean, :201-203): each lane keeps
+    // the largest of its rows' sims; the selection is order-free, so 32-row chunks give
+    // exactly the single-pass result
     float tk[kMaxTopk];
 #pragma unroll
     for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+    for (int t0 = 0; t0 < (chunked ? T : 1); t0 += 32) {
+      if (chunked) load_a_frag(A.bank + (slot * Tmax + t0 + col) * D + 64 * h, t0 + col < T, a);
+      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int t = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float x = t < T ? acc[r] : -INFINITY;
-      topk_insert(tk, x);
+      for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+      // prefetch the next row's bank while the MFMA chain drains
+      if (!chunked && i + 1 < iend) {
+        const int64_t sn = slot_of(i + 1);
+        const int Tn = min(A.bank_len[sn], Tmax);
+        load_a_frag(A.bank + (sn * Tmax + col) * D + 64 * h, col < Tn, a);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float x = t < T ? acc[r] : -INFINITY;
+        topk_insert(tk, x);
+      }
     }
     float other[kMaxTopk];
 #pragma unroll
@@ -588,7 +594,7 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
                               float* C_conf, void* stream) {
   TRK_REQUIRE(F >= 0 && Mmax >= 0 && Nmax >= 0, "build_cost: negative shape");
   TRK_REQUIRE(host_params, "build_cost: null params");
-  TRK_REQUIRE(Tmax >= 1 && Tmax <= 32, "build_cost: Tmax (hist_max) must be in [1, 32], got %lld",
+  TRK_REQUIRE(Tmax >= 1 && Tmax <= 1024, "build_cost: Tmax (hist_max) must be in [1, 1024], got %lld",
               (long long)Tmax);
   TRK_REQUIRE(host_params->topk >= 0 && host_params->topk <= kMaxTopk,
               "build_cost: topk must be in [0, %d]", kMaxTopk);
@@ -637,7 +643,7 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
     a.C_conf = C_conf ? C_conf + co : nullptr;
     a.p = *host_params;
     const size_t lds2 = c2_lds_bytes((int)Nmax);
-    if (g_cost_v2 && lds2 <= 160 * 1024) {
+    if (g_cost_v2 && lds2 <= 160 * 1024 && Tmax <= 32) {
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(cost2_kernel),
@@ -670,7 +676,7 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
                                   void* stream) {
   TRK_REQUIRE(F >= 0 && Mmax >= 0 && Nmax >= 0, "build_cost_dev: negative shape");
   TRK_REQUIRE(host_params, "build_cost_dev: null params");
-  TRK_REQUIRE(Tmax >= 1 && Tmax <= 32, "build_cost_dev: Tmax (hist_max) must be in [1, 32], got %lld",
+  TRK_REQUIRE(Tmax >= 1 && Tmax <= 1024, "build_cost_dev: Tmax (hist_max) must be in [1, 1024], got %lld",
               (long long)Tmax);
   TRK_REQUIRE(host_params->topk >= 0 && host_params->topk <= kMaxTopk, "build_cost_dev: topk must be in [0, %d]",
               kMaxTopk);
@@ -697,7 +703,7 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
     a.C_total = C_total ? C_total + co : nullptr;
     a.C_app = C_app ? C_app + co : nullptr;
     a.p = *host_params;
-    if (work && !g_cost_v2) {
+    if (work && !g_cost_v2 && Tmax <= 32) {
       // the workspace holds all F frames; this chunk's rows start at frame f0
       Cost3Work w = cost3_work(work, F, Nmax);
       w.prof = g_cost_prof ? g_cost_prof + f0 * ((Mmax + 3) / 4) * 16 : nullptr;

@@ -219,8 +219,8 @@ class MultiStreamTracker:
         self.n_streams = n_streams
         self.device = torch.device(device) if device is not None else _device()
         self.T = int(self.cfg["hist_max"])
-        if self.T > 32:
-            raise NotImplementedError("hist_max > 32 is not supported by the cost kernel")
+        if not 1 <= self.T <= 1024:
+            raise ValueError(f"hist_max must be in [1, 1024], got {self.T}")
         self.table = TrackTable(n_streams, int(capacity), self.T, self.device)
         self.params = default_cost_params(self.cfg, gate=True)
         self.params_nogate = default_cost_params(self.cfg, gate=False)

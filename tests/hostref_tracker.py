@@ -88,8 +88,6 @@ class HostBookkeepingTracker:
         self.cap = capacity
         self.device = torch.device(device) if device is not None else _device()
         self.T = int(self.cfg["hist_max"])
-        if self.T > 32:
-            raise NotImplementedError("hist_max > 32 is not supported by the cost kernel")
         self.table = TrackTable(n_streams * capacity, self.T, self.device)
         self.streams = [StreamState(capacity, s * capacity) for s in range(n_streams)]
         self.params = default_cost_params(self.cfg, gate=True)

@@ -25,9 +25,9 @@ def test_host_side_argument_errors(trk):
                              0, 0, ctypes.c_void_p(8), 1 << 30, None)
     assert rc == -1  # null input pointer with K > 0
     p = trk.default_cost_params()
-    rc = L.trk_build_cost(1, 4, 4, None, None, None, 40, None, None, None, None, None, None, None,
+    rc = L.trk_build_cost(1, 4, 4, None, None, None, 2000, None, None, None, None, None, None, None,
                           None, None, None, ctypes.byref(p), None, None, None, None, None, None)
-    assert rc == -1 and b"Tmax" in L.trk_last_error()
+    assert rc == -1 and b"Tmax" in L.trk_last_error()  # hist_max above 1024
     nr = (ctypes.c_int32 * 1)(5000)
     nc = (ctypes.c_int32 * 1)(5)
     rc = L.trk_lsap(1, ctypes.c_void_p(8), 0, 5, 25000, nr, nc, 5, ctypes.c_void_p(8), ctypes.c_void_p(8),

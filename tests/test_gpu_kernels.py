@@ -315,6 +315,34 @@ def test_cost_dev_bank_resident_vs_det_tile(trk, oracle, gpu):
         assert np.max(np.abs(Ct3[f, :M, :N] - exp["C_total"])) <= 2e-6
 
 
+@pytest.mark.parametrize("Tmax", [33, 50, 96])
+def test_cost_bank_longer_than_32(trk, oracle, gpu, Tmax):
+    """hist_max > 32 (any YAML value, reference mainTracking.py:56): the bank is walked
+    in 32-row MFMA chunks with one running top-k; equal to the oracle, with ragged and
+    empty banks, through both entry points (all five outputs / C_total + C_app)."""
+    rng = np.random.default_rng(Tmax)
+    M, N = 40, 45
+    base = _renorm(rng.standard_normal((M, 128)))
+    bank = _renorm(base[:, None, :] + 0.1 * rng.standard_normal((M, Tmax, 128)))
+    blen = rng.integers(0, Tmax + 1, M).astype(np.int32)
+    blen[:3] = [0, Tmax, 31]
+    bank[np.arange(Tmax)[None, :] >= blen[:, None]] = 0
+    det = rng.standard_normal((N, 128)).astype(np.float32)
+    pbox = _boxes(rng, M)
+    dbox = _boxes(rng, N)
+    lconf = rng.uniform(0.55, 0.99, M).astype(np.float32)
+    dconf = rng.uniform(0.55, 0.99, N).astype(np.float32)
+    x = np.zeros((M, 8)); x[:, :4] = np.stack([(pbox[:, 0] + pbox[:, 2]) / 2, (pbox[:, 1] + pbox[:, 3]) / 2,
+                                               (pbox[:, 2] - pbox[:, 0]) / (pbox[:, 3] - pbox[:, 1]),
+                                               pbox[:, 3] - pbox[:, 1]], 1)
+    gm, gs = oracle.gate_params(x, np.tile(np.diag([10., 10, 10, 10, 1000, 1000, 1000, 1000]), (M, 1, 1)))
+    got = _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf)  # also checks the 2-output path
+    exp = oracle.cost_build(_renorm(bank), blen, det, pbox, dbox, lconf, dconf, gm, gs, np.ones(M, np.int32))
+    assert np.max(np.abs(got["C_app"] - exp["C_app"])) <= 2e-6
+    assert np.array_equal(got["C_total"] >= 1e9, exp["C_total"] >= 1e9)
+    assert np.max(np.abs(got["C_total"] - exp["C_total"])) <= 2e-6
+
+
 def test_costcard_api_vs_reference_golden(trk, gpu):
     d = np.load(os.path.join(GOLDEN, "costcard_golden.npz"))
     for tag in "abc":

@@ -299,3 +299,22 @@ def test_kalman_gate_decisions_at_threshold(trk, oracle, gpu):
         assert res[0].matches.reshape(-1, 2).shape[0] == 1, (nupd, res[0])   # inside: matched
         assert res[1].matches.reshape(-1, 2).shape[0] == 0, (nupd, res[1])   # outside: gated
         assert len(res[1].unmatched_dets) == 1
+
+
+def test_device_step_hist_max_above_32(trk, gpu):
+    """hist_max 40 (> one 32-row MFMA chunk of the cost kernel): banks fill past 32
+    entries over 80 frames; the device tracker equals the host bookkeeping."""
+    import hostref_tracker as H
+    conf = dict(hist_max=40, lost_reid_after=3, max_age=8)
+    rng = np.random.default_rng(41)
+    S = 2
+    frames = [_random_scene(rng, n, 80, p_vis=1.0) for n in (10, 24)]
+    dev = trk.MultiStreamTracker(S, conf, capacity=64, device=gpu)
+    host = H.HostBookkeepingTracker(S, conf, capacity=256, device=gpu)
+    for f in range(80):
+        E, B, C, Ns, confs = _batch(frames, f, gpu)
+        rd = dev.step(E, B, C, Ns, confs, [f] * S)
+        rh = host.step(E, B, C, Ns, confs, [f] * S)
+        for s in range(S):
+            assert _same(rd[s], rh[s]), (f, s)
+    assert int(dev.table.bank_len.max().item()) > 32
