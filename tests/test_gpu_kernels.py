@@ -534,7 +534,7 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
             finally:
                 assert L.trk_set_tuning(b"g1dw_persist", 0) == 0
             assert torch.equal(Yp, Yu) and torch.equal(Yp2, Yu)
-        for mode in (0, 2, 4, 5, 1):   # DMA placement / warp-specialised / 256-wide variants (1: default)
+        for mode in (0, 2, 4, 5, 6, 1):   # DMA placement / warp-specialised / 256-wide / role-split (1: default)
             assert L.trk_set_tuning(b"g1dw_mode", mode) == 0
             assert torch.equal(ops.enc_g1_dwconv(X, W1, wdw), Yu), mode
     for v in (1, 3):

@@ -54,6 +54,8 @@ for name, (fn, dbgs, flops) in items.items():
             L.trk_set_tuning(b"g1dw_mode", off % 10)
         else:
             L.trk_set_tuning(b"enc_gemm_offset", off)
+        if os.environ.get("ENC_DBGS"):
+            dbgs = [int(v) for v in os.environ["ENC_DBGS"].split(",")]
         for d in (dbgs if not os.environ.get("ENC_DBG0") else [0]):
             L.trk_set_tuning(b"enc_gemm_dbg", d)
             t = timeit(fn)
