@@ -32,7 +32,7 @@ import torch
 
 from ._lib import (_STEP_PTRS, TRK_F32, TRK_LSAP_MAX_DIM, StepConfig, StepState, TrkError, check,
                    lib)
-from .ops import (_device, _ptr, _stream, build_cost, cost_combine, default_cost_params,
+from .ops import (_device, _ptr, _stream, current_stream as _current_stream, build_cost, cost_combine, default_cost_params,
                   lsap_batched)
 
 D = 128
@@ -397,12 +397,13 @@ class MultiStreamTracker:
         buf = self._result_buf()
         buf.copy_(sc["result"], non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+        cur = _current_stream(self.device)
+        ev.record(cur)
         check(L.trk_step_apply(fp["st"], fp["cf"], pe, pb, pc, pc64, stream), "step_apply")
         # the caller's detection tensors must outlive the frame's kernels
         for x in (det_emb, dbox, dconf, dconf64):
             if x is not None:
-                x.record_stream(torch.cuda.current_stream(self.device))
+                x.record_stream(cur)
         self._cum_N = self._cum_N + N
         self._seq += 1
         h = StepHandle(self, self._seq, buf, ev, S, Nm, self.cap, self._cum_N.copy())

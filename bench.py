@@ -304,6 +304,7 @@ class LiveProbe:
         # time the pipeline then waited for), handed out in order
         self.pool = [_ev() for _ in range(pool)]
         self.pi = 0
+        self.dev = torch.device("cuda", torch.cuda.current_device())
         self._orig = ops.lib
         probe = self
 
@@ -318,7 +319,7 @@ class LiveProbe:
                 def call(*a):
                     if not probe.on:
                         return fn(*a)
-                    st = torch.cuda.current_stream()
+                    st = ops.current_stream(probe.dev)  # cached Stream object (cheap lookup)
                     if probe.pi + 2 <= len(probe.pool):
                         e0, e1 = probe.pool[probe.pi], probe.pool[probe.pi + 1]
                         probe.pi += 2
