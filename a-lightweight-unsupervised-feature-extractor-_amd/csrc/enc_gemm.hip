@@ -147,7 +147,7 @@ __device__ __forceinline__ int swz(int r, int c) { return r * CPR + (c ^ ((r >> 
 __device__ __forceinline__ int unswz_c(int p) { return (p % CPR) ^ (((p / CPR) >> 2) & 3); }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return (uint32_t)trk::f32_to_bf16(a) | ((uint32_t)trk::f32_to_bf16(b) << 16);
+  return trk::pack2_bf16(a, b);
 }
 
 template <int EPI, int BM_, int BN_>

@@ -31,7 +31,7 @@ template <> struct Pair<uint16_t> {
     b = __uint_as_float(s & 0xffff0000u);
   }
   static __device__ __forceinline__ S pack(float a, float b) {
-    return (uint32_t)trk::f32_to_bf16(a) | ((uint32_t)trk::f32_to_bf16(b) << 16);
+    return trk::pack2_bf16(a, b);
   }
 };
 
@@ -295,7 +295,7 @@ template <> struct Vec16<uint16_t> {
     uint32_t w[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      w[k] = (uint32_t)trk::f32_to_bf16(f[2 * k]) | ((uint32_t)trk::f32_to_bf16(f[2 * k + 1]) << 16);
+      w[k] = trk::pack2_bf16(f[2 * k], f[2 * k + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

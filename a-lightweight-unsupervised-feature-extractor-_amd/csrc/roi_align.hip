@@ -157,12 +157,9 @@ __device__ __forceinline__ void store_nhwc(void* out, int64_t o, const float (&v
   if (OUT_BF16) {
     uint16_t* po = reinterpret_cast<uint16_t*>(out) + o;
     if constexpr (VEC == 4) {
-      *reinterpret_cast<uint2*>(po) = make_uint2(
-          (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16),
-          (uint32_t)trk::f32_to_bf16(v[2]) | ((uint32_t)trk::f32_to_bf16(v[3]) << 16));
+      *reinterpret_cast<uint2*>(po) = make_uint2(trk::pack2_bf16(v[0], v[1]), trk::pack2_bf16(v[2], v[3]));
     } else if constexpr (VEC == 2) {
-      *reinterpret_cast<uint32_t*>(po) =
-          (uint32_t)trk::f32_to_bf16(v[0]) | ((uint32_t)trk::f32_to_bf16(v[1]) << 16);
+      *reinterpret_cast<uint32_t*>(po) = trk::pack2_bf16(v[0], v[1]);
     } else {
       po[0] = trk::f32_to_bf16(v[0]);
     }

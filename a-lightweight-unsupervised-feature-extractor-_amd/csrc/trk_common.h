@@ -33,6 +33,14 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// two floats -> packed bf16 pair (a in the low half), round to nearest even: one
+// v_cvt_pk_bf16_f32 (two f32_to_bf16 + shift/or compile to two conversions and a merge)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+
 constexpr int kWave = 64;
 
 }  // namespace trk
