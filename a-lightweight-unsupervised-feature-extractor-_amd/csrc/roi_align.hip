@@ -555,8 +555,21 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
   kc[0].ca = kc[0].cb = kc[1].ca = kc[1].cb = -1;
   const f2_t Z = {0.f, 0.f}, Q = {0.25f, 0.25f};
   f2_t acc[NH][2], hold[NH][2];
-  uint8_t* obase = reinterpret_cast<uint8_t*>(out) +
-                   ((((int64_t)n * PH + ph) * PW) * C + cbase + lane * 4) * (OUT_BF16 ? 2 : 4);
+  // the wave's output row (PW bins x C channels) as one buffer: the bin's offset is a
+  // scalar (soffset), the lane's channel offset the only per-lane part -- no 64-bit
+  // address arithmetic per store
+  constexpr int EB = OUT_BF16 ? 2 : 4;
+  const uint64_t oa = reinterpret_cast<uint64_t>(out) + ((((uint64_t)n * PH + ph) * PW) * C) * EB;
+  // (readfirstlane returns int: both halves go through uint32_t, or a set bit 31 of the
+  // low half would sign-extend into the high one)
+  const uint32_t oa_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)oa);
+  const uint32_t oa_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(oa >> 32));
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((uint64_t)oa_hi << 32) | oa_lo), 0, __builtin_amdgcn_readfirstlane(PW * C * EB),
+      0x00020000);
+  int ovoff[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) ovoff[h] = (cbase + h * 256 + lane * 4) * EB;
 
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
@@ -625,7 +638,19 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
           v[2 * p] = s.x;
           v[2 * p + 1] = s.y;
         }
-        if (act[h]) store_nhwc<4, OUT_BF16>(obase + ((int64_t)(j >> 1) * C + h * 256) * (OUT_BF16 ? 2 : 4), 0, v);
+        if (act[h]) {
+          const int so_ = __builtin_amdgcn_readfirstlane((j >> 1) * C * EB);
+          if constexpr (OUT_BF16) {
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{trk::pack2_bf16(v[0], v[1]), trk::pack2_bf16(v[2], v[3])},
+                                                  ors, ovoff[h], so_, 0);
+          } else {
+            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_{__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                          __float_as_uint(v[2]), __float_as_uint(v[3])},
+                                                   ors, ovoff[h], so_, 0);
+          }
+        }
       }
     }
   }
