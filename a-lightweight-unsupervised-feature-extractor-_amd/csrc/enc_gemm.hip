@@ -41,9 +41,10 @@ int g_enc_gemm_dbg = 0;     // trk_set_tuning("enc_gemm_dbg"): experiments (1 sk
                             // writes; g1dw: 16 no depthwise, 32 two K steps only)
 int g_g1dw_persist = 0;     // trk_set_tuning("g1dw_persist"): 0 = one workgroup per tile; v > 0 = persistent
                             // tile queue, 2 workgroups per CU, the second started (v - 1) x 2048 cycles late
-int g_g1dw_mode = 1;        // trk_set_tuning("g1dw_mode"): where the K loop issues its LDS-DMA (0 top, 1 after the
-                            // MFMAs, 2 interleaved; 4 = warp-specialised DMA waves; 6 = role-split GEMM /
-                            // depthwise waves); all bit-identical
+int g_g1dw_mode = 7;        // trk_set_tuning("g1dw_mode"): 7 (default) = g1dw4_kernel (4-wave workgroups, 16x16x32
+                            // MFMAs; Y1 summed in another order); the 32x32x16 g1dw_kernel variants, bit-identical
+                            // to each other: where the K loop issues its LDS-DMA (0 top, 1 after the MFMAs,
+                            // 2 interleaved); 4 = warp-specialised DMA waves; 5 = 256-wide N tiles; 6 = role-split
 int g_enc_gemm_offset = 0;  // trk_set_tuning("enc_gemm_offset"): > 0 runs gemm4 persistent (2 workgroups per CU)
                             // with each CU's second workgroup started that many x 2048 cycles late
 
@@ -1786,6 +1787,221 @@ __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t nt
 }
 
 // ---------------------------------------------------------------------------
+// g1dw4 (g1dw_mode 7): g1dw_kernel's first 1x1 convs + depthwise 5x5 on 4-wave
+// workgroups with gemm4's operand image and 16x16x32 MFMAs.  The M tile is two
+// ROIs (200 rows) computed as 13 row tiles of 16 (208 rows; 200..207 belong to
+// the next tile and are discarded -- 4 % padding against g1dw_kernel's 12 %), the
+// N tile 128 channels.  Waves 2 (M) x 2 (N): wave (wr, wc) owns row tiles
+// 7 wr .. 7 wr + 6 (six for wr = 1) x 64 columns, a 112 x 64 wave tile with
+// 11 fragment reads per 28 MFMAs (24 B of LDS reads per kflop; g1dw_kernel's
+// 112 x 32 wave tiles of 32x32x16 read 39).  The K loop is L2->LDS + LDS bound,
+// so bytes per flop is what this variant cuts.  DMA ring as gemm4 (BK 32, three
+// buffers, tile kt + 2 issued after step kt's MFMAs); two workgroups per CU so
+// one's depthwise (VALU) runs under the other's K loop.  Epilogue: Y1 rounded
+// to bf16 pairs into LDS [200][64 pairs] (lane_xor1 pairing as gemm4's staging),
+// depthwise weights behind it, then the 8 (ROI, quadrant) depthwise tasks of
+// g1dw_kernel, two per wave (same FMA order).  Y1 sums its 512 products in
+// another order than the 32x32x16 path, so Y1 (and Y2) may differ from
+// g1dw_kernel's by bf16 rounding of f32 ties; tested against the fp32 GEMM.
+constexpr int G1Q_ROWS = 208;                                   // 13 row tiles of 16
+constexpr int G1Q_AP = G1Q_ROWS * 4;                            // A 16-B slots per buffer (832)
+constexpr int G1Q_BUF = G1Q_AP + G1_BN * 4;                     // + B (512) = 1344 slots
+constexpr size_t G1Q_RING = (size_t)3 * G1Q_BUF * 16;           // 63 KiB
+constexpr size_t G1Q_LDS = G1Q_RING > G1_TILE ? G1Q_RING : G1_TILE;   // Y1 reuses the ring
+static_assert(2 * G1Q_LDS <= 160 * 1024, "two g1dw4 workgroups per CU");
+
+// Depthwise 5x5 of one 5x5 output quadrant (QY, QX) of a 10x10 ROI for the lane's
+// channel pair, weights in registers, all 25 accumulators live: each input row of the
+// quadrant's (clipped) 7 x 7 window is read from LDS and unpacked once (dw5_block reads
+// the window's rows in two overlapping blocks).  Same per-output order as dw5_block
+// (ascending input row, then ascending kx), so equal Y1 gives equal Y2.
+template <int QY, int QX>
+__device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, const dw_pair_t (&w)[25],
+                                          uint32_t* __restrict__ dst, int ldd) {
+  constexpr int OY0 = 5 * QY, X0 = 5 * QX;
+  constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY0 + 6 > G1_S - 1 ? G1_S - 1 : OY0 + 6;
+  constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
+  constexpr int NX = IX1 - IX0 + 1;
+  dw_pair_t acc[5][5];
+#pragma unroll
+  for (int oy = 0; oy < 5; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) acc[oy][ox] = dw_pair_t{0.f, 0.f};
+  uint32_t nxt[NX];
+#pragma unroll
+  for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(IY0 * G1_S + IX0 + ix) * (G1_BN / 2)];
+#pragma unroll
+  for (int iy = IY0; iy <= IY1; ++iy) {
+    dw_pair_t in[NX];
+#pragma unroll
+    for (int ix = 0; ix < NX; ++ix) in[ix] = dw_pair_t{__uint_as_float(nxt[ix] << 16), __uint_as_float(nxt[ix] & 0xffff0000u)};
+    if (iy < IY1) {
+#pragma unroll
+      for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[((iy + 1) * G1_S + IX0 + ix) * (G1_BN / 2)];
+    }
+#pragma unroll
+    for (int oy = 0; oy < 5; ++oy) {
+      const int ky = iy - (OY0 + oy) + 2;
+      if (ky < 0 || ky > 4) continue;
+#pragma unroll
+      for (int ox = 0; ox < 5; ++ox)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) {
+          const int ix = X0 + ox + kx - 2;
+          if (ix >= IX0 && ix <= IX1)
+            acc[oy][ox] = __builtin_elementwise_fma(w[ky * 5 + kx], in[ix - IX0], acc[oy][ox]);
+        }
+    }
+  }
+#pragma unroll
+  for (int oy = 0; oy < 5; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) {
+      const uint32_t v = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
+      if (ldd > 0) dst[((OY0 + oy) * G1_S + X0 + ox) * ldd] = v;
+      else asm volatile("" ::"v"(v));  // experiment (enc_gemm_dbg 256): no Y2 stores
+    }
+}
+
+__global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
+                                                        const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
+                                                        int M, int N, int dbg) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint4* ring = reinterpret_cast<uint4*>(smem);
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntile_n = N / G1_BN;
+  const int n0 = (int)(lb % ntile_n) * G1_BN;
+  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);
+  constexpr int K = 512, NK = K / BK;
+
+  // DMA: A slots p = q * 256 + tid (q = 0..2 every wave, q = 3 wave 0 only: 832 slots),
+  // B slots 832 + q * 256 + tid (q = 0, 1); slot p holds row p >> 2, chunk (p & 3) ^ x16(row)
+  const uint16_t* asrc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = min(q * 256 + tid, G1Q_AP - 1), r = p >> 2, c = (p & 3) ^ x16(r);
+    asrc[q] = X + min(m0 + r, (int64_t)M - 1) * K + c * 8;
+  }
+  const uint16_t* bsrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x16(r);
+    bsrc[q] = W1 + (int64_t)(n0 + r) * K + c * 8;
+  }
+  auto issue = [&](int kt) {
+    if (dbg & 128) return;  // experiment: no operand loads
+    uint4* d = ring + (kt % 3) * G1Q_BUF + wave * 64;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
+    if (wave == 0) __builtin_amdgcn_global_load_lds(GPTR(asrc[3] + kt * BK), LPTR(d + 3 * 256), 16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + kt * BK), LPTR(d + G1Q_AP + q * 256), 16, 0, 0);
+  };
+  // retire all but the newest stage's DMA ops (wave 0 issues 6 per stage, the others 5)
+  auto wait_prev = [&]() {
+    if (dbg & 128) return;
+    if (wave == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  };
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int lterm = fr * 4 + (fc ^ x16(fr));
+  const int aoff = (wr * 112) * 4 + lterm;           // + i * 64
+  const int boff = G1Q_AP + (wc * 64) * 4 + lterm;   // + t * 64
+  const int ntm = wr == 0 ? 7 : 6;
+
+  f4v acc[7][4];
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (dbg & 32) ? 2 : NK;
+  issue(0);
+  issue(1);
+  wait_prev();
+  g4_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint4* buf = ring + (kt % 3) * G1Q_BUF;
+    if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
+      bf8v bfr[4], afr[7];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bfr[t] = *reinterpret_cast<const bf8v*>(buf + boff + t * 64);
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+        if (i < ntm) afr[i] = *reinterpret_cast<const bf8v*>(buf + aoff + i * 64);
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+        if (i < ntm)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[t], acc[i][t], 0, 0, 0);
+    }
+    if (kt + 2 < nk) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 2);
+    }
+    if (kt + 1 < nk) {
+      if (kt + 2 < nk) wait_prev();
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    g4_barrier();
+  }
+
+  // depthwise weights: every wave needs the same 25 taps of its lane's channel pair, so
+  // each lane loads them straight into registers (issued now, used after the Y1 writes)
+  dw_pair_t wreg[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) wreg[k] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * lane);
+  // Y1 (bf16 pairs, rows < 200) -> LDS [200][64]: lane pairs (fr, fr ^ 1) trade values so each
+  // lane writes two column pairs: even fr rows +0, +1, odd fr rows +2, +3 (as gemm4's staging)
+  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
+  {
+    const bool odd = fr & 1;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+      if (i < ntm)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f4v v = acc[i][t];
+          const float x0 = lane_xor1(odd ? v[0] : v[2]);
+          const float x1 = lane_xor1(odd ? v[1] : v[3]);
+          const int rb = wr * 112 + i * 16 + fc * 4 + (odd ? 2 : 0);
+          const int cp = (wc * 64 + t * 16 + fr) >> 1;
+          if (rb < 2 * G1_P) y1[rb * (G1_BN / 2) + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
+          if (rb + 1 < 2 * G1_P) y1[(rb + 1) * (G1_BN / 2) + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+        }
+  }
+  __syncthreads();
+
+  if (dbg & 16) return;
+  // depthwise 5x5: wave = output quadrant, for each of the two ROIs; lane = channel pair
+  const int ldd = (dbg & 256) ? 0 : N / 2;
+#pragma unroll 1
+  for (int roi = 0; roi < 2; ++roi) {
+    const int64_t rbase = m0 + roi * G1_P;
+    if (rbase >= M) break;
+    int l = ldd;
+    asm volatile("" : "+s"(l));  // per ROI: keeps the 25 store offsets out of the loop (SGPR spills)
+    const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2) + lane;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0) + lane;
+    switch (wave) {
+      case 0: dw5q_regs<0, 0>(src, wreg, dst, l); break;
+      case 1: dw5q_regs<0, 1>(src, wreg, dst, l); break;
+      case 2: dw5q_regs<1, 0>(src, wreg, dst, l); break;
+      default: dw5q_regs<1, 1>(src, wreg, dst, l); break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // gemm8: 256 x 256 tiles, BK = 64, one 8-wave workgroup per CU (waves 2 (M) x 4
 // (N), wave tile 128 x 64 = 8 x 4 MFMA 16x16x32 tiles: 0.375 KB of fragment
 // reads per MFMA).  Both operands are staged by LDS-DMA into two 64 KiB K-tile
@@ -2324,6 +2540,17 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
     hipLaunchKernelGGL(g1dw256_kernel, dim3((unsigned)nwg2), dim3(1024), G2_LDS, st, (const uint16_t*)X,
                        (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
     return trk::check_launch("g1dw256_kernel");
+  }
+  if (g_g1dw_mode == 7) {   // 4-wave workgroups, 112 x 64 wave tiles of 16x16x32
+    static bool attr_q = false;
+    if (!attr_q) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
+      attr_q = true;
+    }
+    hipLaunchKernelGGL(g1dw4_kernel, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st, (const uint16_t*)X,
+                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
+    return trk::check_launch("g1dw4_kernel");
   }
   if (g_g1dw_mode == 4) {
     TRK_REQUIRE(M * 512 < (int64_t)1 << 31, "enc_g1_dwconv: M * 512 must stay below 2^31");

@@ -64,5 +64,5 @@ for name, (fn, dbgs, flops) in items.items():
 L.trk_set_tuning(b"enc_gemm_dbg", 0)
 L.trk_set_tuning(b"enc_gemm_offset", 0)
 L.trk_set_tuning(b"g1dw_persist", 0)
-L.trk_set_tuning(b"g1dw_mode", 1)
+L.trk_set_tuning(b"g1dw_mode", 7)
 torch.cuda.synchronize()

@@ -15,7 +15,7 @@ def short(n):
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 k0 = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 nk = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-marks = [i for i, r in enumerate(rows) if "g1dw_kernel" in r["Kernel_Name"]]
+marks = [i for i, r in enumerate(rows) if "g1dw" in r["Kernel_Name"]]
 print(f"{len(rows)} kernels, {len(marks)} g1dw launches")
 for s in range(k0, min(k0 + nk, len(marks) - 1)):
     a, b = marks[s], marks[s + 1]
