@@ -1930,18 +1930,31 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
   for (int kt = 0; kt < nk; ++kt) {
     const uint4* buf = ring + (kt % 3) * G1Q_BUF;
     if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
-      bf8v bfr[4], afr[7];
+      // 11 fragment reads up front (wr = 1's seventh reads B slots, unused), then counted
+      // lgkmcnt waits: row tile i's MFMAs start once its A fragment has landed
+      const uint32_t bb = lds_addr(buf + boff), ab = lds_addr(buf + aoff);
+      u32x4 bq[4], aq[7];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bfr[t] = *reinterpret_cast<const bf8v*>(buf + boff + t * 64);
+      for (int t = 0; t < 4; ++t) bq[t] = lds_read128(bb + t * 1024);
 #pragma unroll
-      for (int i = 0; i < 7; ++i)
-        if (i < ntm) afr[i] = *reinterpret_cast<const bf8v*>(buf + aoff + i * 64);
+      for (int i = 0; i < 7; ++i) aq[i] = lds_read128(ab + i * 1024);
 #pragma unroll
-      for (int i = 0; i < 7; ++i)
-        if (i < ntm)
+      for (int i = 0; i < 7; ++i) {
+        __builtin_amdgcn_sched_barrier(0);  // keep each wait in front of its own row tile's MFMAs
+        if (i == 0) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(aq[0]));
+        else if (i == 1) asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(aq[1]));
+        else if (i == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(aq[2]));
+        else if (i == 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(aq[3]));
+        else if (i == 4) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(aq[4]));
+        else if (i == 5) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(aq[5]));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(aq[6]));
+        if (i < ntm) {
+          const bf8v a = __builtin_bit_cast(bf8v, aq[i]);
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[t], acc[i][t], 0, 0, 0);
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf8v, bq[t]), acc[i][t], 0, 0, 0);
+        }
+      }
     }
     if (kt + 2 < nk) {
       __builtin_amdgcn_sched_barrier(0);
