@@ -83,6 +83,17 @@ __device__ __forceinline__ void topk_insert(float (&v)[kMaxTopk], float x) {
     v[q] = hi;
   }
 }
+// the same network on the first KT slots only: slot q depends on slots <= q and x,
+// so the first KT slots equal topk_insert's (cost3 with topk <= 5: 10 ops instead of 16)
+template <int KT>
+__device__ __forceinline__ void topk_insert_k(float (&v)[kMaxTopk], float x) {
+#pragma unroll
+  for (int q = 0; q < KT; ++q) {
+    float hi = fmaxf(v[q], x);
+    x = fminf(v[q], x);
+    v[q] = hi;
+  }
+}
 
 // costCard.bbox_cost / conf_cost / cal_cost C_total (costCard.py:141-168,
 // :196-201, :264-268) + the Mahalanobis gate (mainTracking.py:327-336) for one
@@ -430,6 +441,8 @@ __device__ __forceinline__ void load_b_tile(const float* dnf, int j, int N, int 
   }
 }
 
+// KT: top-k network length (5 when the requested topk <= 5 -- the YAML's 5 -- else kMaxTopk)
+template <int KT>
 __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const Cost3Work w) {
   const int f = blockIdx.y;
   const int lane = threadIdx.x & 63;
@@ -494,17 +507,17 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
-      topk_insert(tk, tr < T ? acc[r] : -INFINITY);
+      topk_insert_k<KT>(tk, tr < T ? acc[r] : -INFINITY);
     }
-    float other[kMaxTopk];
+    float other[KT];
 #pragma unroll
-    for (int q = 0; q < kMaxTopk; ++q) other[q] = __shfl_xor(tk[q], 32);
+    for (int q = 0; q < KT; ++q) other[q] = __shfl_xor(tk[q], 32);
 #pragma unroll
-    for (int q = 0; q < kMaxTopk; ++q) topk_insert(tk, other[q]);
+    for (int q = 0; q < KT; ++q) topk_insert_k<KT>(tk, other[q]);
     const int k = min(topk, T);
     float sum = 0.f;
 #pragma unroll
-    for (int q = 0; q < kMaxTopk; ++q)
+    for (int q = 0; q < KT; ++q)
       if (q < k) sum = sum + tk[q];
     const float app = k <= 0 ? 1.0f : 1.0f - sum / (float)k;
     if (w.prof) {
@@ -711,7 +724,10 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
       w.dt += f0 * Nmax;
       hipLaunchKernelGGL(det_prep_kernel, dim3((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf), dim3(256), 0, st, a, w);
       if (int e = trk::check_launch("det_prep_kernel")) return e;
-      hipLaunchKernelGGL(cost3_kernel, dim3((unsigned)((Mmax + 3) / 4), (unsigned)nf), dim3(256), 0, st, a, w);
+      if (host_params->topk <= 5)
+        hipLaunchKernelGGL(cost3_kernel<5>, dim3((unsigned)((Mmax + 3) / 4), (unsigned)nf), dim3(256), 0, st, a, w);
+      else
+        hipLaunchKernelGGL(cost3_kernel<kMaxTopk>, dim3((unsigned)((Mmax + 3) / 4), (unsigned)nf), dim3(256), 0, st, a, w);
       if (int e = trk::check_launch("cost3_kernel")) return e;
       continue;
     }

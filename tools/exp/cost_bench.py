@@ -30,16 +30,19 @@ L = trk.lib()
 P = ops._ptr
 prm = trk.default_cost_params(gate=True)
 work = torch.empty(int(L.trk_cost_work_bytes(F, N)), device=dev, dtype=torch.uint8)
-def run(w):
+prm8 = trk.default_cost_params(gate=True)
+prm8.topk = 8   # timing only: cost3's 8-slot top-k network (topk <= 5 runs the 5-slot one)
+def run(w, pr=prm):
     assert L.trk_build_cost_dev(F, M, N, P(Ms), P(Ns), P(slots), M, T, P(bank), P(blen), P(pbox), P(lconf), P(gm),
-                                P(gs), P(gon), P(det), P(dbox), P(dconf), ctypes.byref(prm), P(C), None,
+                                P(gs), P(gon), P(det), P(dbox), P(dconf), ctypes.byref(pr), P(C), None,
                                 P(w) if w is not None else None, ops._stream(dev)) == 0
-for name, w in (("cost_kernel", None), ("cost3", work)) * 2:
-    for _ in range(3): run(w)
+for name, w, pr in (("cost_kernel", None, prm), ("cost3", work, prm), ("cost3_topk8", work, prm8)) * 2:
+    run_ = lambda w: run(w, pr)
+    for _ in range(3): run_(w)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(20): run(w)
+    for _ in range(20): run_(w)
     e1.record(); torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 20 * 1e3
     flop = 2.0 * F * M * N * 32 * 128
