@@ -1807,7 +1807,13 @@ constexpr int G1Q_ROWS = 208;                                   // 13 row tiles 
 constexpr int G1Q_AP = G1Q_ROWS * 4;                            // A 16-B slots per buffer (832)
 constexpr int G1Q_BUF = G1Q_AP + G1_BN * 4;                     // + B (512) = 1344 slots
 constexpr size_t G1Q_RING = (size_t)3 * G1Q_BUF * 16;           // 63 KiB
-constexpr size_t G1Q_LDS = G1Q_RING > G1_TILE ? G1Q_RING : G1_TILE;   // Y1 reuses the ring
+// Y1 rows of 64 bf16 pairs at a 68-dword stride: a Y1 store's 32-lane group writes rows
+// {0, 2, 4, 6} + base x 8 consecutive pairs, which the 4-dword row shift spreads over all 32
+// banks (a 64-dword stride put the four rows on the same 8 banks: 4-way conflicts); the
+// depthwise reads 64 consecutive dwords of one row either way
+constexpr int G1Q_YS = 68;
+constexpr size_t G1Q_Y1 = (size_t)2 * G1_P * G1Q_YS * 4;
+constexpr size_t G1Q_LDS = G1Q_RING > G1Q_Y1 ? G1Q_RING : G1Q_Y1;   // Y1 reuses the ring
 static_assert(2 * G1Q_LDS <= 160 * 1024, "two g1dw4 workgroups per CU");
 
 // Depthwise 5x5 of one 5x5 output quadrant (QY, QX) of a 10x10 ROI for the lane's
@@ -1815,7 +1821,7 @@ static_assert(2 * G1Q_LDS <= 160 * 1024, "two g1dw4 workgroups per CU");
 // quadrant's (clipped) 7 x 7 window is read from LDS and unpacked once (dw5_block reads
 // the window's rows in two overlapping blocks).  Same per-output order as dw5_block
 // (ascending input row, then ascending kx), so equal Y1 gives equal Y2.
-template <int QY, int QX>
+template <int QY, int QX, int YS>
 __device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, const dw_pair_t (&w)[25],
                                           uint32_t* __restrict__ dst, int ldd) {
   constexpr int OY0 = 5 * QY, X0 = 5 * QX;
@@ -1829,7 +1835,7 @@ __device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, cons
     for (int ox = 0; ox < 5; ++ox) acc[oy][ox] = dw_pair_t{0.f, 0.f};
   uint32_t nxt[NX];
 #pragma unroll
-  for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(IY0 * G1_S + IX0 + ix) * (G1_BN / 2)];
+  for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(IY0 * G1_S + IX0 + ix) * YS];
 #pragma unroll
   for (int iy = IY0; iy <= IY1; ++iy) {
     dw_pair_t in[NX];
@@ -1837,20 +1843,26 @@ __device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, cons
     for (int ix = 0; ix < NX; ++ix) in[ix] = dw_pair_t{__uint_as_float(nxt[ix] << 16), __uint_as_float(nxt[ix] & 0xffff0000u)};
     if (iy < IY1) {
 #pragma unroll
-      for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[((iy + 1) * G1_S + IX0 + ix) * (G1_BN / 2)];
+      for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[((iy + 1) * G1_S + IX0 + ix) * YS];
     }
+    // groups of up to 5 independent FMAs (the 5 outputs of a row for one tap), each group
+    // closed by an empty asm on its accumulators: left to itself the compiler ran every
+    // output's taps as one dependent chain (an s_nop between dependent v_pk_fma_f32) at 2
+    // waves per SIMD (a sched_barrier alone does not hold: the FMAs have no chain edge)
 #pragma unroll
     for (int oy = 0; oy < 5; ++oy) {
       const int ky = iy - (OY0 + oy) + 2;
       if (ky < 0 || ky > 4) continue;
 #pragma unroll
-      for (int ox = 0; ox < 5; ++ox)
+      for (int kx = 0; kx < 5; ++kx) {
 #pragma unroll
-        for (int kx = 0; kx < 5; ++kx) {
+        for (int ox = 0; ox < 5; ++ox) {
           const int ix = X0 + ox + kx - 2;
           if (ix >= IX0 && ix <= IX1)
             acc[oy][ox] = __builtin_elementwise_fma(w[ky * 5 + kx], in[ix - IX0], acc[oy][ox]);
         }
+        asm volatile("" : "+v"(acc[oy][0]), "+v"(acc[oy][1]), "+v"(acc[oy][2]), "+v"(acc[oy][3]), "+v"(acc[oy][4]));
+      }
     }
   }
 #pragma unroll
@@ -1988,8 +2000,8 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
           const float x1 = lane_xor1(odd ? v[1] : v[3]);
           const int rb = wr * 112 + i * 16 + fc * 4 + (odd ? 2 : 0);
           const int cp = (wc * 64 + t * 16 + fr) >> 1;
-          if (rb < 2 * G1_P) y1[rb * (G1_BN / 2) + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
-          if (rb + 1 < 2 * G1_P) y1[(rb + 1) * (G1_BN / 2) + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+          if (rb < 2 * G1_P) y1[rb * G1Q_YS + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
+          if (rb + 1 < 2 * G1_P) y1[(rb + 1) * G1Q_YS + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
         }
   }
   __syncthreads();
@@ -2003,13 +2015,13 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
     if (rbase >= M) break;
     int l = ldd;
     asm volatile("" : "+s"(l));  // per ROI: keeps the 25 store offsets out of the loop (SGPR spills)
-    const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2) + lane;
+    const uint32_t* src = y1 + roi * G1_P * G1Q_YS + lane;
     uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0) + lane;
     switch (wave) {
-      case 0: dw5q_regs<0, 0>(src, wreg, dst, l); break;
-      case 1: dw5q_regs<0, 1>(src, wreg, dst, l); break;
-      case 2: dw5q_regs<1, 0>(src, wreg, dst, l); break;
-      default: dw5q_regs<1, 1>(src, wreg, dst, l); break;
+      case 0: dw5q_regs<0, 0, G1Q_YS>(src, wreg, dst, l); break;
+      case 1: dw5q_regs<0, 1, G1Q_YS>(src, wreg, dst, l); break;
+      case 2: dw5q_regs<1, 0, G1Q_YS>(src, wreg, dst, l); break;
+      default: dw5q_regs<1, 1, G1Q_YS>(src, wreg, dst, l); break;
     }
   }
 }
