@@ -45,6 +45,8 @@ int g_g1dw_mode = 7;        // trk_set_tuning("g1dw_mode"): 7 (default) = g1dw4_
                             // MFMAs; Y1 summed in another order); the 32x32x16 g1dw_kernel variants, bit-identical
                             // to each other: where the K loop issues its LDS-DMA (0 top, 1 after the MFMAs,
                             // 2 interleaved); 4 = warp-specialised DMA waves; 5 = 256-wide N tiles; 6 = role-split
+int g_dsc_split = 1;        // trk_set_tuning("dsc_split"): 1 = gemm4's DSC tiles compiled per activation (SiLU /
+                            // Hardswish), 0 = one tile body with a per-element select
 int g_enc_gemm_offset = 0;  // trk_set_tuning("enc_gemm_offset"): > 0 runs gemm4 persistent (2 workgroups per CU)
                             // with each CU's second workgroup started that many x 2048 cycles late
 
@@ -98,6 +100,7 @@ struct EncGemmArgs {
   const float* scale;      // EPI_TRANS: s [nroi][kscale]
   int M, N, K, P, groups, kscale;
   int dbg;                 // g_enc_gemm_dbg
+  int hsplit;              // g_dsc_split: gemm4 DSC tiles instantiated per activation
   unsigned long long* prof;  // trk_enc_set_prof (gemm4: per-workgroup phase stamps; diagnostics)
 };
 
@@ -1465,7 +1468,7 @@ static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
 
 // WIDE (P >= 64): a wave's 64 rows span at most 2 ROIs and a tile's 128 at most 3, so
 // the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions)
-template <int EPI, bool WIDE = false>
+template <int EPI, bool WIDE = false, int HSWM = -1>
 __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, unsigned char* smem) {
   uint4* ring = reinterpret_cast<uint4*>(smem);
   // opaque per tile: keeps the compiler from hoisting lane-dependent addresses
@@ -1621,7 +1624,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   }
   // ---- epilogue (the ring is free: every DMA retired, all reads done at the last barrier)
   const int colq = wc * 128 + fr;  // + t * 16
-  const bool hsw = EPI == EPI_DSC && g == 1;
+  // HSWM: -1 = the DSC group decides per tile (a select per element pair, which the compiler
+  // turns into 64 branches, each a dependent exp / rcp chain padded with s_nops); 0 / 1 = the
+  // tile's activation is known at compile time (straight-line SiLU or Hardswish)
+  const bool hsw = HSWM < 0 ? (EPI == EPI_DSC && g == 1) : HSWM == 1;
   float bias8[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) bias8[t] = a.bias[g * a.N + n0 + colq + t * 16];  // one batch of loads
@@ -1770,7 +1776,13 @@ template <int EPI, bool WIDE>
 __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles, int offset, int qslot) {
   extern __shared__ __align__(16) unsigned char smem[];
   if (qslot < 0) {  // one workgroup per tile
-    gemm4_tile<EPI, WIDE>(a, xcd_remap(blockIdx.x, ntiles), smem);
+    const int64_t lb = xcd_remap(blockIdx.x, ntiles);
+    if (EPI == EPI_DSC && a.hsplit) {  // the tile's group (SiLU / Hardswish) as a template argument
+      if ((lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1>(a, lb, smem);
+      else gemm4_tile<EPI, WIDE, 0>(a, lb, smem);
+    } else {
+      gemm4_tile<EPI, WIDE>(a, lb, smem);
+    }
     return;
   }
   const TileQueue tq{g_tileq[qslot], ntiles};
@@ -2409,6 +2421,7 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   }
   EncGemmArgs b = a;
   b.dbg = g_enc_gemm_dbg;
+  b.hsplit = g_dsc_split;
   b.prof = g_enc_prof;
   const int qs = g_enc_gemm_offset > 0 ? next_queue_slot() : -1;
   if (a.P >= 64 && !g_enc_g4_narrow)

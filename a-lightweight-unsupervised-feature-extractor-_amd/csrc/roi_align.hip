@@ -748,6 +748,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "roi_window_kb")) { TRK_REQUIRE(value >= 0 && value <= 150, "roi_window_kb in [0,150]"); g_roi_window_kb = value; return TRK_OK; }
   if (!strcmp(key, "roi_sweep")) { TRK_REQUIRE(value >= 0 && value <= 2, "roi_sweep in {0,1,2}"); g_roi_sweep = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm_offset")) { extern int g_enc_gemm_offset; TRK_REQUIRE(value >= 0 && value <= 64, "enc_gemm_offset in [0, 64]"); g_enc_gemm_offset = value; return TRK_OK; }
+  if (!strcmp(key, "dsc_split")) { extern int g_dsc_split; TRK_REQUIRE(value == 0 || value == 1, "dsc_split in {0, 1}"); g_dsc_split = value; return TRK_OK; }
   if (!strcmp(key, "g1dw_persist")) { extern int g_g1dw_persist; TRK_REQUIRE(value >= 0 && value <= 66, "g1dw_persist in [0, 66]"); g_g1dw_persist = value; return TRK_OK; }
   if (!strcmp(key, "g1dw_mode")) { extern int g_g1dw_mode; TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 5 || value == 6 || value == 7, "g1dw_mode in {0, 1, 2, 4, 5, 6, 7}"); g_g1dw_mode = value; return TRK_OK; }
   if (!strcmp(key, "enc_g4_narrow")) { extern int g_enc_g4_narrow; TRK_REQUIRE(value == 0 || value == 1, "enc_g4_narrow in {0, 1}"); g_enc_g4_narrow = value; return TRK_OK; }
