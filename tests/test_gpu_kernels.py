@@ -562,6 +562,14 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         finally:
             assert L.trk_set_tuning(b"enc_gemm_offset", 0) == 0
         assert torch.equal(XRNp, XRN) and torch.equal(srp, sr) and torch.equal(snp, sn) and torch.equal(stp, st)
+    # DSC tiles compiled per activation (dsc_split 1, the default) == one body with a per-element
+    # select (dsc_split 0): the same operations on every element
+    try:
+        assert L.trk_set_tuning(b"dsc_split", 0) == 0
+        XRNs, srs, sns = ops.enc_dsc_gemm(Y2, P, W2, b2)
+    finally:
+        assert L.trk_set_tuning(b"dsc_split", 1) == 0
+    assert torch.equal(XRNs, XRN) and torch.equal(srs, sr) and torch.equal(sns, sn)
 
 
 def _partials(total, P, parts=3):
