@@ -95,6 +95,19 @@ __device__ __forceinline__ void topk_insert_k(float (&v)[kMaxTopk], float x) {
   }
 }
 
+// torch's clamp(min=lo): a NaN stays NaN (fmaxf would return lo), so a NaN box or
+// confidence reaches C_total and the solver raises as scipy does
+__device__ __forceinline__ float clamp_lo(float x, float lo) { return x < lo ? lo : x; }
+
+// torch.topk treats NaN as the largest value, so a NaN similarity (a NaN embedding)
+// is always among the top k and makes the mean NaN; the max / min network drops
+// NaNs, so the kernels carry a per-column NaN flag beside it.  nan: this lane's
+// flag; the column's two lane halves (col, col + 32) are merged here.
+__device__ __forceinline__ float app_nan(float app, bool nan, int col) {
+  const unsigned long long b = __ballot(nan);
+  return ((b >> col) & 1ull) | ((b >> (col + 32)) & 1ull) ? __builtin_nanf("") : app;
+}
+
 // costCard.bbox_cost / conf_cost / cal_cost C_total (costCard.py:141-168,
 // :196-201, :264-268) + the Mahalanobis gate (mainTracking.py:327-336) for one
 // (track, detection) pair.  Track-side inputs are wave-uniform.
@@ -105,14 +118,14 @@ __device__ __forceinline__ float combine(const trk_cost_params& p, float app, co
                                          float& cf) {
   const float px1 = bp[0], py1 = bp[1], px2 = bp[2], py2 = bp[3];
   const float cpx = 0.5f * (px1 + px2), cpy = 0.5f * (py1 + py2);
-  const float wp = fmaxf(px2 - px1, 1.0f), hp = fmaxf(py2 - py1, 1.0f);
-  const float sp = fmaxf(sqrtf(wp * wp + hp * hp), 1.0f);
+  const float wp = clamp_lo(px2 - px1, 1.0f), hp = clamp_lo(py2 - py1, 1.0f);
+  const float sp = clamp_lo(sqrtf(wp * wp + hp * hp), 1.0f);
   const float Ap = wp * hp;
-  const float cpv = fmaxf(conf_prev, 1e-6f);
+  const float cpv = clamp_lo(conf_prev, 1e-6f);
   const float dx = cpx - ccx, dy = cpy - ccy;
   const float dist = sqrtf(fmaf(dy, dy, dx * dx));  // torch.norm CPU rounding
   cen = dist / sp;
-  scl = fabsf(logf(fmaxf(Ac / Ap, 1e-6f)));
+  scl = fabsf(logf(clamp_lo(Ac / Ap, 1e-6f)));
   cf = fabsf(logf(ccv / cpv));
   const float bbox = p.alpha * cen + p.beta * scl;
   float tot = p.w_app * app + p.w_bbox * bbox;
@@ -140,9 +153,9 @@ __device__ __forceinline__ void det_terms(const float* bc, float conf, float& cc
   const float x1 = bc[0], y1 = bc[1], x2 = bc[2], y2 = bc[3];
   ccx = 0.5f * (x1 + x2);
   ccy = 0.5f * (y1 + y2);
-  const float wc = fmaxf(x2 - x1, 1.0f), hc = fmaxf(y2 - y1, 1.0f);
+  const float wc = clamp_lo(x2 - x1, 1.0f), hc = clamp_lo(y2 - y1, 1.0f);
   Ac = wc * hc;
-  ccv = fmaxf(conf, 1e-6f);
+  ccv = clamp_lo(conf, 1e-6f);
   const double dx1 = x1, dy1 = y1, dx2 = x2, dy2 = y2;
   const double w = fmax(dx2 - dx1, 1.0), hh = fmax(dy2 - dy1, 1.0);
   z0 = (float)(dx1 + 0.5 * w);
@@ -207,6 +220,7 @@ cost_kernel(const CostArgs A) {
     float tk[kMaxTopk];
 #pragma unroll
     for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+    bool nan = false;
     for (int t0 = 0; t0 < (chunked ? T : 1); t0 += 32) {
       if (chunked) load_a_frag(A.bank + (slot * Tmax + t0 + col) * D + 64 * h, t0 + col < T, a);
       f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -222,6 +236,7 @@ cost_kernel(const CostArgs A) {
       for (int r = 0; r < 16; ++r) {
         const int t = t0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float x = t < T ? acc[r] : -INFINITY;
+        nan |= __builtin_isnan(x);
         topk_insert(tk, x);
       }
     }
@@ -241,6 +256,7 @@ cost_kernel(const CostArgs A) {
         if (q < k) sum = sum + tk[q];
       app = 1.0f - sum / (float)k;
     }
+    app = app_nan(app, nan && k > 0, col);
     if (h != 0 || !jok) continue;
 
     float cen, scl, cf;
@@ -332,10 +348,13 @@ __global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
     float tk[kMaxTopk];
 #pragma unroll
     for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+    bool nan = false;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int t = (r & 3) + 8 * (r >> 2) + 4 * h;
-      topk_insert(tk, t < T ? acc[r] : -INFINITY);
+      const float x = t < T ? acc[r] : -INFINITY;
+      nan |= __builtin_isnan(x);
+      topk_insert(tk, x);
     }
     float other[kMaxTopk];
 #pragma unroll
@@ -353,6 +372,7 @@ __global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
         if (q < k) sum = sum + tk[q];
       app = 1.0f - sum / (float)k;
     }
+    app = app_nan(app, nan && k > 0, col);
     if (h != 0 || !jok) continue;
     const DetTerms t = dt_lds[j];
     float cen, scl, cf;
@@ -504,10 +524,13 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
     float tk[kMaxTopk];
 #pragma unroll
     for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+    bool nan = false;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
-      topk_insert_k<KT>(tk, tr < T ? acc[r] : -INFINITY);
+      const float x = tr < T ? acc[r] : -INFINITY;
+      nan |= __builtin_isnan(x);
+      topk_insert_k<KT>(tk, x);
     }
     float other[KT];
 #pragma unroll
@@ -519,7 +542,7 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
 #pragma unroll
     for (int q = 0; q < KT; ++q)
       if (q < k) sum = sum + tk[q];
-    const float app = k <= 0 ? 1.0f : 1.0f - sum / (float)k;
+    const float app = app_nan(k <= 0 ? 1.0f : 1.0f - sum / (float)k, nan && k > 0, col);
     if (w.prof) {
       asm volatile("" ::"v"(app));
       const unsigned long long t1 = c3_stamp();

@@ -98,6 +98,40 @@ nchw_to_nhwc_kernel(const float* __restrict__ in, float* __restrict__ out,
   }
 }
 
+// The same transpose with 16-B accesses on both sides (HW % 4 == 0, C % 4 == 0):
+// 16 lanes read 64 consecutive pixels of one channel, 16 lanes write 64
+// consecutive channels of one pixel (256 B each); the 4 x 4 element turn goes
+// through the LDS tile.  HBM-bound: 2 x 4 B per element.
+__global__ void __launch_bounds__(256)
+nchw_to_nhwc4_kernel(const float* __restrict__ in, float* __restrict__ out, int C, int HW) {
+  __shared__ float tile[64][65];
+  const int64_t b = blockIdx.z;
+  const int c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+  const float* src = in + b * (int64_t)C * HW;
+  float* dst = out + b * (int64_t)C * HW;
+  const int q = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+  float4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + r0 + 16 * k, p = p0 + 4 * q;
+    v[k] = (c < C && p < HW) ? *reinterpret_cast<const float4*>(src + (int64_t)c * HW + p)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float* t = &tile[r0 + 16 * k][4 * q];
+    t[0] = v[k].x; t[1] = v[k].y; t[2] = v[k].z; t[3] = v[k].w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int pl = r0 + 16 * k, p = p0 + pl, c = c0 + 4 * q;
+    if (p < HW && c < C)
+      *reinterpret_cast<float4*>(dst + (int64_t)p * C + c) =
+          make_float4(tile[4 * q][pl], tile[4 * q + 1][pl], tile[4 * q + 2][pl], tile[4 * q + 3][pl]);
+  }
+}
+
 // Per-wave sample tables in registers: entry q of the y (x) table lives in
 // lane q % 64, slot q / 64 (<= 2 slots: PH*gh, PW*gw <= 128).  Lookups in the
 // bin loop are readlanes with a wave-uniform index, so the per-sample weights
@@ -793,9 +827,15 @@ extern "C" int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64
                 trk_roi_align_workspace_bytes(B, C, H, W, in_layout));
     const int64_t HW = H * W;
     dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)B);
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, st, input,
-                       reinterpret_cast<float*>(workspace), C, HW);
-    if (int e = trk::check_launch("nchw_to_nhwc_kernel")) return e;
+    if (HW % 4 == 0 && C % 4 == 0 && trk::aligned16_ptr(input) && trk::aligned16_ptr(workspace)) {
+      hipLaunchKernelGGL(nchw_to_nhwc4_kernel, grid, dim3(256), 0, st, input, reinterpret_cast<float*>(workspace),
+                         (int)C, (int)HW);
+      if (int e = trk::check_launch("nchw_to_nhwc4_kernel")) return e;
+    } else {
+      hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, st, input,
+                         reinterpret_cast<float*>(workspace), C, HW);
+      if (int e = trk::check_launch("nchw_to_nhwc_kernel")) return e;
+    }
     nhwc = reinterpret_cast<const float*>(workspace);
   }
   // gh/gw for adaptive sampling depend on each ROI; size the LDS tables for the

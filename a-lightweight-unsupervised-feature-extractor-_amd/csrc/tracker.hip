@@ -517,8 +517,18 @@ __global__ void __launch_bounds__(kStepThreads) step_end_kernel(const StepArgs A
   const trk_step_state& S = A.st;
   const int s = A.s0 + blockIdx.x;
   const int flags = S.flags[s];
-  if (flags & 2) return;
   const int t = threadIdx.x;
+  // a failed frame (refused row bound, or a stage-1 solver error) leaves the live list
+  // and the id counter as they were: the results block says so, so the host's live
+  // count stays exact and the stream keeps running after the error
+  if (flags & 2) {
+    if (t == 0) {
+      int64_t* res = res_of(A, s);
+      res[3] = S.n_live[s];
+      res[5] = S.next_id[s];
+    }
+    return;
+  }
   const int64_t cap = A.cfg.cap, base = (int64_t)s * cap, Nmax = A.cfg.Nmax;
   int64_t* res = res_of(A, s);
   int64_t* mt = res + kResHdr;
@@ -537,8 +547,8 @@ __global__ void __launch_bounds__(kStepThreads) step_end_kernel(const StepArgs A
     nud = S.n2[s];
     if (M2 > 0) {
       const int st2 = S.lsap_status[A.cfg.S + s];
-      if (st2 != 0) {
-        if (t == 0) { S.flags[s] = 2; res[4] = st2; }
+      if (st2 != 0) {  // stage 1's outcome stands (the reference raises after it, :561)
+        if (t == 0) { S.flags[s] = 2; res[4] = st2; res[3] = nl; res[5] = next0; }
         return;
       }
       for (int j = t; j < nud; j += kStepThreads) taken[j] = 0;

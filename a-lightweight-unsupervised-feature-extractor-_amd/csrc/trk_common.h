@@ -43,4 +43,6 @@ __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
 
 constexpr int kWave = 64;
 
+inline bool aligned16_ptr(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 }  // namespace trk

@@ -161,9 +161,10 @@ class StepHandle:
     """A frame in flight: its results are copied into pinned host memory by the
     stream; result() waits for that copy only (frames are consumed in order)."""
 
-    def __init__(self, tracker, seq, buf, event, S, Nmax, cap, after_N):
+    def __init__(self, tracker, seq, buf, event, S, Nmax, cap, stride, after_N):
         self._tr, self.seq, self._buf, self._ev = tracker, seq, buf, event
-        self._S, self._Nmax, self._cap, self._after = S, Nmax, cap, after_N
+        # the results layout of the frame's launch (the scratch may be re-sized later)
+        self._S, self._Nmax, self._cap, self._stride, self._after = S, Nmax, cap, stride, after_N
         self._res = None
 
     def done(self) -> bool:
@@ -178,7 +179,7 @@ class StepHandle:
 
     def _parse(self):
         self._ev.synchronize()
-        stride, Nmax, cap = self._tr._stride, self._Nmax, self._cap
+        stride, Nmax, cap = self._stride, self._Nmax, self._cap
         r = self._buf.numpy()[:self._S * stride].reshape(self._S, stride)
         out, err = [], None
         for s in range(self._S):
@@ -234,6 +235,7 @@ class MultiStreamTracker:
         self._live_exact = np.zeros(n_streams, np.int64)   # n_live after the last consumed frame
         self._cum_N = np.zeros(n_streams, np.int64)        # detections launched so far
         self._cum_at_exact = np.zeros(n_streams, np.int64)
+        self._last_stream = None  # raw stream handle of the last frame's launches
         self.sync_wait_s = 0.0  # host time blocked waiting on results (bench diagnostics)
 
     @property
@@ -245,6 +247,9 @@ class MultiStreamTracker:
         """per-frame device scratch sized for (capacity, Nmax)"""
         if Nmax <= self._nmax and self._scr_cap == self.cap:
             return
+        # frames in flight still use the old scratch (their kernels hold its pointers): let
+        # them finish before it is freed
+        self.drain()
         self._nmax = max(Nmax, self._nmax)
         self._scr_cap = self.cap
         S, cap, Nm, dev = self.n_streams, self.cap, self._nmax, self.device
@@ -361,6 +366,8 @@ class MultiStreamTracker:
             raise AssertionError("scratch sizing")
         if len(self._pending) >= self.max_inflight:
             self._consume_through(self._pending[0])
+        if self._live_ub().max() > TRK_LSAP_MAX_DIM:  # the bound counts frames in flight: read them
+            self.drain()
         Mb = int(min(self.cap, max(1, self._live_ub().max())))
         self.last_Mb = Mb  # row stride of this frame's stage cost matrices (tools, tests)
         if Mb > TRK_LSAP_MAX_DIM:
@@ -374,6 +381,13 @@ class MultiStreamTracker:
             if dconf64 is not None:
                 dconf64 = pad(dconf64)
         stream = _stream(self.device)
+        if self._last_stream is not None and stream.value != self._last_stream:
+            # the caller switched streams: frame k+1 reads the table frame k writes, so
+            # order it behind everything enqueued on the previous frame's stream
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.ExternalStream(self._last_stream, device=self.device))
+            _current_stream(self.device).wait_event(ev)
+        self._last_stream = stream.value
         L = lib()
         hN = (ctypes.c_int32 * S)(*N.tolist())
         hF = (ctypes.c_int64 * S)(*fid.tolist())
@@ -406,7 +420,7 @@ class MultiStreamTracker:
                 x.record_stream(cur)
         self._cum_N = self._cum_N + N
         self._seq += 1
-        h = StepHandle(self, self._seq, buf, ev, S, Nm, self.cap, self._cum_N.copy())
+        h = StepHandle(self, self._seq, buf, ev, S, Nm, self.cap, self._stride, self._cum_N.copy())
         self._pending.append(h)
         if after_launch is not None:
             after_launch()

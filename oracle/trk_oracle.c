@@ -130,8 +130,12 @@ static void ora_normalize(const float* x, int D, float* y) {
   for (int d = 0; d < D; ++d) y[d] = x[d] / nrm;
 }
 
+/* descending; NaN first: torch.topk treats NaN as the largest value, so a NaN    */
+/* similarity is always in the top k and the mean is NaN                          */
 static int cmp_desc(const void* a, const void* b) {
   float x = *(const float*)a, y = *(const float*)b;
+  int xn = isnan(x), yn = isnan(y);
+  if (xn || yn) return yn - xn;
   return (x < y) - (x > y);
 }
 

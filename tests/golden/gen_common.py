@@ -126,7 +126,32 @@ SCENES = {
                              low_conf=[(5, 2), (14, 0), (9, 30)])),
     "s64": (12, 64, 8, dict(gaps=[(1, 3, 2)], births=[(60, 4)], low_conf=[(2, 5)])),
     "reid": (13, 10, 62, dict(gaps=[(2, 4, 53), (6, 5, 55)], births=[(9, 20)])),
+    # the metric's size (BASELINE c3: N = 256 per frame): banks fill to T = 30, six tracks
+    # lost for 54 frames come back through the ReID-only stage (miss_count > 50), short
+    # gaps re-activate in stage 1, births at frames 2 and 60 (none while the six are lost:
+    # with cost_max 50 and a loosened gate a lost track takes a newborn detection in stage
+    # 1, which the reference does too), low-confidence detections (no track / no update)
+    "n256": (14, 256, 64, dict(
+        gaps=[(o, 3, 54) for o in range(6)] + [(o, 10, 3) for o in range(10, 22)] +
+             [(o, 30, 6) for o in range(40, 46)] + [(o, 45, 1) for o in range(60, 90)],
+        births=[(o, 2) for o in range(245, 256)] + [(o, 60) for o in range(240, 245)],
+        low_conf=[(100, 0), (101, 5), (102, 20), (103, 40), (241, 60)])),
 }
+
+# scenes whose fixture stores only the reference's outputs (plus a digest of the
+# inputs): the inputs are regenerated here from the seed (8 MB of embeddings)
+OUTPUT_ONLY = {"n256"}
+
+
+def scene_digest(frames) -> str:
+    """sha256 over every frame's embs / boxes / confs, as fixtures record it"""
+    import hashlib
+    h = hashlib.sha256()
+    for fr in frames:
+        h.update(np.ascontiguousarray(fr["embs"], np.float32).tobytes())
+        h.update(np.asarray(fr["bboxes"], np.float64).reshape(-1, 4).tobytes())
+        h.update(np.asarray(fr["confs"], np.float64).tobytes())
+    return h.hexdigest()
 
 
 def scene(name: str):

@@ -165,7 +165,7 @@ def _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf, gate=
                           gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
                           gate_on=t(np.ones(M, np.int32), torch.int32), want=("C_total", "C_app"))
     for k in ("C_total", "C_app"):
-        assert np.array_equal(out3[k][0].cpu().numpy(), res[k]), k
+        assert np.array_equal(out3[k][0].cpu().numpy(), res[k], equal_nan=True), k
     return res
 
 
@@ -313,6 +313,49 @@ def test_cost_dev_bank_resident_vs_det_tile(trk, oracle, gpu):
         assert np.max(np.abs(Ca3[f, :M, :N] - exp["C_app"])) <= 2e-6
         assert np.array_equal(Ct3[f, :M, :N] >= 1e9, exp["C_total"] >= 1e9)
         assert np.max(np.abs(Ct3[f, :M, :N] - exp["C_total"])) <= 2e-6
+
+
+def test_cost_nan_inputs_propagate_like_torch(trk, oracle, gpu):
+    """A NaN embedding, bank row, box or confidence reaches C_total as NaN where the
+    reference's torch ops put it (torch.topk ranks NaN largest, clamp(min=) keeps
+    NaN: mainTracking.py:201-203, costCard.py:150-201), so hungarian_assign raises
+    scipy's ValueError instead of assigning around it; all other entries are
+    unchanged (vs the oracle, which restates the same rules)."""
+    rng = np.random.default_rng(31)
+    M, N = 20, 24
+    base = _renorm(rng.standard_normal((M, 128)))
+    bank = _renorm(base[:, None, :] + 0.05 * rng.standard_normal((M, 30, 128)))
+    blen = np.full(M, 30, np.int32)
+    blen[:4] = [0, 1, 3, 7]
+    bank[np.arange(30)[None, :] >= blen[:, None]] = 0
+    det = rng.standard_normal((N, 128)).astype(np.float32)
+    pbox, dbox = _boxes(rng, M), _boxes(rng, N)
+    lconf = rng.uniform(0.55, 0.99, M).astype(np.float32)
+    dconf = rng.uniform(0.55, 0.99, N).astype(np.float32)
+    det[3, 17] = np.nan          # one embedding
+    bank[9, 2, 5] = np.nan       # one stored bank row of a full bank
+    bank[1, 0, 0] = np.nan       # a bank with one entry
+    dbox[7, 2] = np.nan          # a detection box
+    dconf[11] = np.nan           # a detection confidence
+    pbox[13, 1] = np.nan         # a predicted track box
+    lconf[15] = np.nan           # a track's last confidence
+    # ungated (a gated pair's 1e9 replaces whatever C_total held, NaN included, as in the
+    # reference's apply_kalman_gating; the gate itself is unchanged by this rule)
+    gm, gs = np.zeros((M, 4)), np.tile(np.eye(4).reshape(1, 16), (M, 1))
+    got = _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf, gate=False)
+    with np.errstate(invalid="ignore"):
+        exp = oracle.cost_build(_renorm(bank), blen, det, pbox, dbox, lconf, dconf)
+    for k in ("C_app", "C_total"):
+        g, e = got[k], exp[k]
+        assert np.array_equal(np.isnan(g), np.isnan(e)), k
+        assert np.isnan(g).any(), k
+        f = ~np.isnan(e)
+        assert np.max(np.abs(g[f] - e[f])) <= 2e-6, k
+    nanc = np.isnan(got["C_total"])
+    assert nanc[:, 3].all() and nanc[9].all() and nanc[1].all() and nanc[:, 7].all() and nanc[:, 11].all()
+    assert nanc[13].all() and nanc[15].all() and not nanc[0].any()   # row 0: empty bank, C_app = 1
+    with pytest.raises(ValueError, match="invalid numeric entries"):
+        trk.hungarian_assign(torch.from_numpy(got["C_total"]).to(gpu), cost_max=50.0)
 
 
 @pytest.mark.parametrize("Tmax", [33, 50, 96])

@@ -164,3 +164,51 @@ def test_encoder_restatement_vs_reference(oracle, s):
     with torch.no_grad():
         z = oracle.encoder_forward(sd, x).numpy()
     assert np.max(np.abs(z - d[f"z_s{s}"])) < 1e-5
+
+
+def test_cost_nan_semantics_follow_torch(oracle):
+    """NaN inputs: the oracle ranks a NaN similarity first (torch.topk puts NaN above
+    every number) and keeps NaN through the clamps (torch clamp(min=)), as the
+    reference's build_C_app_topk / bbox_cost / conf_cost do (mainTracking.py:191-203,
+    costCard.py:150-201).  Checked against the same torch ops, literally."""
+    import torch
+    rng = np.random.default_rng(4)
+    M, N, T = 6, 7, 9
+    bank = rng.standard_normal((M, T, 128)).astype(np.float32)
+    bank /= np.linalg.norm(bank, axis=-1, keepdims=True)
+    det = rng.standard_normal((N, 128)).astype(np.float32)
+    det[2, 0] = np.nan
+    bank[4, 7, 3] = np.nan
+    blen = np.full(M, T, np.int32)
+    blen[1] = 3
+    pbox = np.tile(np.float32([[100, 300, 180, 420]]), (M, 1)) + rng.uniform(0, 20, (M, 4)).astype(np.float32)
+    dbox = np.tile(np.float32([[100, 300, 180, 420]]), (N, 1)) + rng.uniform(0, 20, (N, 4)).astype(np.float32)
+    dbox[5, 3] = np.nan
+    lc = rng.uniform(0.5, 1, M).astype(np.float32)
+    dc = rng.uniform(0.5, 1, N).astype(np.float32)
+    dc[6] = np.nan
+    with np.errstate(invalid="ignore"):
+        got = oracle.cost_build(bank, blen, det, pbox, dbox, lc, dc)
+    # the reference's torch ops
+    F_det = torch.from_numpy(det / (np.linalg.norm(det, axis=1, keepdims=True) + 1e-12))
+    capp = []
+    for i in range(M):
+        b = bank[i, :blen[i]]
+        F_bank = torch.from_numpy(b / (np.linalg.norm(b, axis=1, keepdims=True) + 1e-12))
+        sim = F_bank @ F_det.T
+        capp.append(1.0 - torch.topk(sim, k=min(5, sim.shape[0]), dim=0)[0].mean(0))
+    capp = torch.stack(capp).numpy()
+    bp, bc = torch.from_numpy(pbox), torch.from_numpy(dbox)
+    wp, hp = (bp[:, 2] - bp[:, 0]).clamp(min=1.0), (bp[:, 3] - bp[:, 1]).clamp(min=1.0)
+    wc, hc = (bc[:, 2] - bc[:, 0]).clamp(min=1.0), (bc[:, 3] - bc[:, 1]).clamp(min=1.0)
+    scl = torch.abs(torch.log(((wc * hc)[None, :] / (wp * hp)[:, None]).clamp(min=1e-6))).numpy()
+    cf = torch.abs(torch.log(torch.from_numpy(dc).clamp(min=1e-6)[None, :] /
+                             torch.from_numpy(lc).clamp(min=1e-6)[:, None])).numpy()
+    assert np.array_equal(np.isnan(got["C_app"]), np.isnan(capp))
+    assert np.array_equal(np.isnan(got["C_scale"]), np.isnan(scl))
+    assert np.array_equal(np.isnan(got["C_conf"]), np.isnan(cf))
+    assert np.isnan(got["C_app"][:, 2]).all() and np.isnan(got["C_app"][4]).all()
+    tot_nan = np.isnan(capp) | np.isnan(scl) | np.isnan(cf) | np.isnan(dbox).any(1)[None, :]
+    assert np.array_equal(np.isnan(got["C_total"]), tot_nan)
+    f = ~np.isnan(capp)
+    assert np.max(np.abs(got["C_app"][f] - capp[f])) <= 2e-6

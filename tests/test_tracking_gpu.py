@@ -318,3 +318,125 @@ def test_device_step_hist_max_above_32(trk, gpu):
         for s in range(S):
             assert _same(rd[s], rh[s]), (f, s)
     assert int(dev.table.bank_len.max().item()) > 32
+
+
+def test_pipelined_step_async_equals_host_bookkeeping(trk, gpu):
+    """The bench's path: frames enqueued with step_async, up to max_inflight=3 unread,
+    results read only at the end.  N and Nmax vary per frame (the scratch grows while
+    frames are in flight), the table starts at 8 slots (it doubles with frames
+    pending) and the caller switches between two streams every few frames; every
+    frame equals the synchronous host bookkeeping."""
+    import hostref_tracker as H
+    conf = dict(lost_reid_after=3, max_age=8)
+    rng = np.random.default_rng(2024)
+    S, F = 3, 36
+    frames = [_random_scene(rng, n, F) for n in (6, 20, 40)]
+    dev = trk.MultiStreamTracker(S, conf, capacity=8, device=gpu, max_inflight=3)
+    host = H.HostBookkeepingTracker(S, conf, capacity=256, device=gpu)
+    side = torch.cuda.Stream(device=gpu)
+    handles, expect = [], []
+    for f in range(F):
+        E, B, C, Ns, confs = _batch(frames, f, gpu)
+        # torch's padding to Nmax: grow Nmax in steps while frames are pending
+        extra = (f // 7) * 5
+        if extra:
+            pad = lambda x, *tail: torch.nn.functional.pad(x, (0, 0) * len(tail) + (0, extra))
+            E, B, C = pad(E, 128), pad(B, 4), pad(C)
+        expect.append(host.step(E, B, C, Ns, confs, [f] * S))
+        torch.cuda.current_stream(gpu).synchronize()
+        if (f // 5) % 2:
+            side.wait_stream(torch.cuda.current_stream(gpu))
+            with torch.cuda.stream(side):
+                handles.append(dev.step_async(E, B, C, Ns, [f] * S))
+        else:
+            torch.cuda.current_stream(gpu).wait_stream(side)
+            handles.append(dev.step_async(E, B, C, Ns, [f] * S))
+    assert dev.cap > 8
+    for f, (h, rh) in enumerate(zip(handles, expect)):
+        rd = h.result()
+        for s in range(S):
+            assert _same(rd[s], rh[s]), (f, s)
+
+
+def test_error_frame_then_stream_continues(trk, gpu):
+    """A frame whose stage-1 cost holds a NaN raises the reference's ValueError
+    (hungarian_assign -> scipy) and leaves the tracks as the reference leaves them
+    (predicted, nothing else applied); the following frames -- enqueued while the
+    failed one is still unread -- equal the host bookkeeping that raised on the
+    same frame."""
+    import hostref_tracker as H
+    rng = np.random.default_rng(9)
+    F, bad = 16, 6
+    frames = [_random_scene(rng, 12, F, p_vis=1.0)]
+    emb, box, cf = frames[0][bad]
+    emb = emb.copy()
+    emb[0, 5] = np.nan
+    frames[0][bad] = (emb, box, cf)
+    dev = trk.MultiStreamTracker(1, capacity=64, device=gpu, max_inflight=3)
+    host = H.HostBookkeepingTracker(1, capacity=256, device=gpu)
+    handles, expect = [], []
+    for f in range(F):
+        E, B, C, Ns, confs = _batch(frames, f, gpu)
+        if f == bad:
+            with pytest.raises(ValueError, match="invalid numeric entries"):
+                host.step(E, B, C, Ns, confs, [f])
+            expect.append(None)
+        else:
+            expect.append(host.step(E, B, C, Ns, confs, [f]))
+        handles.append(dev.step_async(E, B, C, Ns, [f]))
+    for f, (h, rh) in enumerate(zip(handles, expect)):
+        if rh is None:
+            with pytest.raises(ValueError, match="invalid numeric entries"):
+                h.result()
+            continue
+        assert _same(h.result()[0], rh[0]), f
+
+
+def _n256():
+    """the N = 256 scene regenerated from its seed (the fixture holds the reference's
+    outputs and a digest of the inputs it ran on)"""
+    import gen_common as G
+    d = np.load(os.path.join(GOLDEN, "track_golden_n256.npz"))
+    frames = G.scene("n256")
+    assert G.scene_digest(frames) == str(d["digest"]), "regenerated n256 inputs differ from the fixture's"
+    return d, frames
+
+
+def test_tracking_update_matches_reference_at_n256(trk, gpu):
+    """The metric's size (BASELINE c3, N = 256 per frame) against the reference's own
+    Tracking.update run on the same 64 frames (tests/golden/make_golden.py): full
+    30-deep banks, stage-2 ReID of six tracks lost for 54 frames (frame 57), births,
+    low-confidence detections -- every frame's matches, unmatched track ids and
+    unmatched detections identical."""
+    d, frames = _n256()
+    t = trk.Tracking()
+    for fr in frames:
+        f = fr["frame_id"]
+        got = t.update({"embs": list(fr["embs"]), "bboxes": fr["bboxes"], "confs": fr["confs"],
+                        "input_hw": (1280, 1280), "frame_id": f})
+        assert got == _expected(d, f), f"n256 frame {f}"
+    assert int(t._mst.table.bank_len.max().item()) == 30
+
+
+def test_multistream_pipelined_matches_reference_at_n256(trk, gpu):
+    """The bench's configuration: 8 streams of the N = 256 scene in one
+    MultiStreamTracker, frames enqueued with step_async (up to 3 unread, read at the
+    end); every stream equals the reference frame by frame.  (The streams carry the
+    same detections: the reference's new-track ids follow the detection order, so a
+    permuted copy is a different problem.)"""
+    d, frames = _n256()
+    S = 8
+    mst = trk.MultiStreamTracker(S, device=gpu, max_inflight=3)
+    handles = []
+    for fr in frames:
+        n = len(fr["confs"])
+        E = torch.from_numpy(fr["embs"]).to(gpu)[None].expand(S, n, 128)
+        B = torch.as_tensor(np.asarray(fr["bboxes"], np.float32).reshape(n, 4)).to(gpu)[None].expand(S, n, 4)
+        C = torch.as_tensor(np.asarray(fr["confs"], np.float32)).to(gpu)[None].expand(S, n)
+        h = np.asarray(fr["confs"], np.float64)
+        dc64 = torch.from_numpy(h).to(gpu)[None].expand(S, n)
+        handles.append(mst.step_async(E, B, C, [n] * S, [fr["frame_id"]] * S, dconf64=dc64))
+    for f, h in enumerate(handles):
+        exp = _expected(d, f)
+        for s, r in enumerate(h.result()):
+            assert r.as_tuple() == exp, (f, s)
