@@ -28,29 +28,53 @@ namespace {
 
 constexpr int D = 128;
 
-// 4x4 inverse, Gauss-Jordan with partial pivoting (f64)
+// 4x4 inverse, Gauss-Jordan with partial pivoting (f64).  Fully unrolled with the
+// row swap as selects over static indices: a swap through a runtime row index put
+// m[][] in scratch memory (272 B per lane; step_apply wrote 66 MB per launch of it).
+// Same pivot choice (first row with the strictly largest |m[r][c]|) and operation
+// order as the indexed form, so the results are bit-identical.
 __device__ inline void inv4(const double* A, double* out) {
   double m[4][8];
+#pragma unroll
   for (int r = 0; r < 4; ++r)
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
       m[r][c] = A[r * 4 + c];
       m[r][c + 4] = r == c ? 1.0 : 0.0;
     }
+#pragma unroll
   for (int c = 0; c < 4; ++c) {
     int p = c;
-    for (int r = c + 1; r < 4; ++r)
-      if (fabs(m[r][c]) > fabs(m[p][c])) p = r;
-    if (p != c)
-      for (int k = 0; k < 8; ++k) { double t = m[c][k]; m[c][k] = m[p][k]; m[p][k] = t; }
+    double best = fabs(m[c][c]);
+#pragma unroll
+    for (int r = c + 1; r < 4; ++r) {
+      const double v = fabs(m[r][c]);
+      if (v > best) { best = v; p = r; }
+    }
+#pragma unroll
+    for (int r = c + 1; r < 4; ++r) {
+      const bool sw = p == r;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double a = m[c][k], b = m[r][k];
+        m[c][k] = sw ? b : a;
+        m[r][k] = sw ? a : b;
+      }
+    }
     const double d = m[c][c];
+#pragma unroll
     for (int k = 0; k < 8; ++k) m[c][k] /= d;
+#pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (r == c) continue;
       const double fct = m[r][c];
+#pragma unroll
       for (int k = 0; k < 8; ++k) m[r][k] -= fct * m[c][k];
     }
   }
+#pragma unroll
   for (int r = 0; r < 4; ++r)
+#pragma unroll
     for (int c = 0; c < 4; ++c) out[r * 4 + c] = m[r][c + 4];
 }
 

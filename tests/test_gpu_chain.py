@@ -146,3 +146,36 @@ def test_c2_chain_fp32_vs_oracle(trk, oracle, gpu):
     er, ec = oracle.lsap(exp["C_total"])
     assert np.array_equal(r, er) and np.array_equal(c, ec)
     assert np.array_equal(r, np.arange(N)) and np.mean(c == perm) >= 0.95
+
+
+def test_reference_half_configuration(trk, gpu):
+    """The reference's own GPU configuration (tracking.py:177-178 model.half();
+    tracking.py:209-221 rois built in feat.dtype, so fp16 boxes; :313 normalize(z.float())):
+    an fp16 map through roi_align_from_input_boxes and the .half() model does not raise,
+    and at the c3 size (8 maps x 256 ROIs) its embeddings agree with the fp32 path on the
+    same fp16 inputs (per-row cosine >= 0.999); on the golden inputs it matches the
+    reference's fp32 embeddings (cosine >= 0.999)."""
+    import os
+    from conftest import GOLDEN
+    rng = np.random.default_rng(16)
+    m32, sd = _model(trk, gpu)
+    m16, _ = _model(trk, gpu)
+    m16 = m16.half()
+    feats = torch.nn.functional.silu(torch.randn((8, 1, 512, 40, 40), device=gpu,
+                                                 generator=torch.Generator(device=gpu).manual_seed(5))).half()
+    rois16 = []
+    for b in range(8):
+        boxes = _boxes(rng, 256)
+        rois16.append(trk.roi_align_from_input_boxes(feats[b], boxes.tolist(), (1280, 1280), out_size=(10, 10)))
+    x16 = torch.cat(rois16)
+    assert x16.dtype == torch.float16 and x16.shape == (2048, 512, 10, 10)
+    with torch.no_grad():
+        z16 = torch.nn.functional.normalize(m16(x16).float(), dim=1)
+        z32 = m32(x16.float())
+    cos = (z16 * z32).sum(1)
+    assert float(cos.min()) >= 0.999, float(cos.min())
+    d = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
+    x = torch.from_numpy(G.encoder_input(int(d["seed_s10"]), 16, 10)).to(gpu)
+    with torch.no_grad():
+        z = torch.nn.functional.normalize(m16(x.half()).float(), dim=1).cpu().numpy()
+    assert float((z * d["z_s10"]).sum(1).min()) >= 0.999
