@@ -46,10 +46,11 @@ PREROLL = 30
 
 # ------------------------------------------------------------ workload ----
 MAP_POOL = 16  # frames' maps in the rotating pool: 16 x 26 MB > the 256 MB Infinity Cache
-# map layout the detector hands over: "nhwc" (channels_last, what an NHWC backbone on
-# MI355X emits; roi_align reads it directly) or "nchw" (the reference's YOLOv7 layout;
-# roi_align then transposes each frame's map once, +17 us per 8-stream frame)
-MAP_LAYOUT = os.environ.get("TRK_MAP_LAYOUT", "nhwc")
+# map layout the detector hands over: "nchw" (the default: the reference's YOLOv7 SPPCSPC
+# output, what the drop-in receives; roi_align transposes each frame's map once inside the
+# timed step) or "nhwc" (channels_last, what an NHWC backbone on MI355X would emit;
+# roi_align reads it directly)
+MAP_LAYOUT = os.environ.get("TRK_MAP_LAYOUT", "nchw")
 
 
 def make_scenes(dev, streams, N, frames, seed, C=512, H=40, pool=MAP_POOL):
@@ -348,14 +349,15 @@ class LiveProbe:
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for v in self.ev.values() for a, b in v) * 1e3 / max(steps, 1)
 
-    def embed_gaps_us(self, n_side=1):
-        """mean time between one frame's last encoder launch ending (enc_head)
-        and the next frame's roi stage starting, on the side stream: the side
-        stream's idle time per frame (None with several side streams: frames
-        then overlap on purpose)"""
+    def embed_gaps_us(self, n_side=1, head_deferred=False):
+        """mean time between one frame's last launch on the embedding stream ending
+        (enc_head, or the transition GEMM when the head is deferred to the tracker's
+        stream) and the next frame's roi stage starting on it: the embedding stream's
+        idle time per frame (None with several embedding streams: frames then overlap
+        on purpose)"""
         if n_side != 1:
             return None
-        ends, starts = self.ev["enc_head"], self.ev["roi_stage"]
+        ends, starts = self.ev["enc_gemm_trans" if head_deferred else "enc_head"], self.ev["roi_stage"]
         gaps = [e1.elapsed_time(s0) * 1e3 for (_, e1), (s0, _) in zip(ends, starts[1:])]
         return float(np.mean(gaps)) if gaps else None
 
@@ -445,7 +447,10 @@ def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
                         gating loop (:327-336) -- oracle/literal.py
     One stream at N=256 (tracks = the stream's objects, banks of 30).  The
     literal mode's loops take seconds per frame, so its cost stage is sampled on
-    frames_lit frames (the stages are timed separately and the medians added)."""
+    frames_lit frames (the stages are timed separately and the medians added).
+    Threads: every physical core, capped by OMP_NUM_THREADS where the box sets it
+    (16 on a one-GPU gpurun box: that GPU's CPU share); torch and the oracle's
+    OpenMP loops (roi_align over ROIs, cost over track rows) use the same count."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     import literal as LIT
@@ -458,6 +463,11 @@ def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
     gm = np.zeros((N, 4)); gs = np.tile(np.eye(4).reshape(1, 16) / 11.0, (N, 1))
     kf_x = [np.zeros(8) for _ in range(N)]
     kf_P = [np.diag([10.0] * 4 + [1000.0] * 4) for _ in range(N)]
+    model, cores = _cpu_info()
+    cap = os.environ.get("OMP_NUM_THREADS")
+    thr = min(int(cap), cores or int(cap)) if cap else (cores or os.cpu_count() or 1)
+    torch.set_num_threads(thr)
+    os.environ.setdefault("OMP_NUM_THREADS", str(thr))  # the oracle's OpenMP (read at its first parallel loop)
     t_roi, t_enc, t_cost, t_lsap, t_lit = [], [], [], [], []
     t_start = time.perf_counter()
     for q in range(3 + frames_vec):
@@ -490,14 +500,13 @@ def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
     med = lambda v: float(np.median(v))
     vec = med(t_roi) + med(t_enc) + med(t_cost) + med(t_lsap)
     lit = med(t_roi) + med(t_enc) + med(t_lit) + med(t_lsap)
-    model, cores = _cpu_info()
-    thr = torch.get_num_threads()
     return dict(value=round(N / vec, 2), unit="ROIs/s", cores=thr, kind="port",
                 sample=f"one stream, N={N}, 3 warm-up frames, medians over {len(t_roi)} frames "
-                       f"(literal cost stage: {len(t_lit)} frames): roi_align {med(t_roi) * 1e3:.0f} ms (C, 1 thread) + "
-                       f"fp32 encoder {med(t_enc) * 1e3:.0f} ms (torch CPU, {thr} threads) + cost "
-                       f"{med(t_cost) * 1e3:.1f} ms (C, 1 thread) + scipy LSAP {med(t_lsap) * 1e3:.1f} ms",
+                       f"(literal cost stage: {len(t_lit)} frames): roi_align {med(t_roi) * 1e3:.0f} ms (C, {thr} "
+                       f"OpenMP threads) + fp32 encoder {med(t_enc) * 1e3:.0f} ms (torch CPU, {thr} threads) + cost "
+                       f"{med(t_cost) * 1e3:.1f} ms (C, {thr} OpenMP threads) + scipy LSAP {med(t_lsap) * 1e3:.1f} ms",
                 cpu_model=model, physical_cores=cores,
+                core_cap=(f"OMP_NUM_THREADS={cap} (the box's CPU share for this GPU)" if cap else None),
                 modes={"vectorised": {"ms_per_frame": round(vec * 1e3, 1), "rois_per_s": round(N / vec, 2)},
                        "reference_literal": {"ms_per_frame": round(lit * 1e3, 1), "rois_per_s": round(N / lit, 2),
                                              "cost_ms": round(med(t_lit) * 1e3, 1)}})
@@ -585,7 +594,7 @@ def main():
     kernel_sum = probe.sum_per_step_us(args.steps)
     live = probe.means_us()
     live = {k: v for k, v in live.items() if not k.endswith("_live")}
-    side_gap = probe.embed_gaps_us(len(pipe.sides))
+    side_gap = probe.embed_gaps_us(len(pipe.sides), pipe.defer_head)
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
@@ -669,7 +678,13 @@ def main():
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as fh:
             pk = json.load(fh)["kernels"]
         rf["traffic_over_algorithmic"] = {k: round((pk[k]["read_bytes"] + pk[k]["write_bytes"]) / algo[k][0], 3)
-                                          for k in algo if k in pk}
+                                          for k in algo if k in pk and k != "cost"}
+        # the tracker's cost launches alternate stage 1 (M x N = 256 x 256 per stream) and
+        # stage 2 (ReID-only rows x the detections stage 1 left: none in this workload, so
+        # the launch exits at once): only stage 1 carries the algorithmic bytes
+        if "cost_stage1" in pk:
+            rf["traffic_over_algorithmic"]["cost_stage1"] = round(
+                (pk["cost_stage1"]["read_bytes"] + pk["cost_stage1"]["write_bytes"]) / algo["cost"][0], 3)
     except (OSError, KeyError, ValueError):
         rf["traffic_over_algorithmic"] = None
     rf["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL",

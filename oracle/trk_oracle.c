@@ -38,6 +38,8 @@ void ora_roi_align(const float* input, int B, int C, int H, int W,
                    int PH, int PW, int sampling_ratio, int aligned,
                    float* out) {
   (void)B;
+  /* ROIs are independent: one per OpenMP thread (bench cpu_baseline); same result */
+#pragma omp parallel for schedule(dynamic, 4)
   for (int n = 0; n < K; ++n) {
     const float* r = rois + (size_t)n * 5;
     int b = (int)r[0];
@@ -142,9 +144,9 @@ static int cmp_desc(const void* a, const void* b) {
 void ora_cost_app_topk(const float* bank, const int* bank_len, int M, int Tmax,
                        const float* det, int N, int D, int topk, float* C_app) {
   float* dn = (float*)malloc(sizeof(float) * (size_t)N * D);
-  float* bn = (float*)malloc(sizeof(float) * (size_t)(Tmax > 0 ? Tmax : 1) * D);
-  float* col = (float*)malloc(sizeof(float) * (size_t)(Tmax > 0 ? Tmax : 1));
   for (int j = 0; j < N; ++j) ora_normalize(det + (size_t)j * D, D, dn + (size_t)j * D);
+  /* track rows are independent: one per OpenMP thread (bench cpu_baseline); same result */
+#pragma omp parallel for schedule(dynamic, 4)
   for (int i = 0; i < M; ++i) {
     int T = bank_len[i];
     if (T > Tmax) T = Tmax;
@@ -153,6 +155,8 @@ void ora_cost_app_topk(const float* bank, const int* bank_len, int M, int Tmax,
       for (int j = 0; j < N; ++j) C_app[(size_t)i * N + j] = 1.0f;
       continue;
     }
+    float* bn = (float*)malloc(sizeof(float) * (size_t)(Tmax > 0 ? Tmax : 1) * D);
+    float* col = (float*)malloc(sizeof(float) * (size_t)(Tmax > 0 ? Tmax : 1));
     for (int t = 0; t < T; ++t)
       ora_normalize(bank + ((size_t)i * Tmax + t) * D, D, bn + (size_t)t * D);
     for (int j = 0; j < N; ++j) {
@@ -167,8 +171,9 @@ void ora_cost_app_topk(const float* bank, const int* bank_len, int M, int Tmax,
       float mean = acc / (float)k;
       C_app[(size_t)i * N + j] = 1.0f - mean;
     }
+    free(bn); free(col);
   }
-  free(dn); free(bn); free(col);
+  free(dn);
 }
 
 typedef struct {
@@ -186,6 +191,7 @@ void ora_cost_combine(const float* C_app, int M, int N,
                       const ora_cost_params* prm,
                       float* C_total, float* C_center_out,
                       float* C_scale_out, float* C_conf_out) {
+#pragma omp parallel for schedule(static)
   for (int i = 0; i < M; ++i) {
     const float* bp = pbox + (size_t)i * 4;
     float cpx = 0.5f * (bp[0] + bp[2]), cpy = 0.5f * (bp[1] + bp[3]);

@@ -75,6 +75,98 @@ def test_timed_region_max_over_ranks_gloo():
     assert not np.array_equal(res[0][3], res[1][3])
 
 
+# --------------------------------------------- per-rank replicas, real steps ----
+def _replica_steps(rank, frames=5, streams=2, N=10):
+    """One rank's replica of the bench workload on the CPU: bench.make_scenes with the
+    rank's seed (1000 + rank, as bench.main), then per step and stream the reference's
+    CPU path restated -- oracle roi_align -> fp32 encoder -> oracle/tracker_ref
+    (Tracking.update) -- returning (step fn, scene, trackers)."""
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import bench
+    import gen_common as G
+    import oracle as O
+    import tracker_ref as TR
+    sc = bench.make_scenes(torch.device("cpu"), streams, N, frames, seed=1000 + rank, pool=2)
+    sd = {k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}
+    trackers = [TR.TrackerRef() for _ in range(streams)]
+
+    def step(f):
+        fmap = bench.frame_map(sc, f).numpy()
+        out = []
+        for s in range(streams):
+            rois = sc["np"]["rois"][f, s * N:(s + 1) * N].copy()
+            rois[:, 0] = 0
+            roi = O.roi_align(fmap[s:s + 1], rois, (10, 10), 40 / 1280.0, 2, True)
+            with torch.no_grad():
+                emb = O.encoder_forward(sd, torch.from_numpy(roi)).numpy()
+            box, conf = sc["np"]["dbox"][f, s], sc["np"]["dconf"][f, s]
+            m, ut, ud = trackers[s].update(list(emb), box.tolist(), conf.tolist())
+            out.append((m, ut, ud))
+        return out
+    return step, sc
+
+
+def _identity(sc, results):
+    """fraction of matches that keep the object their track first matched
+    (bench.Pipeline.check_identity's rule), over frames 1.."""
+    ids, ok, tot = {}, 0, 0
+    for f, res in enumerate(results):
+        for s, (m, _, _) in enumerate(res):
+            for tid, j in m:
+                o = int(sc["obj"][f, s][j])
+                ids.setdefault((s, tid), o)
+                ok += ids[(s, tid)] == o
+                tot += 1
+    return ok / max(tot, 1), tot
+
+
+def _replica_worker(rank, world, port, q):
+    torch.set_num_threads(2)
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import bench
+        step, sc = _replica_steps(rank)
+        step(0)  # warm-up frame: every track is born here
+        el, out = bench.timed_region(lambda k: step(k + 1), 4, tdist, lambda: None, torch.device("cpu"))
+        q.put((rank, el, out, sc["np"]["rois"].copy()))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_replicas_run_real_steps_gloo():
+    """Two gloo ranks each build their own bench workload (make_scenes, rank seed) and
+    run real tracker steps -- ROI Align, encoder, the reference's Tracking.update, all
+    restated on the CPU -- inside bench.timed_region: one barrier pair and one MAX
+    all-reduce, no data-path collective.  Each rank's results equal the same replica
+    run alone in this process (replicas are independent), tracks keep their objects,
+    and the two ranks' workloads differ."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, el, out, rois = q.get(timeout=240)
+        res[r] = (el, out, rois)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0]  # MAX over ranks
+    assert not np.array_equal(res[0][2], res[1][2])
+    torch.set_num_threads(4)
+    for r in (0, 1):
+        step, sc = _replica_steps(r)
+        alone = [step(f) for f in range(5)]
+        assert res[r][1] == alone[1:], r
+        ident, nmatch = _identity(sc, alone)
+        assert nmatch >= 4 * 2 * 8 and ident == 1.0, (r, ident, nmatch)
+
+
 def test_timed_region_single_process():
     sys.path.insert(0, REPO)
     import bench

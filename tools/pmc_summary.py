@@ -15,10 +15,18 @@ def load(d, counter):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     acc = defaultdict(list)
     for f in files:
+        cost3 = []
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            if "cost3_kernel" in r["Kernel_Name"]:
+                cost3.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+        # the device tracker launches cost3 twice per frame, stage 1 then stage 2
+        # (trk_build_cost_dev: same grid, sizes read on the device): split them by order
+        cost3.sort()
+        for q, (_, v) in enumerate(cost3):
+            acc["cost3_kernel stage %d" % (1 + q % 2)].append(v)
     return acc
 
 
@@ -49,6 +57,12 @@ def main():
                        "nchw_to_nhwc_kernel": "nchw_to_nhwc", "track_update_kernel": "track_update"}
         tab = {}
         for k, v in out.items():
+            if k.startswith("cost3_kernel stage"):
+                if v["read_bytes_corrected"] is not None and v["write_bytes"] is not None:
+                    tab["cost_stage" + k[-1]] = dict(read_bytes=round(v["read_bytes_corrected"]),
+                                                    write_bytes=round(v["write_bytes"]), launches=v["launches"],
+                                                    kernel=k)
+                continue
             for pat, nm in short_names.items():
                 if pat in k and v["read_bytes_corrected"] is not None and v["write_bytes"] is not None:
                     tab[nm] = dict(read_bytes=round(v["read_bytes_corrected"]), write_bytes=round(v["write_bytes"]),
