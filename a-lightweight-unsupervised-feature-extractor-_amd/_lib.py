@@ -98,6 +98,8 @@ def _declare(L):
     L.trk_enc_se.restype = i32
     L.trk_enc_head.argtypes = [P, i64, i64, i64, P, P, P, ctypes.c_double, P, P, P, f32, P, P, i64, P, P]
     L.trk_enc_head.restype = i32
+    L.trk_nchw_to_nhwc.argtypes = [P, i64, i64, i64, i64, P, P]
+    L.trk_nchw_to_nhwc.restype = i32
     L.trk_kf_predict.argtypes = [i64, P, P, P, P, P, P, P]
     L.trk_kf_predict.restype = i32
     L.trk_track_update.argtypes = [i64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, i64, f32, f32,

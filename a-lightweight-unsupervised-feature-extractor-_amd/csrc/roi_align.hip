@@ -804,6 +804,22 @@ extern "C" size_t trk_roi_align_workspace_bytes(int64_t B, int64_t C, int64_t H,
   return (size_t)(B * C * H * W) * sizeof(float);
 }
 
+extern "C" int trk_nchw_to_nhwc(const float* in, int64_t B, int64_t C, int64_t H, int64_t W, float* out,
+                                void* stream) {
+  TRK_REQUIRE(B >= 1 && C >= 1 && H >= 1 && W >= 1 && B * C * H * W < (int64_t)1 << 31,
+              "nchw_to_nhwc: bad shape [%lld,%lld,%lld,%lld]", (long long)B, (long long)C, (long long)H, (long long)W);
+  TRK_REQUIRE(in && out, "nchw_to_nhwc: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t HW = H * W;
+  dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)B);
+  if (HW % 4 == 0 && C % 4 == 0 && trk::aligned16_ptr(in) && trk::aligned16_ptr(out)) {
+    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, grid, dim3(256), 0, st, in, out, (int)C, (int)HW);
+    return trk::check_launch("nchw_to_nhwc4_kernel");
+  }
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, st, in, out, C, HW);
+  return trk::check_launch("nchw_to_nhwc_kernel");
+}
+
 extern "C" int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64_t H, int64_t W,
                                  int in_layout, const float* rois, int64_t K, float spatial_scale,
                                  int PH, int PW, int sampling_ratio, int aligned, void* out,
@@ -825,17 +841,7 @@ extern "C" int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64
     TRK_REQUIRE(workspace && workspace_bytes >= trk_roi_align_workspace_bytes(B, C, H, W, in_layout),
                 "roi_align: NCHW input needs a workspace of %zu bytes",
                 trk_roi_align_workspace_bytes(B, C, H, W, in_layout));
-    const int64_t HW = H * W;
-    dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)B);
-    if (HW % 4 == 0 && C % 4 == 0 && trk::aligned16_ptr(input) && trk::aligned16_ptr(workspace)) {
-      hipLaunchKernelGGL(nchw_to_nhwc4_kernel, grid, dim3(256), 0, st, input, reinterpret_cast<float*>(workspace),
-                         (int)C, (int)HW);
-      if (int e = trk::check_launch("nchw_to_nhwc4_kernel")) return e;
-    } else {
-      hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, st, input,
-                         reinterpret_cast<float*>(workspace), C, HW);
-      if (int e = trk::check_launch("nchw_to_nhwc_kernel")) return e;
-    }
+    if (int e = trk_nchw_to_nhwc(input, B, C, H, W, reinterpret_cast<float*>(workspace), stream)) return e;
     nhwc = reinterpret_cast<const float*>(workspace);
   }
   // gh/gw for adaptive sampling depend on each ROI; size the LDS tables for the

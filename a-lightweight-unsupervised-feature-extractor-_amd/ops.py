@@ -15,7 +15,7 @@ import torch
 from . import _lib
 from ._lib import CostParams, check, lib
 
-__all__ = ["dwconv5_nhwc", "act_mean", "scale_rows", "roi_align", "roi_align_from_input_boxes", "build_cost", "cost_combine", "lsap_batched",
+__all__ = ["dwconv5_nhwc", "act_mean", "scale_rows", "roi_align", "nchw_to_nhwc", "roi_align_from_input_boxes", "build_cost", "cost_combine", "lsap_batched",
            "linear_sum_assignment", "CostParams", "default_cost_params"]
 
 
@@ -325,6 +325,20 @@ def roi_align(input: torch.Tensor, boxes: Union[torch.Tensor, List[torch.Tensor]
                                  _ptr(ws), ws_bytes, _stream(x.device))
     check(rc, "roi_align")
     return out if out.dtype == out_dtype else out.to(out_dtype)
+
+
+def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """An f32 [B, C, H, W] map in channels_last storage (a [B, H, W, C] copy), by the
+    same kernel roi_align uses for NCHW input: passing the result to roi_align skips
+    that copy, so a caller can convert a frame's map ahead of its ROI Align."""
+    _need_gpu(x, "nchw_to_nhwc")
+    if x.dim() != 4 or x.dtype != torch.float32:
+        raise ValueError("nchw_to_nhwc: expected an f32 [B, C, H, W] tensor")
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty((B, H, W, C), device=x.device, dtype=torch.float32)
+    check(lib().trk_nchw_to_nhwc(_ptr(x), B, C, H, W, _ptr(out), _stream(x.device)), "nchw_to_nhwc")
+    return out.permute(0, 3, 1, 2)
 
 
 def roi_align_from_input_boxes(feat: torch.Tensor, boxes_in: Sequence[Sequence[float]],

@@ -144,6 +144,22 @@ class Pipeline:
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
                            if os.environ.get("TRK_ROI_STREAM", "0") == "1" else None)
         self.roi_pending = {}
+        # NCHW maps: frame f's NCHW -> NHWC copy (roi_align's first kernel) issued on the
+        # tracker's stream two frames ahead, right after frame f-2's tracker step, so the
+        # HBM-bound copy runs beside the encoder's MFMA-bound kernels instead of in front of
+        # the frame's ROI Align on the embedding stream (TRK_MAP_AHEAD=0: inside roi_align)
+        self.map_ahead = (MAP_LAYOUT == "nchw" and self.track_stream is not None and
+                          os.environ.get("TRK_MAP_AHEAD", "1") == "1")
+        self.map_pending = {}
+
+    def _map_ahead(self, f):
+        if not self.map_ahead or f in self.map_pending or f >= len(self.sc["rois"]):
+            return
+        with torch.cuda.stream(self.track_stream):
+            m = trk.nchw_to_nhwc(frame_map(self.sc, f))
+            ev = torch.cuda.Event()
+            ev.record(self.track_stream)
+        self.map_pending[f] = (m, ev)
 
     def capture(self):
         """Capture roi_align + encoder as two hipGraphs (static ROI / embedding
@@ -170,7 +186,14 @@ class Pipeline:
         return self.stage_embed(roi)
 
     def stage_roi(self, f):
-        return trk.roi_align(frame_map(self.sc, f), self.sc["rois"][f], (self.S, self.S), 40 / 1280.0, 2, True,
+        fm = frame_map(self.sc, f)
+        if self.map_ahead:
+            self._map_ahead(f)  # (frames not converted ahead: now)
+            fm, ev = self.map_pending.pop(f)
+            st = torch.cuda.current_stream()
+            st.wait_event(ev)
+            fm.record_stream(st)
+        return trk.roi_align(fm, self.sc["rois"][f], (self.S, self.S), 40 / 1280.0, 2, True,
                              out_dtype=torch.bfloat16, channels_last=True)
 
     def stage_embed(self, roi):
@@ -258,8 +281,10 @@ class Pipeline:
             hook = lambda: self.embed_async(f + 1)
         # the whole tracker step is enqueued (no host wait inside a frame); its
         # results reach pinned host memory by one copy and are read in order
-        return self.tracker.step_async(emb, sc["dbox"][f], sc["dconf"][f], [sc["N"]] * sc["streams"],
-                                       [f] * sc["streams"], after_launch=hook)
+        h = self.tracker.step_async(emb, sc["dbox"][f], sc["dconf"][f], [sc["N"]] * sc["streams"],
+                                    [f] * sc["streams"], after_launch=hook)
+        self._map_ahead(f + 2)  # on this (the tracker's) stream, behind the frame's step
+        return h
 
     def check_identity(self, f, res):
         """fraction of detections matched to the track that has followed the
@@ -291,7 +316,7 @@ class LiveProbe:
     trk_roi_align_fwd (NCHW->NHWC transpose + sweep = the roi stage) and the
     two summing GEMMs (a 4-8 MB hipMemsetAsync of the sums precedes the GEMM)."""
 
-    NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_enc_g1_dwconv": "enc_g1_dwconv",
+    NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_nchw_to_nhwc": "map_nhwc", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
@@ -575,7 +600,7 @@ def main():
     # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
     # the syncs around the timed region make it do exactly `steps` embeddings (those of
     # frames first + depth .. last + depth) and `steps` assignments
-    frames = PREROLL + args.warmup + args.steps + int(os.environ.get("TRK_PREFETCH_DEPTH", "1"))
+    frames = PREROLL + args.warmup + args.steps + int(os.environ.get("TRK_PREFETCH_DEPTH", "1")) + 1
     sc = make_scenes(dev, args.streams, args.n, frames, seed=1000 + rank)
     pipe = Pipeline(sc, model)
     if args.graph:

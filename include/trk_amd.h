@@ -75,6 +75,11 @@ int trk_set_tuning(const char* key, int value);
  *          whole channel vectors); may be NULL for NHWC input.
  * ---------------------------------------------------------------------- */
 size_t trk_roi_align_workspace_bytes(int64_t B, int64_t C, int64_t H, int64_t W, int in_layout);
+/* The NCHW -> NHWC map copy that trk_roi_align_fwd makes for an NCHW input, as
+ * its own call: in [B,C,H,W] f32 -> out [B,H,W,C] f32 (out may then be passed to
+ * trk_roi_align_fwd as TRK_NHWC).  Lets a caller convert a frame's map ahead of
+ * its ROI Align, e.g. on another stream beside the previous frame's encoder. */
+int trk_nchw_to_nhwc(const float* in, int64_t B, int64_t C, int64_t H, int64_t W, float* out, void* stream);
 int trk_roi_align_fwd(const float* input, int64_t B, int64_t C, int64_t H, int64_t W, int in_layout,
                       const float* rois, int64_t K, float spatial_scale,
                       int PH, int PW, int sampling_ratio, int aligned,

@@ -352,8 +352,9 @@ def test_cost_nan_inputs_propagate_like_torch(trk, oracle, gpu):
         f = ~np.isnan(e)
         assert np.max(np.abs(g[f] - e[f])) <= 2e-6, k
     nanc = np.isnan(got["C_total"])
-    assert nanc[:, 3].all() and nanc[9].all() and nanc[1].all() and nanc[:, 7].all() and nanc[:, 11].all()
-    assert nanc[13].all() and nanc[15].all() and not nanc[0].any()   # row 0: empty bank, C_app = 1
+    assert nanc[1:, 3].all() and nanc[9].all() and nanc[1].all() and nanc[:, 7].all() and nanc[:, 11].all()
+    assert nanc[13].all() and nanc[15].all()
+    assert not nanc[0, 3] and not np.isnan(got["C_app"][0]).any()  # row 0: empty bank, C_app = 1 (no sims)
     with pytest.raises(ValueError, match="invalid numeric entries"):
         trk.hungarian_assign(torch.from_numpy(got["C_total"]).to(gpu), cost_max=50.0)
 
