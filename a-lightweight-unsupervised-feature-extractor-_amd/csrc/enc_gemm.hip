@@ -35,20 +35,7 @@
 #include "trk_common.h"
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
-int g_enc_g4_narrow = 0;  // trk_set_tuning("enc_g4_narrow"): 1 = 3-slot ROI sums even for P >= 64 (A/B)
-int g_enc_gemm = 1;      // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
-int g_enc_gemm_dbg = 0;     // trk_set_tuning("enc_gemm_dbg"): experiments (1 skip epilogue, 2 stores, 4 sums, 8 sum
-                            // writes; g1dw: 16 no depthwise, 32 two K steps only)
-int g_g1dw_persist = 0;     // trk_set_tuning("g1dw_persist"): 0 = one workgroup per tile; v > 0 = persistent
-                            // tile queue, 2 workgroups per CU, the second started (v - 1) x 2048 cycles late
-int g_g1dw_mode = 7;        // trk_set_tuning("g1dw_mode"): 7 (default) = g1dw4_kernel (4-wave workgroups, 16x16x32
-                            // MFMAs; Y1 summed in another order); the 32x32x16 g1dw_kernel variants, bit-identical
-                            // to each other: where the K loop issues its LDS-DMA (0 top, 1 after the MFMAs,
-                            // 2 interleaved); 4 = warp-specialised DMA waves; 5 = 256-wide N tiles; 6 = role-split
-int g_dsc_split = 1;        // trk_set_tuning("dsc_split"): 1 = gemm4's DSC tiles compiled per activation (SiLU /
-                            // Hardswish), 0 = one tile body with a per-element select
-int g_enc_gemm_offset = 0;  // trk_set_tuning("enc_gemm_offset"): > 0 runs gemm4 persistent (2 workgroups per CU)
-                            // with each CU's second workgroup started that many x 2048 cycles late
+int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
 
 namespace {
 
@@ -99,8 +86,6 @@ struct EncGemmArgs {
   int ld_sums;             // covering the ROI); group g at column g * N
   const float* scale;      // EPI_TRANS: s [nroi][kscale]
   int M, N, K, P, groups, kscale;
-  int dbg;                 // g_enc_gemm_dbg
-  int hsplit;              // g_dsc_split: gemm4 DSC tiles instantiated per activation
   unsigned long long* prof;  // trk_enc_set_prof (gemm4: per-workgroup phase stamps; diagnostics)
 };
 
@@ -411,997 +396,7 @@ int launch(const EncGemmArgs& a, hipStream_t st) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// Persistent tile queue: tiles are dealt from 8 per-XCD ranges (tile order as
-// xcd_remap, so one XCD's L2 sees contiguous M tiles); a workgroup takes tiles of
-// its own range first (blockIdx % 8, the dispatcher's round-robin -- placement is a
-// speed hint only) and then steals from the others, so workgroups that start late
-// -- behind CUs another stream still holds -- just take fewer tiles.  The last
-// workgroup to leave resets the counters for the next launch using this slot.
-constexpr int kQueues = 64;                 // launch slots (round-robin on the host)
-__device__ unsigned int g_tileq[kQueues][10];  // [0..7] next index per XCD range, [8] workgroups done
-
-struct TileQueue {
-  unsigned int* q;
-  int64_t ntiles;
-  __device__ int64_t range_lo(int x) const {
-    const int64_t b = ntiles / 8, r = ntiles % 8;
-    return x * b + (x < r ? x : r);
-  }
-  // next tile for this workgroup (uniform), or -1; tid 0 fetches, LDS broadcast
-  __device__ int64_t next(int* slot, int& cur) const {
-    if (threadIdx.x == 0) {
-      int64_t t = -1;
-      for (; cur < 8 && t < 0; ) {
-        const int x = (int)((blockIdx.x + cur) & 7);
-        const int64_t lo = range_lo(x), n = range_lo(x + 1) - lo;
-        const unsigned int i = atomicAdd(&q[x], 1u);
-        if ((int64_t)i < n) t = lo + i;
-        else ++cur;
-      }
-      *slot = (int)t;
-    }
-    __syncthreads();
-    const int t = *slot;
-    __syncthreads();
-    return t;
-  }
-  __device__ void finish() const {
-    if (threadIdx.x == 0) {
-      __threadfence();
-      if (atomicAdd(&q[8], 1u) == gridDim.x - 1) {
-        for (int x = 0; x < 9; ++x) atomicExch(&q[x], 0u);
-        __threadfence();
-      }
-    }
-  }
-};
-
-int next_queue_slot() {
-  static int s = 0;
-  s = (s + 1) % kQueues;
-  return s;
-}
-
-// ---------------------------------------------------------------------------
-// First 1x1 convs + the four depthwise 5x5 convs in one kernel (10x10 ROIs).
-//
-// The M tile is two whole ROIs (200 rows, computed as 7 MFMA row tiles of 32;
-// rows 200..223 belong to the next tile and are discarded), so the 5x5
-// neighbourhood of every output pixel is inside the tile: Y1 = X . W1^T is
-// rounded to bf16 into LDS (exactly what the plain GEMM would store) and the
-// depthwise conv runs from there with dwconv5_rows2_kernel's f32 FMA order (taps
-// in the zero padding skipped), writing only Y2.  Y1 never reaches HBM.  N tile =
-// 128 channels; 8 waves: wave w owns column tile w & 3 and row tiles (w >> 2) +
-// 2t.  K loop as enc_gemm_kernel (LDS-DMA ring, NSTAGE = 3).
-constexpr int G1_ROWS = 224, G1_BN = 128, G1_S = 10, G1_P = 100;
-constexpr int G1_AP = G1_ROWS * CPR;               // A 16-B pieces per stage (896)
-constexpr size_t G1_STAGE = (size_t)(G1_ROWS + G1_BN) * CPR * 16;
-constexpr size_t G1_TILE = (size_t)2 * G1_P * (G1_BN / 2) * 4;   // bf16 pairs [200][64]
-constexpr size_t G1_W = (size_t)25 * (G1_BN / 2) * 8;            // f32 pairs [25][64]
-constexpr size_t G1_LDS = NSTAGE * G1_STAGE > G1_TILE + G1_W ? NSTAGE * G1_STAGE : G1_TILE + G1_W;
-
-// Depthwise 5x5 of output rows [OY0, OY1) x columns [X0, X0 + 5) of a 10x10
-// ROI for the lane's channel pair: input rows / columns clipped to the ROI (the
-// zero padding's taps are skipped at compile time), weights read from LDS.  Each
-// output accumulates its taps in ascending input row, then ascending kx --
-// dwconv5_rows2_kernel's order, so Y2 is bit-identical.
-template <int OY0, int OY1, int X0>
-__device__ __forceinline__ void dw5_block(const uint32_t* __restrict__ src, const dw_pair_t* __restrict__ w,
-                                          uint32_t* __restrict__ dst, int ldd) {
-  constexpr int NY = OY1 - OY0;
-  constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY1 + 1 > G1_S - 1 ? G1_S - 1 : OY1 + 1;
-  constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
-  constexpr int NX = IX1 - IX0 + 1;
-  dw_pair_t acc[NY][5];
-#pragma unroll
-  for (int oy = 0; oy < NY; ++oy)
-#pragma unroll
-    for (int ox = 0; ox < 5; ++ox) acc[oy][ox] = dw_pair_t{0.f, 0.f};
-  // input rows are software-pipelined: row iy + 1 is read from LDS while row iy is used
-  uint32_t nxt[NX];
-#pragma unroll
-  for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(IY0 * G1_S + IX0 + ix) * (G1_BN / 2)];
-#pragma unroll 1
-  for (int iy = IY0; iy <= IY1; ++iy) {  // rolled: one input row's values live at a time
-    dw_pair_t in[NX];
-#pragma unroll
-    for (int ix = 0; ix < NX; ++ix) in[ix] = dw_pair_t{__uint_as_float(nxt[ix] << 16), __uint_as_float(nxt[ix] & 0xffff0000u)};
-    const int iyn = iy < IY1 ? iy + 1 : iy;
-#pragma unroll
-    for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(iyn * G1_S + IX0 + ix) * (G1_BN / 2)];
-#pragma unroll
-    for (int oy = 0; oy < NY; ++oy) {
-      const int ky = iy - (OY0 + oy) + 2;
-      if (ky < 0 || ky > 4) continue;
-      dw_pair_t wr[5];  // weight row ky (LDS)
-#pragma unroll
-      for (int kx = 0; kx < 5; ++kx) wr[kx] = w[(ky * 5 + kx) * (G1_BN / 2)];
-#pragma unroll
-      for (int ox = 0; ox < 5; ++ox)
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) {
-          const int ix = X0 + ox + kx - 2;
-          if (ix >= IX0 && ix <= IX1)
-            acc[oy][ox] = __builtin_elementwise_fma(wr[kx], in[ix - IX0], acc[oy][ox]);
-        }
-    }
-  }
-#pragma unroll
-  for (int oy = 0; oy < NY; ++oy)
-#pragma unroll
-    for (int ox = 0; ox < 5; ++ox) {
-      const uint32_t v = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
-      if (ldd > 0) dst[((OY0 + oy) * G1_S + X0 + ox) * ldd] = v;
-      else asm volatile("" ::"v"(v));  // experiment (enc_gemm_dbg 256): no Y2 stores
-    }
-}
-
-// one 5x5 output quadrant (QY, QX), in two row blocks (fewer live accumulators)
-template <int QY, int QX>
-__device__ __forceinline__ void dw5_quadrant(const uint32_t* __restrict__ src, const dw_pair_t* __restrict__ w,
-                                             uint32_t* __restrict__ dst, int ldd) {
-  dw5_block<5 * QY, 5 * QY + 3, 5 * QX>(src, w, dst, ldd);
-  dw5_block<5 * QY + 3, 5 * QY + 5, 5 * QX>(src, w, dst, ldd);
-}
-
-template <int MODE>
-__device__ __forceinline__ void g1dw_tile(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                          const float* __restrict__ wdw, uint16_t* __restrict__ Y2, int M, int N,
-                                          int dbg, int64_t lb, unsigned char* smem) {
-  uint4* As = reinterpret_cast<uint4*>(smem);       // [NSTAGE][224 * CPR]
-  uint4* Bs = As + NSTAGE * G1_AP;                   // [NSTAGE][128 * CPR]
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));                      // per tile: keep lane addresses out of the tile loop
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave & 3, wr = wave >> 2;
-  const int ntile_n = N / G1_BN;
-  const int n0 = (int)(lb % ntile_n) * G1_BN;
-  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);   // two ROIs per tile
-  constexpr int K = 512;
-
-  // DMA sources: A pieces p = q*512 + tid (q = 0: all waves; q = 1: waves 0..5)
-  const uint16_t* asrc[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int p = min(q * 512 + tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
-    const int64_t row = min(m0 + r, (int64_t)M - 1);
-    asrc[q] = X + row * K + c * 8;
-  }
-  const uint16_t* bsrc;
-  {
-    const int p = tid, r = p / CPR, c = unswz_c(p);
-    bsrc = W1 + (int64_t)(n0 + r) * K + c * 8;
-  }
-  // DMA op j (0: A rows 0..127, 1: A rows 128..223 (waves 0..5), 2: B) of a stage
-  auto issue_op = [&](int j, int stage, int k0) {
-    if (dbg & 128) return;  // experiment: no operand loads
-    if (j == 0)
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
-    else if (j == 1) {
-      if (wave < (G1_AP - 512) / 64)
-        __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
-    } else {
-      __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
-    }
-  };
-  auto issue = [&](int stage, int k0) {
-    issue_op(0, stage, k0);
-    issue_op(1, stage, k0);
-    issue_op(2, stage, k0);
-  };
-  // row tiles of this wave: wr, wr + 2, wr + 4 (+ wr + 6 for wr == 0)
-  constexpr int TMX = 4;
-  const int ntm = wr == 0 ? 4 : 3;
-  f16_t acc[TMX];
-#pragma unroll
-  for (int i = 0; i < TMX; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-
-  // waves 0..5 issue 3 DMA ops per stage, waves 6..7 issue 2
-  const int nk = (dbg & 32) ? 2 : K / BK;
-  issue(0, 0);
-  issue(1, BK);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int st = kt % NSTAGE;
-    if (kt + 1 < nk) {
-      if (wave < (G1_AP - 512) / 64) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const bool pf = kt + 2 < nk;
-    const int pst = (kt + 2) % NSTAGE, pk = (kt + 2) * BK;
-    if (MODE == 0 && pf) issue(pst, pk);
-    const uint4* as = As + st * G1_AP;
-    const uint4* bs = Bs + st * G1_BN * CPR;
-    if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        const int c = ks * 2 + (lane >> 5);
-        const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
-#pragma unroll
-        for (int i = 0; i < TMX; ++i) {
-          if (i < ntm) {
-            const int rt = wr + 2 * i;
-            const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
-          }
-          // MODE 2: the stage's three DMA ops interleaved with the MFMAs
-          if (MODE == 2 && pf && ((ks == 0 && (i == 0 || i == 2)) || (ks == 1 && i == 0))) {
-            __builtin_amdgcn_sched_barrier(0);
-            issue_op(ks == 0 ? i / 2 : 2, pst, pk);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
-    if (MODE == 1 && pf) {  // after this step's MFMAs are issued
-      __builtin_amdgcn_sched_barrier(0);
-      issue(pst, pk);
-    }
-  }
-  __syncthreads();
-
-  const int cp = lane;
-  // depthwise weights [25][64 channel pairs] of the tile: global loads issued now,
-  // written to LDS after Y1 (their latency hides behind the Y1 writes)
-  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G1_TILE);
-  constexpr int NWQ = (25 * (G1_BN / 2) + 511) / 512;
-  dw_pair_t wreg[NWQ];
-#pragma unroll
-  for (int j = 0; j < NWQ; ++j) {
-    const int q = min(j * 512 + tid, 25 * (G1_BN / 2) - 1), k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
-    wreg[j] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
-  }
-  // Y1 (bf16-rounded, rows < 200 of the tile) -> LDS [200][64 channel pairs]
-  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
-  {
-    const int cl = wn * 32 + (lane & 31);  // channel within the tile
-#pragma unroll
-    for (int i = 0; i < TMX; ++i) {
-      if (i < ntm) {
-        const int rt = wr + 2 * i;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NWQ; ++j)
-    if (j * 512 + tid < 25 * (G1_BN / 2)) wl[j * 512 + tid] = wreg[j];
-  __syncthreads();
-
-  // depthwise 5x5: wave = (ROI, 5x5 output quadrant): 8 equal tasks, lane = channel pair
-  if (dbg & 16) return;
-  {
-    const int roi = wave >> 2, quad = wave & 3;
-    const int64_t rbase = m0 + roi * G1_P;
-    if (rbase < M) {
-      const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2) + cp;
-      const dw_pair_t* wq = wl + cp;
-      uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0) + cp;
-      const int ldd = (dbg & 256) ? 0 : N / 2;
-      switch (quad) {
-        case 0: dw5_quadrant<0, 0>(src, wq, dst, ldd); break;
-        case 1: dw5_quadrant<0, 1>(src, wq, dst, ldd); break;
-        case 2: dw5_quadrant<1, 0>(src, wq, dst, ldd); break;
-        default: dw5_quadrant<1, 1>(src, wq, dst, ldd); break;
-      }
-    }
-  }
-}
-
-template <int MODE>
-__global__ void __launch_bounds__(512) g1dw_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                                   const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                   int M, int N, int dbg) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  g1dw_tile<MODE>(X, W1, wdw, Y2, M, N, dbg, xcd_remap(blockIdx.x, gridDim.x), smem);
-}
-
-// ---------------------------------------------------------------------------
-// g1dw, warp-specialised: 10 waves = 8 MFMA waves (the tile split of g1dw_tile)
-// + 2 DMA waves that issue the whole stage (22 LDS-DMA wave-instructions).  The
-// K loop is L2->LDS bound (~27 TB/s chip-wide for this tile shape) and a wave
-// that issues LDS-DMA stalls while the memory pipeline is full; with the issue
-// on waves of their own, the MFMA waves keep the matrix pipe busy meanwhile.
-// One s_barrier per K step for all 10 waves: the DMA waves wait (vmcnt) for
-// stage kt, the barrier publishes it, then they issue stage kt + 2 while the
-// MFMA waves consume stage kt.  The depthwise phase runs on all 10 waves, one
-// (ROI, output row pair) task each.  Same arithmetic as g1dw_kernel.
-__global__ void __launch_bounds__(640, 5) g1dw_ws_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                                      const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                      int M, int N) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* As = reinterpret_cast<uint4*>(smem);       // [NSTAGE][224 * CPR]
-  uint4* Bs = As + NSTAGE * G1_AP;                   // [NSTAGE][128 * CPR]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntile_n = N / G1_BN;
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int n0 = (int)(lb % ntile_n) * G1_BN;
-  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);
-  constexpr int K = 512, NK = K / BK, NBLK = (G1_AP + G1_BN * CPR) / 64;  // 22 blocks of 64 pieces
-  constexpr int NI = NBLK / 2;                                             // per DMA wave (11)
-  static_assert(NBLK % 2 == 0 && G1_AP % 64 == 0, "DMA blocks");
-  const bool dmaw = wave >= 8;
-
-  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
-  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G1_TILE);
-  if (dmaw) {
-    // ---- DMA waves: piece q = 64 b + lane of a block sits at row 16 b + lane / 4 (of A,
-    // or of B past the A blocks), chunk unswz_c(lane); 32-bit element offsets from the
-    // uniform operand bases (M * 512 < 2^31: checked on the host)
-    const int p = wave - 8;
-    const int lrow = lane >> 2, lcol = unswz_c(lane) * 8;
-    auto issue = [&](int stage, int k0) {
-      int lr = lrow;
-      asm volatile("" : "+v"(lr));  // offsets rebuilt per stage: no hoisted per-block state
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int b = 2 * i + p;
-        if (b < G1_AP / 64) {
-          const int row = min((int)m0 + 16 * b + lr, M - 1);
-          __builtin_amdgcn_global_load_lds(GPTR(X + (row * K + lcol + k0)), LPTR(As + stage * G1_AP + b * 64), 16,
-                                           0, 0);
-        } else {
-          const int row = n0 + 16 * (b - G1_AP / 64) + lr;
-          __builtin_amdgcn_global_load_lds(GPTR(W1 + (row * K + lcol + k0)),
-                                           LPTR(Bs + stage * G1_BN * CPR + (b - G1_AP / 64) * 64), 16, 0, 0);
-        }
-      }
-    };
-    issue(0, 0);
-    issue(1, BK);
-#pragma unroll 1
-    for (int kt = 0; kt < NK; ++kt) {
-      if (kt + 1 < NK) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");   // stage kt landed, kt + 1 in flight
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (kt + 2 < NK) issue((kt + 2) % NSTAGE, (kt + 2) * BK);  // buffer last read in step kt - 1
-    }
-    __syncthreads();
-  } else {
-    // ---- MFMA waves: the g1dw_tile split (wave: column tile wave & 3, row tiles (wave >> 2) + 2t)
-    constexpr int TMX = 4;
-    const int wn = wave & 3, wr = wave >> 2;
-    const int ntm = wr == 0 ? 4 : 3;
-    f16_t acc[TMX];
-#pragma unroll
-    for (int i = 0; i < TMX; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-#pragma unroll 1
-    for (int kt = 0; kt < NK; ++kt) {
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const uint4* as = As + (kt % NSTAGE) * G1_AP;
-      const uint4* bs = Bs + (kt % NSTAGE) * G1_BN * CPR;
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        const int c = ks * 2 + (lane >> 5);
-        const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
-#pragma unroll
-        for (int i = 0; i < TMX; ++i) {
-          if (i < ntm) {
-            const int rt = wr + 2 * i;
-            const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    const int cl = wn * 32 + (lane & 31);
-#pragma unroll
-    for (int i = 0; i < TMX; ++i) {
-      if (i < ntm) {
-        const int rt = wr + 2 * i;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
-        }
-      }
-    }
-  }
-  for (int q = tid; q < 25 * (G1_BN / 2); q += 640) {
-    const int k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
-    wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
-  }
-  __syncthreads();
-
-  // depthwise 5x5: one (ROI, output row pair) task per wave
-  {
-    const int roi = wave / (G1_S / 2), y0 = 2 * (wave % (G1_S / 2));
-    const int64_t rbase = m0 + roi * G1_P;
-    if (rbase < M) {
-      const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2);
-      dw_pair_t a0[G1_S], a1[G1_S];
-#pragma unroll
-      for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const int yy = y0 - 2 + r;
-        if (yy < 0 || yy >= G1_S) continue;
-        dw_pair_t rr[G1_S];
-#pragma unroll
-        for (int x = 0; x < G1_S; ++x) {
-          const uint32_t v = src[(yy * G1_S + x) * (G1_BN / 2) + lane];
-          rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
-        }
-        if (r <= 4) {
-          dw_pair_t wv[5];
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G1_BN / 2) + lane];
-#pragma unroll
-          for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-            for (int kx = 0; kx < 5; ++kx)
-              if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
-        }
-        if (r >= 1) {
-          dw_pair_t wv[5];
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G1_BN / 2) + lane];
-#pragma unroll
-          for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-            for (int kx = 0; kx < 5; ++kx)
-              if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
-        }
-      }
-      uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
-#pragma unroll
-      for (int x = 0; x < G1_S; ++x) {
-        dst[(y0 * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a0[x].x, a0[x].y);
-        dst[((y0 + 1) * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a1[x].x, a1[x].y);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// g1dw with 256-channel N tiles (g1dw_mode 5): one 16-wave workgroup per CU per
-// tile of 2 ROIs x 256 channels.  Against the 128-channel tile it halves the
-// L2 -> LDS traffic of the A operand (each X row is staged 4 instead of 8 times:
-// 1.9 instead of 2.95 GB per launch), which the K loop pays for one-to-one
-// (DESIGN.md §4).  Waves: row parity wr = wave >> 3 (row tiles wr + 2t), column
-// tile wave & 7 (the g1dw_tile split over 8 column tiles).  Depthwise: 20 tasks
-// (ROI, output row pair, 128-channel half) over the 16 waves.  LDS: Y1 [200][128
-// pairs] + weights [25][128] (128 KiB), the operand ring aliased below it.
-constexpr int G2_BN = 256;
-constexpr size_t G2_STAGE = (size_t)(G1_ROWS + G2_BN) * CPR * 16;      // 30 KiB
-constexpr size_t G2_TILE = (size_t)2 * G1_P * (G2_BN / 2) * 4;         // 100 KiB
-constexpr size_t G2_W = (size_t)25 * (G2_BN / 2) * 8;                  // 25 KiB
-constexpr size_t G2_LDS = NSTAGE * G2_STAGE > G2_TILE + G2_W ? NSTAGE * G2_STAGE : G2_TILE + G2_W;
-static_assert(G2_LDS <= 160 * 1024, "g1dw256 LDS");
-
-__global__ void __launch_bounds__(1024) g1dw256_kernel(const uint16_t* __restrict__ X,
-                                                       const uint16_t* __restrict__ W1,
-                                                       const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                       int M, int N) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* As = reinterpret_cast<uint4*>(smem);          // [NSTAGE][224 * CPR]
-  uint4* Bs = As + NSTAGE * G1_AP;                      // [NSTAGE][256 * CPR]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave & 7, wr = wave >> 3;
-  const int ntile_n = N / G2_BN;
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int n0 = (int)(lb % ntile_n) * G2_BN;
-  const int64_t m0 = (lb / ntile_n) * (2 * G1_P);
-  constexpr int K = 512, NK = K / BK;
-  constexpr int BP = G2_BN * CPR;                       // B pieces per stage (1024)
-
-  // DMA: A pieces 0..895 (threads 0..895), B pieces 0..1023 (all threads)
-  const uint16_t* asrc;
-  {
-    const int p = min(tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
-    asrc = X + min(m0 + r, (int64_t)M - 1) * K + c * 8;
-  }
-  const uint16_t* bsrc = W1 + (int64_t)(n0 + tid / CPR) * K + unswz_c(tid) * 8;
-  const bool adma = wave < G1_AP / 64;                  // waves 0..13 stage A pieces
-  auto issue = [&](int stage, int k0) {
-    if (adma) __builtin_amdgcn_global_load_lds(GPTR(asrc + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * BP + wave * 64), 16, 0, 0);
-  };
-  constexpr int TMX = 4;
-  const int ntm = wr == 0 ? 4 : 3;
-  f16_t acc[TMX];
-#pragma unroll
-  for (int i = 0; i < TMX; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-
-  issue(0, 0);
-  issue(1, BK);
-  for (int kt = 0; kt < NK; ++kt) {
-    if (kt + 1 < NK) {
-      if (adma) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const uint4* as = As + (kt % NSTAGE) * G1_AP;
-    const uint4* bs = Bs + (kt % NSTAGE) * BP;
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int c = ks * 2 + (lane >> 5);
-      const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
-#pragma unroll
-      for (int i = 0; i < TMX; ++i) {
-        if (i < ntm) {
-          const int rt = wr + 2 * i;
-          const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
-        }
-      }
-    }
-    if (kt + 2 < NK) {  // after this step's MFMAs (g1dw_mode 1); the buffer was last read in step kt - 1
-      __builtin_amdgcn_sched_barrier(0);
-      issue((kt + 2) % NSTAGE, (kt + 2) * BK);
-    }
-  }
-  __syncthreads();
-
-  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
-  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + G2_TILE);
-  {
-    const int cl = wn * 32 + (lane & 31);
-#pragma unroll
-    for (int i = 0; i < TMX; ++i) {
-      if (i < ntm) {
-        const int rt = wr + 2 * i;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G2_BN + cl] = trk::f32_to_bf16(acc[i][r]);
-        }
-      }
-    }
-  }
-  for (int q = tid; q < 25 * (G2_BN / 2); q += 1024) {
-    const int k = q / (G2_BN / 2), pp = q % (G2_BN / 2);
-    wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
-  }
-  __syncthreads();
-
-  // depthwise 5x5: task = (ROI, output row pair, 128-channel half), lane = channel pair
-  for (int task = wave; task < 20; task += 16) {
-    const int roi = task / 10, rem = task % 10, y0 = 2 * (rem % 5), cp = (rem / 5) * 64 + lane;
-    const int64_t rbase = m0 + roi * G1_P;
-    if (rbase >= M) continue;
-    const uint32_t* src = y1 + roi * G1_P * (G2_BN / 2);
-    dw_pair_t a0[G1_S], a1[G1_S];
-#pragma unroll
-    for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const int yy = y0 - 2 + r;
-      if (yy < 0 || yy >= G1_S) continue;
-      dw_pair_t rr[G1_S];
-#pragma unroll
-      for (int x = 0; x < G1_S; ++x) {
-        const uint32_t v = src[(yy * G1_S + x) * (G2_BN / 2) + cp];
-        rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
-      }
-      if (r <= 4) {
-        dw_pair_t wv[5];
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G2_BN / 2) + cp];
-#pragma unroll
-        for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx)
-            if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
-      }
-      if (r >= 1) {
-        dw_pair_t wv[5];
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G2_BN / 2) + cp];
-#pragma unroll
-        for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx)
-            if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
-      }
-    }
-    uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + n0);
-#pragma unroll
-    for (int x = 0; x < G1_S; ++x) {
-      dst[(y0 * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a0[x].x, a0[x].y);
-      dst[((y0 + 1) * G1_S + x) * (N / 2) + cp] = pack_bf16x2(a1[x].x, a1[x].y);
-    }
-  }
-}
-
-// persistent: two workgroups per CU take tiles from the queue; each CU's second
-// workgroup starts offset x 2048 cycles late so its K loop runs beside the first
-// one's depthwise phase
-__global__ void __launch_bounds__(512) g1dw_persist_kernel(const uint16_t* __restrict__ X,
-                                                           const uint16_t* __restrict__ W1,
-                                                           const float* __restrict__ wdw,
-                                                           uint16_t* __restrict__ Y2, int M, int N, int dbg,
-                                                           int64_t ntiles, int qslot, int offset) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const TileQueue tq{g_tileq[qslot], ntiles};
-  if (offset > 0 && blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < offset; ++i) __builtin_amdgcn_s_sleep(32);
-  int cur = 0;
-  for (;;) {
-    const int64_t t = tq.next(reinterpret_cast<int*>(smem), cur);  // LDS is free between tiles
-    if (t < 0) break;
-    g1dw_tile<0>(X, W1, wdw, Y2, M, N, dbg, t, smem);
-    __syncthreads();  // the next tile's DMA reuses the LDS the depthwise phase read
-  }
-  tq.finish();
-}
-
-
-// ---------------------------------------------------------------------------
-// g1dw, interleaved (persistent, one workgroup per CU): the depthwise 5x5 of
-// the previous tile runs INSIDE the K loop of the current tile's GEMM, so its
-// VALU work fills the MFMA / LDS-DMA latency of the K loop instead of running
-// as a separate phase.  LDS: a 4-stage operand ring (three K steps in flight),
-// the previous tile's Y1 [200][64 pairs] and its depthwise weights.
-//   per tile t:  K step kt: barrier, DMA of step kt + 3, MFMAs of tile t, and on
-//                even kt one depthwise input-row step of tile t - 1;
-//                barrier; Y1(t) and weights(t) -> LDS; next tile.
-// Depthwise work per tile = 10 (ROI, output row pair) tasks = 52 valid input-row
-// steps: waves 0..5 own one interior task each (6 steps), waves 6..7 own the
-// two border tasks of one ROI (4 + 4 steps); every wave is done by K step 14.
-// Same arithmetic as g1dw_kernel (bit-identical).
-constexpr int IL_NST = 4;
-constexpr size_t IL_RING = (size_t)IL_NST * G1_STAGE;                 // 90112
-constexpr size_t IL_LDS = IL_RING + G1_TILE + G1_W + 16;               // 154128
-static_assert(IL_LDS <= 160 * 1024, "g1dw_il: one workgroup per CU");
-
-// one input row yy (kernel rows r / r - 1 for output rows y0 / y0 + 1)
-__device__ __forceinline__ void il_dw_row(const uint32_t* __restrict__ src, const dw_pair_t* __restrict__ wl, int yy,
-                                          int r, dw_pair_t (&a0)[G1_S], dw_pair_t (&a1)[G1_S], int cp) {
-  dw_pair_t rr[G1_S];
-#pragma unroll
-  for (int x = 0; x < G1_S; ++x) {
-    const uint32_t v = src[(yy * G1_S + x) * (G1_BN / 2) + cp];
-    rr[x] = dw_pair_t{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
-  }
-  if (r <= 4) {
-    dw_pair_t wv[5];
-#pragma unroll
-    for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[(r * 5 + kx) * (G1_BN / 2) + cp];
-#pragma unroll
-    for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-      for (int kx = 0; kx < 5; ++kx)
-        if (x + kx >= 2 && x + kx < G1_S + 2) a0[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a0[x]);
-  }
-  if (r >= 1) {
-    dw_pair_t wv[5];
-#pragma unroll
-    for (int kx = 0; kx < 5; ++kx) wv[kx] = wl[((r - 1) * 5 + kx) * (G1_BN / 2) + cp];
-#pragma unroll
-    for (int x = 0; x < G1_S; ++x)
-#pragma unroll
-      for (int kx = 0; kx < 5; ++kx)
-        if (x + kx >= 2 && x + kx < G1_S + 2) a1[x] = __builtin_elementwise_fma(wv[kx], rr[x + kx - 2], a1[x]);
-  }
-}
-
-__global__ void __launch_bounds__(512) g1dw_il_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                                      const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                      int M, int N, int64_t ntiles, int qslot) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* As = reinterpret_cast<uint4*>(smem);                     // [IL_NST][224 * CPR]
-  uint4* Bs = As + IL_NST * G1_AP;                                 // [IL_NST][128 * CPR]
-  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem + IL_RING);      // previous tile's Y1
-  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + IL_RING + G1_TILE);
-  int* slot = reinterpret_cast<int*>(smem + IL_RING + G1_TILE + G1_W);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave & 3, wr = wave >> 2;
-  const int ntile_n = N / G1_BN;
-  constexpr int K = 512, NK = K / BK;
-  const TileQueue tq{g_tileq[qslot], ntiles};
-  int cur = 0;
-  // depthwise plan of this wave: (roi, y0, first / last input-row step r)
-  const int d_roi = wave < 6 ? wave / 3 : wave - 6;
-  const int d_y0a = wave < 6 ? 2 * (1 + wave % 3) : 0;    // interior pair, or border pair 0
-  const int ops = wave < (G1_AP - 512) / 64 ? 3 : 2;      // DMA ops per stage of this wave
-
-  int64_t t = tq.next(slot, cur), tp = -1;
-  while (t >= 0 || tp >= 0) {
-    const bool gemm = t >= 0;
-    const int n0 = gemm ? (int)(t % ntile_n) * G1_BN : 0;
-    const int64_t m0 = gemm ? (t / ntile_n) * (2 * G1_P) : 0;
-    const uint16_t* asrc[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = min(q * 512 + tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
-      asrc[q] = X + min(m0 + r, (int64_t)M - 1) * K + c * 8;
-    }
-    const uint16_t* bsrc = W1 + (int64_t)(n0 + tid / CPR) * K + unswz_c(tid) * 8;
-    auto issue = [&](int stage, int k0) {
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
-      if (ops == 3)
-        __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
-    };
-    // previous tile's depthwise target
-    const int pn0 = tp >= 0 ? (int)(tp % ntile_n) * G1_BN : 0;
-    const int64_t prbase = tp >= 0 ? (tp / ntile_n) * (2 * G1_P) + d_roi * G1_P : M;
-    const bool dw = tp >= 0 && prbase < M;
-    const uint32_t* dsrc = y1 + d_roi * G1_P * (G1_BN / 2);
-    uint32_t* ddst = reinterpret_cast<uint32_t*>(Y2 + (dw ? prbase : 0) * N + pn0);
-    dw_pair_t a0[G1_S], a1[G1_S];
-
-    constexpr int TMX = 4;
-    const int ntm = wr == 0 ? 4 : 3;
-    f16_t acc[TMX];
-#pragma unroll
-    for (int i = 0; i < TMX; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-    if (gemm) {
-      issue(0, 0);
-      issue(1, BK);
-      issue(2, 2 * BK);
-    }
-#pragma unroll 1
-    for (int kt = 0; kt < NK; ++kt) {
-      if (gemm) {
-        // stage kt landed; kt + 1, kt + 2 (and at most one step's Y2 stores) may stay in flight
-        if (kt + 2 < NK) {
-          if (ops == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else if (kt + 1 < NK) {
-          if (ops == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      }
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (gemm) {
-        if (kt + 3 < NK) issue((kt + 3) % IL_NST, (kt + 3) * BK);
-        const uint4* as = As + (kt % IL_NST) * G1_AP;
-        const uint4* bs = Bs + (kt % IL_NST) * G1_BN * CPR;
-#pragma unroll
-        for (int ks = 0; ks < BK / 16; ++ks) {
-          const int c = ks * 2 + (lane >> 5);
-          const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
-#pragma unroll
-          for (int i = 0; i < TMX; ++i) {
-            if (i < ntm) {
-              const int rt = wr + 2 * i;
-              const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
-              acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
-            }
-          }
-        }
-      }
-      // one depthwise input-row step of the previous tile on even K steps
-      if (dw && !(kt & 1)) {
-        const int s = kt >> 1;
-        int y0, r;
-        if (wave < 6) { y0 = d_y0a; r = s; }
-        else if (s < 4) { y0 = 0; r = s + 2; }          // border pair 0: input rows 0..3
-        else { y0 = 8; r = s - 4; }                      // border pair 4: input rows 6..9
-        const bool active = wave < 6 ? s < 6 : true;
-        if (active) {
-          const bool first = wave < 6 ? s == 0 : (s == 0 || s == 4);
-          const bool last = wave < 6 ? s == 5 : (s == 3 || s == 7);
-          if (first) {
-#pragma unroll
-            for (int x = 0; x < G1_S; ++x) { a0[x] = dw_pair_t{0.f, 0.f}; a1[x] = dw_pair_t{0.f, 0.f}; }
-          }
-          il_dw_row(dsrc, wl, y0 - 2 + r, r, a0, a1, lane);
-          if (last) {
-#pragma unroll
-            for (int x = 0; x < G1_S; ++x) {
-              ddst[(y0 * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a0[x].x, a0[x].y);
-              ddst[((y0 + 1) * G1_S + x) * (N / 2) + lane] = pack_bf16x2(a1[x].x, a1[x].y);
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();  // every read of Y1(tp) / weights(tp) and of the ring is done
-    if (gemm) {
-      const int cl = wn * 32 + (lane & 31);
-#pragma unroll
-      for (int i = 0; i < TMX; ++i) {
-        if (i < ntm) {
-          const int rt = wr + 2 * i;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
-          }
-        }
-      }
-      for (int q = tid; q < 25 * (G1_BN / 2); q += 512) {
-        const int k = q / (G1_BN / 2), pp = q % (G1_BN / 2);
-        wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * pp);
-      }
-    }
-    tp = t;
-    t = gemm ? tq.next(slot, cur) : -1;  // next() ends with a barrier: Y1 / weights visible
-    if (!gemm) break;                     // the drain pass ran the last tile's depthwise
-  }
-  tq.finish();
-}
-
-// ---------------------------------------------------------------------------
-// g1dw, role-split (g1dw_mode 6; persistent, one 16-wave workgroup per CU):
-// waves 0..7 run the GEMM of tile t (the g1dw_il_kernel K loop, 4-stage ring),
-// waves 8..15 run the depthwise 5x5 of tile t - 1 from LDS at the same time,
-// as g1dw_kernel's straight-line (ROI, quadrant) tasks.  An MFMA holds its
-// SIMD's vector issue for 8 of its 32 cycles, so the depthwise VALU of the
-// partner waves can fill the other 24 (MI355X_MICROARCH.md, vector-instruction
-// issue cost).  The GEMM waves do not use s_barrier inside the K loop (the
-// depthwise waves would have to take part): each arrives on an LDS counter
-// once its DMA pieces of the step have landed and waits until all 8 have
-// (also the ring's write-after-read guard: a wave arrives after its reads of
-// the previous step).  Tile boundaries use s_barrier for all 16 waves.
-// Bit-identical to g1dw_kernel.  Measured (tools/exp/enc_breakdown.py, 2048 ROIs):
-// 646-721 us against g1dw_kernel<1>'s 486-492.  The depthwise does overlap (it adds
-// 70-120 us here, 180 there), but the counter handshake costs ~900 cycles per K
-// step (406 us with neither MFMAs nor depthwise); an earlier form that kept the K
-// loop's s_barrier for all 16 waves (one depthwise input row per two K steps)
-// measured 711 us: the coupled row steps were latency-bound.  Kept as a knob.
-__device__ __forceinline__ void sp_arrive_wait(uint32_t addr, uint32_t target) {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\tds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
-  uint32_t v;
-  for (;;) {
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-    if (__builtin_amdgcn_readfirstlane(v) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-__global__ void __launch_bounds__(1024) g1dw_sp_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                                       const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                       int M, int N, int64_t ntiles, int qslot, int dbg) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* As = reinterpret_cast<uint4*>(smem);                     // [IL_NST][224 * CPR]
-  uint4* Bs = As + IL_NST * G1_AP;                                 // [IL_NST][128 * CPR]
-  uint32_t* y1 = reinterpret_cast<uint32_t*>(smem + IL_RING);      // previous tile's Y1
-  dw_pair_t* wl = reinterpret_cast<dw_pair_t*>(smem + IL_RING + G1_TILE);
-  int* slot = reinterpret_cast<int*>(smem + IL_RING + G1_TILE + G1_W);
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(slot + 1);           // K-step arrivals (64 per wave)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool mma = wave < 8;
-  const int wn = wave & 3, wr = (wave >> 2) & 1;
-  const int ntile_n = N / G1_BN;
-  constexpr int K = 512, NK = K / BK;
-  const TileQueue tq{g_tileq[qslot], ntiles};
-  int cur = 0;
-  const int ops = wave < (G1_AP - 512) / 64 ? 3 : 2;
-  if (threadIdx.x == 0) *cnt = 0;
-  uint32_t arrivals = 0;                                           // steps this wave has completed
-
-  int64_t t = tq.next(slot, cur), tp = -1;                         // next() ends with a barrier
-  while (t >= 0 || tp >= 0) {
-    int tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));  // per tile: keep lane addresses out of the tile loop (no spills)
-    const int lane = tid & 63;
-    const bool gemm = t >= 0;
-    const int n0 = gemm ? (int)(t % ntile_n) * G1_BN : 0;
-    const int64_t m0 = gemm ? (t / ntile_n) * (2 * G1_P) : 0;
-    if (mma) {
-      constexpr int TMX = 4;
-      const int ntm = wr == 0 ? 4 : 3;
-      f16_t acc[TMX];
-      const uint16_t* asrc[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int p = min(q * 512 + tid, G1_AP - 1), r = p / CPR, c = unswz_c(p);
-        asrc[q] = X + min(m0 + r, (int64_t)M - 1) * K + c * 8;
-      }
-      const uint16_t* bsrc = W1 + (int64_t)(n0 + tid / CPR) * K + unswz_c(tid) * 8;
-      auto issue = [&](int stage, int k0) {
-        __builtin_amdgcn_global_load_lds(GPTR(asrc[0] + k0), LPTR(As + stage * G1_AP + wave * 64), 16, 0, 0);
-        if (ops == 3)
-          __builtin_amdgcn_global_load_lds(GPTR(asrc[1] + k0), LPTR(As + stage * G1_AP + 512 + wave * 64), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(GPTR(bsrc + k0), LPTR(Bs + stage * G1_BN * CPR + wave * 64), 16, 0, 0);
-      };
-#pragma unroll
-      for (int i = 0; i < TMX; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-      if (gemm) {
-        issue(0, 0);
-        issue(1, BK);
-        issue(2, 2 * BK);
-#pragma unroll 1
-        for (int kt = 0; kt < NK; ++kt) {
-          if (kt + 2 < NK) {
-            if (ops == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          } else if (kt + 1 < NK) {
-            if (ops == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-          } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          ++arrivals;
-          sp_arrive_wait((uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)cnt), arrivals * 8 * 64);
-          if (dbg & 64) continue;  // experiment: no MFMAs / further loads
-          if (kt + 3 < NK) issue((kt + 3) % IL_NST, (kt + 3) * BK);
-          const uint4* as = As + (kt % IL_NST) * G1_AP;
-          const uint4* bs = Bs + (kt % IL_NST) * G1_BN * CPR;
-#pragma unroll
-          for (int ks = 0; ks < BK / 16; ++ks) {
-            const int c = ks * 2 + (lane >> 5);
-            const bf8_t bfr = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * 32 + (lane & 31), c)]);
-#pragma unroll
-            for (int i = 0; i < TMX; ++i) {
-              if (i < ntm) {
-                const int rt = wr + 2 * i;
-                const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(rt * 32 + (lane & 31), c)]);
-                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[i], 0, 0, 0);
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();  // (with the depthwise waves') every read of Y1(tp) and of the ring is done
-      if (gemm) {
-        const int cl = wn * 32 + (lane & 31);
-#pragma unroll
-        for (int i = 0; i < TMX; ++i) {
-          if (i < ntm) {
-            const int rt = wr + 2 * i;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int rl = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-              if (rl < 2 * G1_P) reinterpret_cast<uint16_t*>(y1)[rl * G1_BN + cl] = trk::f32_to_bf16(acc[i][r]);
-            }
-          }
-        }
-      }
-    } else {
-      // depthwise 5x5 of the previous tile: wave = (ROI, 5x5 output quadrant), lane = channel pair
-      const int dwv = wave - 8, roi = dwv >> 2, quad = dwv & 3;
-      const int64_t rbase = tp >= 0 ? (tp / ntile_n) * (2 * G1_P) + roi * G1_P : M;
-      if (rbase < M && !(dbg & 16)) {   // dbg 16 (experiment): no depthwise
-        const int pn0 = (int)(tp % ntile_n) * G1_BN;
-        const uint32_t* src = y1 + roi * G1_P * (G1_BN / 2) + lane;
-        const dw_pair_t* wq = wl + lane;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + rbase * N + pn0) + lane;
-        switch (quad) {
-          case 0: dw5_quadrant<0, 0>(src, wq, dst, N / 2); break;
-          case 1: dw5_quadrant<0, 1>(src, wq, dst, N / 2); break;
-          case 2: dw5_quadrant<1, 0>(src, wq, dst, N / 2); break;
-          default: dw5_quadrant<1, 1>(src, wq, dst, N / 2); break;
-        }
-      }
-      __syncthreads();  // (with the GEMM waves') every read of weights(tp) is done
-      if (gemm) {
-        for (int q = tid - 512; q < 25 * (G1_BN / 2); q += 512) {
-          const int kk = q / (G1_BN / 2), pp = q % (G1_BN / 2);
-          wl[q] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)kk * N + n0 + 2 * pp);
-        }
-      }
-    }
-    tp = t;
-    t = gemm ? tq.next(slot, cur) : -1;  // next() ends with a barrier: Y1 / weights visible
-    if (!gemm) break;                     // the drain pass ran the last tile's depthwise
-  }
-  tq.finish();
-}
+constexpr int G1_BN = 128, G1_S = 10, G1_P = 100;  // g1dw4: N tile, ROI side, ROI rows
 
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -1468,7 +463,7 @@ static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
 
 // WIDE (P >= 64): a wave's 64 rows span at most 2 ROIs and a tile's 128 at most 3, so
 // the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions)
-template <int EPI, bool WIDE = false, int HSWM = -1>
+template <int EPI, bool WIDE, int HSWM>
 __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, unsigned char* smem) {
   uint4* ring = reinterpret_cast<uint4*>(smem);
   // opaque per tile: keeps the compiler from hoisting lane-dependent addresses
@@ -1618,16 +613,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   }
 
   if (prof) pst[1] = eg_stamp();
-  if (a.dbg & 1) {
-    if (tid == 0 && acc[0][0][0] == 12345.f) a.sums[0] = 1;
-    return;
-  }
   // ---- epilogue (the ring is free: every DMA retired, all reads done at the last barrier)
   const int colq = wc * 128 + fr;  // + t * 16
-  // HSWM: -1 = the DSC group decides per tile (a select per element pair, which the compiler
-  // turns into 64 branches, each a dependent exp / rcp chain padded with s_nops); 0 / 1 = the
-  // tile's activation is known at compile time (straight-line SiLU or Hardswish)
-  const bool hsw = HSWM < 0 ? (EPI == EPI_DSC && g == 1) : HSWM == 1;
+  // HSWM: the tile's activation, known at compile time (straight-line SiLU or Hardswish)
+  const bool hsw = EPI == EPI_DSC && HSWM == 1;
   float bias8[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) bias8[t] = a.bias[g * a.N + n0 + colq + t * 16];  // one batch of loads
@@ -1652,7 +641,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
   // consumer adds llrintf(p0 * 2^24) + llrintf(p1 * 2^24) (the former int64 atomics' sum)
   float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [2][SLOTS][256]
-  if (!(a.dbg & 4)) {
+  {
     const int64_t r0w = m0 + wr * 64;
     const int64_t roiw = r0w / a.P;
     const int wslot0 = (int)(roiw - roi_base);
@@ -1712,7 +701,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
     }
   }
   if (prof) pst[3] = eg_stamp();
-  if (EPI == EPI_DSC && !(a.dbg & 2)) {
+  if (EPI == EPI_DSC) {
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
     const bool odd = fr & 1;
 #pragma unroll
@@ -1733,17 +722,16 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   {
     const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
     const int nslot = (int)(last_row / a.P - roi_base) + 1;
-    if (!(a.dbg & 8))
-      for (int q = tid; q < nslot * 256; q += 256) {
-        const int slot = q >> 8, c = q & 255;
-        const int64_t roi = roi_base + slot;
-        const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
-        a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] =
-            llrintf(part[slot * 256 + c] * kFix) + llrintf(part[(G4_SLOTS + slot) * 256 + c] * kFix);
-      }
+    for (int q = tid; q < nslot * 256; q += 256) {
+      const int slot = q >> 8, c = q & 255;
+      const int64_t roi = roi_base + slot;
+      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
+      a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] =
+          llrintf(part[slot * 256 + c] * kFix) + llrintf(part[(G4_SLOTS + slot) * 256 + c] * kFix);
+    }
   }
   if (prof) pst[5] = eg_stamp();
-  if (EPI == EPI_DSC && !(a.dbg & 2)) {
+  if (EPI == EPI_DSC) {
     const uint32_t* stage = reinterpret_cast<const uint32_t*>(smem);
     const int64_t cbase = (int64_t)g * a.N + n0;
 #pragma unroll 4
@@ -1767,35 +755,15 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   }
 }
 
-// Persistent: 2 workgroups per CU walk the tiles (XCD-remapped).  The second
-// resident of each CU starts a fraction of a tile late (enc_gemm_offset x
-// 2048-cycle sleeps), so the two workgroups sharing a CU stay out of phase:
-// one's MFMA loop runs under the other's VALU / store epilogue instead of both
-// alternating between them in lockstep.
+// one workgroup per tile (XCD-remapped); a DSC tile's group (SiLU / Hardswish) is a
+// template argument of its body, so each body is straight-line (a per-element select
+// was compiled into 64 branches of nop-padded exp / rcp chains)
 template <int EPI, bool WIDE>
-__global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles, int offset, int qslot) {
+__global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles) {
   extern __shared__ __align__(16) unsigned char smem[];
-  if (qslot < 0) {  // one workgroup per tile
-    const int64_t lb = xcd_remap(blockIdx.x, ntiles);
-    if (EPI == EPI_DSC && a.hsplit) {  // the tile's group (SiLU / Hardswish) as a template argument
-      if ((lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1>(a, lb, smem);
-      else gemm4_tile<EPI, WIDE, 0>(a, lb, smem);
-    } else {
-      gemm4_tile<EPI, WIDE>(a, lb, smem);
-    }
-    return;
-  }
-  const TileQueue tq{g_tileq[qslot], ntiles};
-  if (offset > 0 && blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < offset; ++i) __builtin_amdgcn_s_sleep(32);
-  int cur = 0;
-  for (;;) {
-    const int64_t t = tq.next(reinterpret_cast<int*>(smem), cur);  // LDS is free between tiles
-    if (t < 0) break;
-    gemm4_tile<EPI, WIDE>(a, t, smem);
-    __syncthreads();  // the next tile's DMA reuses the LDS the epilogue read
-  }
-  tq.finish();
+  const int64_t lb = xcd_remap(blockIdx.x, ntiles);
+  if (EPI == EPI_DSC && (lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1>(a, lb, smem);
+  else gemm4_tile<EPI, WIDE, 0>(a, lb, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -1882,14 +850,13 @@ __device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, cons
 #pragma unroll
     for (int ox = 0; ox < 5; ++ox) {
       const uint32_t v = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
-      if (ldd > 0) dst[((OY0 + oy) * G1_S + X0 + ox) * ldd] = v;
-      else asm volatile("" ::"v"(v));  // experiment (enc_gemm_dbg 256): no Y2 stores
+      dst[((OY0 + oy) * G1_S + X0 + ox) * ldd] = v;
     }
 }
 
 __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
                                                         const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                        int M, int N, int dbg) {
+                                                        int M, int N) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint4* ring = reinterpret_cast<uint4*>(smem);
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -1917,7 +884,6 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
     bsrc[q] = W1 + (int64_t)(n0 + r) * K + c * 8;
   }
   auto issue = [&](int kt) {
-    if (dbg & 128) return;  // experiment: no operand loads
     uint4* d = ring + (kt % 3) * G1Q_BUF + wave * 64;
 #pragma unroll
     for (int q = 0; q < 3; ++q)
@@ -1929,7 +895,6 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
   };
   // retire all but the newest stage's DMA ops (wave 0 issues 6 per stage, the others 5)
   auto wait_prev = [&]() {
-    if (dbg & 128) return;
     if (wave == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   };
@@ -1946,14 +911,14 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (dbg & 32) ? 2 : NK;
+  const int nk = NK;
   issue(0);
   issue(1);
   wait_prev();
   g4_barrier();
   for (int kt = 0; kt < nk; ++kt) {
     const uint4* buf = ring + (kt % 3) * G1Q_BUF;
-    if (!(dbg & 64)) {  // dbg 64 (experiment): no MFMAs
+    {
       // 11 fragment reads up front (wr = 1's seventh reads B slots, unused), then counted
       // lgkmcnt waits: row tile i's MFMAs start once its A fragment has landed
       const uint32_t bb = lds_addr(buf + boff), ab = lds_addr(buf + aoff);
@@ -2018,9 +983,8 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
   }
   __syncthreads();
 
-  if (dbg & 16) return;
   // depthwise 5x5: wave = output quadrant, for each of the two ROIs; lane = channel pair
-  const int ldd = (dbg & 256) ? 0 : N / 2;
+  const int ldd = N / 2;
 #pragma unroll 1
   for (int roi = 0; roi < 2; ++roi) {
     const int64_t rbase = m0 + roi * G1_P;
@@ -2038,379 +1002,10 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
   }
 }
 
-// ---------------------------------------------------------------------------
-// gemm8: 256 x 256 tiles, BK = 64, one 8-wave workgroup per CU (waves 2 (M) x 4
-// (N), wave tile 128 x 64 = 8 x 4 MFMA 16x16x32 tiles: 0.375 KB of fragment
-// reads per MFMA).  Both operands are staged by LDS-DMA into two 64 KiB K-tile
-// buffers: tile kt + 1's 8 loads per thread are issued at the top of step kt
-// and have the whole step's MFMAs to land; one vmcnt(0) + barrier per step.
-// The LDS image of a 256 x 64 operand is 16-B chunk c of row r at r * 8 + (c ^
-// ((r >> 1) & 7)) -- the 16-lane groups of every ds_read_b128 hit 16 distinct
-// bank groups -- laid down lane-linearly by the DMA (the XOR is applied to the
-// per-lane source address).  The SE scale of the transition is applied in LDS by
-// the thread that staged each chunk (its own vmcnt(0) orders it), before the
-// step's barrier.  Epilogue (transition): bias + SiLU + per-ROI column sums; a
-// wave's 128 rows are exactly one 128-row partial tile of the ROI sums.
-constexpr int G8_BM = 256, G8_BN = 256, G8_BK = 64, G8_CH = G8_BK / 8;
-constexpr int G8_POS = G8_BM * G8_CH;                          // 16-B slots of one operand image (2048)
-constexpr size_t G8_BUF = (size_t)2 * G8_POS * 16;             // A + B images of one K tile: 64 KiB
-constexpr int G8_SROI = 4;                                      // ROIs a 256-row tile spans (P >= 86)
-constexpr size_t G8_STILE = (size_t)G8_SROI * 512 * 4;          // s rows of those ROIs (kscale <= 512)
-constexpr size_t G8_LDS = 2 * G8_BUF + G8_STILE;               // 136 KiB
-
-__device__ __forceinline__ int g8_swz(int r, int c) { return r * G8_CH + (c ^ ((r >> 1) & 7)); }
-
-__device__ __forceinline__ unsigned long long g8_stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
-// PROF (trk_enc_set_prof, diagnostics only): waves 0 and 4 of each workgroup record
-// [start, prologue done, K loop done, end, sum of the per-step vmcnt waits, sum of
-// the per-step barrier waits, hw id, 0] at prof[(wg * 2 + wave / 4) * 8]
-// MF = 0: v_mfma_f32_16x16x32_bf16, wave tile 8 x 4 MFMA tiles; MF = 1:
-// v_mfma_f32_32x32x16_bf16, 4 x 2 tiles (half the MFMA instructions; at two waves
-// per SIMD a 32x32x16 retires 33 % more flops per cycle than two 16x16x32 --
-// tools/exp/clock_probe.hip).  Same LDS images and fragment bytes.
-template <int EPI, bool PROF, int MF>
-__global__ void __launch_bounds__(512) gemm8_kernel(EncGemmArgs a, int64_t ntiles, unsigned long long* prof) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* bufs = reinterpret_cast<uint4*>(smem);                // [2][A 2048 | B 2048] uint4
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int64_t lb = xcd_remap(blockIdx.x, ntiles);
-  const int ntile_n = a.N / G8_BN;
-  const int ntl = (int)(lb % (ntile_n * a.groups));
-  const int64_t mt = lb / (ntile_n * a.groups);
-  const int g = ntl / ntile_n, n0 = (ntl % ntile_n) * G8_BN;
-  const int64_t m0 = mt * G8_BM;
-  const uint16_t* Ag = a.A + (int64_t)g * a.K;
-  const uint16_t* Bg = a.B + (int64_t)g * a.N * a.K;
-  const int nk = a.K / G8_BK;
-  const int64_t roi_base = m0 / a.P;
-
-  // DMA sources: slot p = q * 512 + tid of each image (row p >> 3, data chunk by the swizzle)
-  const uint16_t* asrc[4];
-  const uint16_t* bsrc[4];
-  int achunk[4], arow[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int p = q * 512 + tid, r = p >> 3, c = (p & 7) ^ ((r >> 1) & 7);
-    arow[q] = r;
-    achunk[q] = c;
-    asrc[q] = Ag + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
-    bsrc[q] = Bg + (int64_t)(n0 + r) * a.K + c * 8;
-  }
-  auto issue = [&](int kt) {
-    uint4* d = bufs + (kt & 1) * (2 * G8_POS) + wave * 64;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * G8_BK), LPTR(d + q * 512), 16, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + kt * G8_BK), LPTR(d + G8_POS + q * 512), 16, 0, 0);
-  };
-
-  // transition: the SE scales of the tile's ROIs (LDS, [G8_SROI][kscale] f32) and, per staged
-  // chunk, the s row it is scaled with
-  const float* stile = reinterpret_cast<const float*>(smem + 2 * G8_BUF);
-  int srow[4];
-  if constexpr (EPI == EPI_TRANS) {
-    const int per = a.kscale / 4;                       // 16-B pieces per s row
-    const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
-    for (int p = tid; p < G8_SROI * per; p += 512) {
-      const int slot = p / per;
-      const int64_t roi = min(roi_base + slot, nroi - 1);
-      reinterpret_cast<float4*>(smem + 2 * G8_BUF)[p] =
-          *reinterpret_cast<const float4*>(a.scale + roi * a.kscale + (p % per) * 4);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t row = min(m0 + arow[q], (int64_t)a.M - 1);
-      srow[q] = (int)(row / a.P - roi_base) * a.kscale + achunk[q] * 8;
-    }
-  }
-  auto transform = [&](int kt) {  // x_f columns of K tile kt: bf16(x * s[roi][k])
-    if constexpr (EPI == EPI_TRANS) {
-      if (kt * G8_BK < a.kscale) {
-        uint4* d = bufs + (kt & 1) * (2 * G8_POS);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint4 v = d[q * 512 + tid];
-          const float4 s0 = *reinterpret_cast<const float4*>(stile + srow[q] + kt * G8_BK);
-          const float4 s1 = *reinterpret_cast<const float4*>(stile + srow[q] + kt * G8_BK + 4);
-          const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            w[e] = pack_bf16x2(__uint_as_float(w[e] << 16) * sv[2 * e], __uint_as_float(w[e] & 0xffff0000u) * sv[2 * e + 1]);
-          d[q * 512 + tid] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-      }
-    }
-  };
-
-  typename std::conditional<MF == 0, f4v[8][4], f16_t[4][2]>::type acc;
-  if constexpr (MF == 0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][t][e] = 0.f;
-  }
-
-  const int fr = lane & 15, fc = lane >> 4;
-  const int f32r = lane & 31, f32h = lane >> 5;
-  unsigned long long p_t0 = 0, p_t1 = 0, p_t2 = 0, p_w = 0, p_b = 0;
-  if constexpr (PROF) p_t0 = g8_stamp();
-  issue(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // s tile (plain stores) visible before the first transform
-  transform(0);
-  __syncthreads();
-  if constexpr (PROF) p_t1 = g8_stamp();
-  // K step: 16 MFMA groups s = (k half h, row tile i), 4 MFMAs each; the A fragment of
-  // group s + 1 (and the next half's B fragments) are read while group s runs, and the
-  // next K tile's 8 LDS-DMA pieces are issued one per odd group, between MFMAs
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool pf = kt + 1 < nk;
-    const uint4* ab = bufs + (kt & 1) * (2 * G8_POS);
-    const uint4* bb = ab + G8_POS;
-    uint4* dn = bufs + ((kt + 1) & 1) * (2 * G8_POS) + wave * 64;
-    auto issue_piece = [&](int q) {  // piece q: A slots q*512.. (q < 4), B slots (q - 4)*512..
-      if (q < 4)
-        __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + (kt + 1) * G8_BK), LPTR(dn + q * 512), 16, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds(GPTR(bsrc[q - 4] + (kt + 1) * G8_BK), LPTR(dn + G8_POS + (q - 4) * 512), 16, 0, 0);
-    };
-    if constexpr (MF == 0) {
-      auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 7) * 16 + fr, (s >> 3) * 4 + fc)); };
-      bf8v bfr[2][4];
-  #pragma unroll
-      for (int t = 0; t < 4; ++t) bfr[0][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, fc));
-      bf8v afr = rd_a(0);
-  #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int h = s >> 3, i = s & 7;
-        bf8v anext = afr;
-        if (s < 15) anext = rd_a(s + 1);
-        if (s == 4) {
-  #pragma unroll
-          for (int t = 0; t < 4; ++t) bfr[1][t] = *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 16 + fr, 4 + fc));
-        }
-  #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[h][t], acc[i][t], 0, 0, 0);
-        if (pf && (s & 1)) issue_piece(s >> 1);
-        afr = anext;
-      }
-    } else {
-      // 16 groups s = (k step ks = s >> 2, row tile i = s & 3), 2 MFMAs each; lane (r, h)
-      // reads 16 B of row r at chunk 2 ks + h
-      auto rd_a = [&](int s) { return *reinterpret_cast<const bf8v*>(ab + g8_swz(wr * 128 + (s & 3) * 32 + f32r, (s >> 2) * 2 + f32h)); };
-      auto rd_b = [&](int ks, int t) { return *reinterpret_cast<const bf8v*>(bb + g8_swz(wc * 64 + t * 32 + f32r, ks * 2 + f32h)); };
-      const bool top = a.dbg & 512;  // experiment: the next K tile's 8 DMA pieces all before the MFMAs
-      if (pf && top) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) issue_piece(q);
-      }
-      bf8v bfr[2][2];
-      bfr[0][0] = rd_b(0, 0);
-      bfr[0][1] = rd_b(0, 1);
-      bf8v afr = rd_a(0);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int ks = s >> 2, i = s & 3;
-        bf8v anext = afr;
-        if (s < 15) anext = rd_a(s + 1);
-        if (i == 1 && ks < 3) {
-          bfr[(ks + 1) & 1][0] = rd_b(ks + 1, 0);
-          bfr[(ks + 1) & 1][1] = rd_b(ks + 1, 1);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[ks & 1][t], acc[i][t], 0, 0, 0);
-        if (pf && !top && (s & 1)) issue_piece(s >> 1);
-        afr = anext;
-      }
-    }
-    unsigned long long pa = 0, pb = 0;
-    if constexpr (PROF) pa = g8_stamp();
-    if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (PROF) pb = g8_stamp();
-      transform(kt + 1);
-    } else if constexpr (PROF) {
-      pb = pa;
-    }
-    __syncthreads();
-    if constexpr (PROF) {
-      const unsigned long long pc = g8_stamp();
-      p_w += pb - pa;
-      p_b += pc - pb;
-    }
-  }
-  if constexpr (PROF) p_t2 = g8_stamp();
-
-  if constexpr (EPI == EPI_TRANS) {
-    // bias + SiLU + per-ROI column sums over this wave's 128 rows (one partial tile)
-    const int64_t r0 = m0 + wr * 128;
-    const int P = a.P;
-    const int64_t roi0 = r0 / P;
-    const int nxt = P - (int)(r0 - roi0 * P);   // first row (within the 128) of ROI roi0 + 1
-    const bool full = r0 + 128 <= (int64_t)a.M;
-    const int64_t last = min(r0 + 128, (int64_t)a.M) - 1;
-    const int nslot = (int)(last / P - roi0) + 1;
-    const int64_t th = r0 / kPartRows;
-    if constexpr (MF == 0) {
-      float bias4[4];
-  #pragma unroll
-      for (int t = 0; t < 4; ++t) bias4[t] = a.bias[n0 + wc * 64 + t * 16 + fr];
-  #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        float sm[3] = {0.f, 0.f, 0.f};
-  #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          f4v v = acc[i][t];
-  #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e] + bias4[t]);
-          const int lo = i * 16;
-          if (full && lo + 16 <= nxt) {
-            sm[0] += (v[0] + v[1]) + (v[2] + v[3]);
-          } else if (full && lo >= nxt && lo + 16 <= nxt + P) {
-            sm[1] += (v[0] + v[1]) + (v[2] + v[3]);
-          } else if (full && lo >= nxt + P) {
-            sm[2] += (v[0] + v[1]) + (v[2] + v[3]);
-          } else {
-  #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int ro = lo + fc * 4 + e;
-              const float x = (r0 + ro < a.M) ? v[e] : 0.f;
-              sm[0] += ro < nxt ? x : 0.f;
-              sm[1] += (ro >= nxt && ro < nxt + P) ? x : 0.f;
-              sm[2] += ro >= nxt + P ? x : 0.f;
-            }
-          }
-        }
-  #pragma unroll
-        for (int q = 0; q < 3; ++q) sm[q] = sum_xor32(sum_xor16(sm[q]));
-        if (fc == 0) {
-  #pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            if (q < nslot) {
-              const int64_t roi = roi0 + q;
-              const int j = (int)(th - roi * P / kPartRows);
-              a.sums[(roi * kPart + j) * a.ld_sums + (int64_t)g * a.N + n0 + wc * 64 + t * 16 + fr] =
-                  llrintf(sm[q] * kFix);
-            }
-          }
-        }
-      }
-    } else {
-      // 32x32 tiles: lane (c = lane & 31, h) holds rows (r & 3) + 8 (r >> 2) + 4 h of
-      // column c in register r
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int col = n0 + wc * 64 + t * 32 + f32r;
-        const float bias = a.bias[col];
-        float sm[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          f16_t v = acc[i][t];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) v[e] = silu_f(v[e] + bias);
-          const int lo = i * 32;
-          if (full && (lo + 32 <= nxt || (lo >= nxt && lo + 32 <= nxt + P) || lo >= nxt + P)) {
-            float x = 0.f;
-#pragma unroll
-            for (int e = 0; e < 16; e += 4) x += (v[e] + v[e + 1]) + (v[e + 2] + v[e + 3]);
-            const int q = lo + 32 <= nxt ? 0 : lo + 32 <= nxt + P ? 1 : 2;
-            sm[0] += q == 0 ? x : 0.f;
-            sm[1] += q == 1 ? x : 0.f;
-            sm[2] += q == 2 ? x : 0.f;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              const int ro = lo + (e & 3) + 8 * (e >> 2) + 4 * f32h;
-              const float x = (r0 + ro < a.M) ? v[e] : 0.f;
-              sm[0] += ro < nxt ? x : 0.f;
-              sm[1] += (ro >= nxt && ro < nxt + P) ? x : 0.f;
-              sm[2] += ro >= nxt + P ? x : 0.f;
-            }
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) sm[q] = sum_xor32(sm[q]);
-        if (f32h == 0) {
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            if (q < nslot) {
-              const int64_t roi = roi0 + q;
-              const int j = (int)(th - roi * P / kPartRows);
-              a.sums[(roi * kPart + j) * a.ld_sums + (int64_t)g * a.N + col] = llrintf(sm[q] * kFix);
-            }
-          }
-        }
-      }
-    }
-  }
-  if constexpr (PROF) {
-    const unsigned long long p_t3 = g8_stamp();
-    if ((wave & 3) == 0 && lane == 0) {
-      unsigned long long* o = prof + ((int64_t)blockIdx.x * 2 + (wave >> 2)) * 8;
-      unsigned hw;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      o[0] = p_t0; o[1] = p_t1; o[2] = p_t2; o[3] = p_t3; o[4] = p_w; o[5] = p_b; o[6] = hw; o[7] = 0;
-    }
-  }
-}
-
-
-template <int EPI, int MF>
-int launch8(const EncGemmArgs& a, hipStream_t st) {
-  const int64_t nwg = ((int64_t)a.M + G8_BM - 1) / G8_BM * (a.N / G8_BN) * a.groups;
-  TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm8: too many workgroups");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, false, MF>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<EPI, true, MF>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS);
-    attr = true;
-  }
-  if (g_enc_prof)
-    hipLaunchKernelGGL((gemm8_kernel<EPI, true, MF>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, g_enc_prof);
-  else
-    hipLaunchKernelGGL((gemm8_kernel<EPI, false, MF>), dim3((unsigned)nwg), dim3(512), G8_LDS, st, a, nwg, nullptr);
-  return trk::check_launch("gemm8_kernel");
-}
-
-int cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm4: too many workgroups");
-  // persistent grid (enc_gemm_offset > 0) or one workgroup per tile (0, the default: in the
-  // pipeline the GEMMs share the GPU with the tracker's kernels, and a persistent grid then
-  // waits for CUs the tracker still holds)
-  const int64_t grid = g_enc_gemm_offset > 0 ? std::min<int64_t>(nwg, 2 * (int64_t)cu_count()) : nwg;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, false>),
@@ -2420,19 +1015,13 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
     attr = true;
   }
   EncGemmArgs b = a;
-  b.dbg = g_enc_gemm_dbg;
-  b.hsplit = g_dsc_split;
   b.prof = g_enc_prof;
-  const int qs = g_enc_gemm_offset > 0 ? next_queue_slot() : -1;
-  if (a.P >= 64 && !g_enc_g4_narrow)
-    hipLaunchKernelGGL((gemm4_kernel<EPI, true>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg,
-                       g_enc_gemm_offset, qs);
+  if (a.P >= 64)
+    hipLaunchKernelGGL((gemm4_kernel<EPI, true>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
   else
-    hipLaunchKernelGGL((gemm4_kernel<EPI, false>), dim3((unsigned)grid), dim3(256), G4_LDS, st, b, nwg,
-                       g_enc_gemm_offset, qs);
+    hipLaunchKernelGGL((gemm4_kernel<EPI, false>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
   return trk::check_launch("gemm4_kernel");
 }
-
 
 // out[roi][c] = (float)(sum_j part[roi][j][c] * 2^-24) over the 1..3 partials
 __global__ void __launch_bounds__(256) sums_reduce_kernel(const long long* __restrict__ part, int64_t R, int P,
@@ -2508,8 +1097,6 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  if (g_enc_gemm >= 2 && P >= 86 && K % 64 == 0 && kscale % 64 == 0 && kscale <= 512)
-    return g_enc_gemm == 2 ? launch8<EPI_TRANS, 0>(a, st) : launch8<EPI_TRANS, 1>(a, st);
   if (g_enc_gemm >= 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
   return launch<EPI_TRANS, 128, 256>(a, st);
 }
@@ -2525,91 +1112,17 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_g1_dwconv: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_kernel<2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_persist_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
     attr = true;
   }
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (g_g1dw_persist == 66) {   // interleaved depthwise, one workgroup per CU
-    static bool attr_il = false;
-    if (!attr_il) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_il_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)IL_LDS);
-      attr_il = true;
-    }
-    const int64_t grid = std::min<int64_t>(nwg, (int64_t)cu_count());
-    hipLaunchKernelGGL(g1dw_il_kernel, dim3((unsigned)grid), dim3(512), IL_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, nwg, next_queue_slot());
-    return trk::check_launch("g1dw_il_kernel");
-  }
-  if (g_g1dw_mode == 6) {   // role-split: GEMM waves + depthwise waves, one workgroup per CU
-    static bool attr_sp = false;
-    if (!attr_sp) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_sp_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)IL_LDS);
-      attr_sp = true;
-    }
-    const int64_t grid = std::min<int64_t>(nwg, (int64_t)cu_count());
-    hipLaunchKernelGGL(g1dw_sp_kernel, dim3((unsigned)grid), dim3(1024), IL_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, nwg, next_queue_slot(), g_enc_gemm_dbg);
-    return trk::check_launch("g1dw_sp_kernel");
-  }
-  if (g_g1dw_persist > 0) {
-    const int64_t grid = std::min<int64_t>(nwg, 2 * (int64_t)cu_count());
-    hipLaunchKernelGGL(g1dw_persist_kernel, dim3((unsigned)grid), dim3(512), G1_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg, nwg,
-                       next_queue_slot(), g_g1dw_persist - 1);
-    return trk::check_launch("g1dw_persist_kernel");
-  }
-  if (g_g1dw_mode == 5 && N % 256 == 0) {
-    static bool attr_256 = false;
-    if (!attr_256) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw256_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G2_LDS);
-      attr_256 = true;
-    }
-    const int64_t nwg2 = (M / 200 + (M % 200 ? 1 : 0)) * (N / 256);
-    hipLaunchKernelGGL(g1dw256_kernel, dim3((unsigned)nwg2), dim3(1024), G2_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
-    return trk::check_launch("g1dw256_kernel");
-  }
-  if (g_g1dw_mode == 7) {   // 4-wave workgroups, 112 x 64 wave tiles of 16x16x32
-    static bool attr_q = false;
-    if (!attr_q) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
-      attr_q = true;
-    }
-    hipLaunchKernelGGL(g1dw4_kernel, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
-    return trk::check_launch("g1dw4_kernel");
-  }
-  if (g_g1dw_mode == 4) {
-    TRK_REQUIRE(M * 512 < (int64_t)1 << 31, "enc_g1_dwconv: M * 512 must stay below 2^31");
-    static bool attr_ws = false;
-    if (!attr_ws) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw_ws_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1_LDS);
-      attr_ws = true;
-    }
-    hipLaunchKernelGGL(g1dw_ws_kernel, dim3((unsigned)nwg), dim3(640), G1_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
-    return trk::check_launch("g1dw_ws_kernel");
-  }
-  auto kern = g_g1dw_mode == 1 ? g1dw_kernel<1> : g_g1dw_mode == 2 ? g1dw_kernel<2> : g1dw_kernel<0>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), G1_LDS, st, (const uint16_t*)X,
-                     (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, g_enc_gemm_dbg);
-  return trk::check_launch("g1dw_kernel");
+  hipLaunchKernelGGL(g1dw4_kernel, dim3((unsigned)nwg), dim3(256), G1Q_LDS, reinterpret_cast<hipStream_t>(stream),
+                     (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+  return trk::check_launch("g1dw4_kernel");
 }
 
-// diagnostics: gemm8 per-workgroup timestamps (PROF variant above); buf holds
-// >= 16 * workgroups u64, nullptr switches back to the plain kernel
+// diagnostics: gemm4 per-workgroup phase stamps (8 u64 per workgroup); nullptr
+// switches them off
 extern "C" int trk_enc_set_prof(unsigned long long* buf) {
   g_enc_prof = buf;
   return TRK_OK;

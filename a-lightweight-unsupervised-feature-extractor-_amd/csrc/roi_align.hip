@@ -781,17 +781,11 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   TRK_REQUIRE(key, "set_tuning: null key");
   if (!strcmp(key, "roi_window_kb")) { TRK_REQUIRE(value >= 0 && value <= 150, "roi_window_kb in [0,150]"); g_roi_window_kb = value; return TRK_OK; }
   if (!strcmp(key, "roi_sweep")) { TRK_REQUIRE(value >= 0 && value <= 2, "roi_sweep in {0,1,2}"); g_roi_sweep = value; return TRK_OK; }
-  if (!strcmp(key, "enc_gemm_offset")) { extern int g_enc_gemm_offset; TRK_REQUIRE(value >= 0 && value <= 64, "enc_gemm_offset in [0, 64]"); g_enc_gemm_offset = value; return TRK_OK; }
-  if (!strcmp(key, "dsc_split")) { extern int g_dsc_split; TRK_REQUIRE(value == 0 || value == 1, "dsc_split in {0, 1}"); g_dsc_split = value; return TRK_OK; }
-  if (!strcmp(key, "g1dw_persist")) { extern int g_g1dw_persist; TRK_REQUIRE(value >= 0 && value <= 66, "g1dw_persist in [0, 66]"); g_g1dw_persist = value; return TRK_OK; }
-  if (!strcmp(key, "g1dw_mode")) { extern int g_g1dw_mode; TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 5 || value == 6 || value == 7, "g1dw_mode in {0, 1, 2, 4, 5, 6, 7}"); g_g1dw_mode = value; return TRK_OK; }
-  if (!strcmp(key, "enc_g4_narrow")) { extern int g_enc_g4_narrow; TRK_REQUIRE(value == 0 || value == 1, "enc_g4_narrow in {0, 1}"); g_enc_g4_narrow = value; return TRK_OK; }
   if (!strcmp(key, "se_waves")) { extern int g_se_waves; TRK_REQUIRE(value == 8 || value == 16, "se_waves in {8, 16}"); g_se_waves = value; return TRK_OK; }
   if (!strcmp(key, "head_waves")) { extern int g_head_waves; TRK_REQUIRE(value == 8 || value == 16, "head_waves in {8, 16}"); g_head_waves = value; return TRK_OK; }
   if (!strcmp(key, "roi_wlds")) { TRK_REQUIRE(value == 0 || value == 1, "roi_wlds in {0, 1}"); g_roi_wlds = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
-  if (!strcmp(key, "enc_gemm_dbg")) { extern int g_enc_gemm_dbg; g_enc_gemm_dbg = value; return TRK_OK; }
-  if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value >= 0 && value <= 3, "enc_gemm in {0,1,2,3}"); g_enc_gemm = value; return TRK_OK; }
+  if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value == 0 || value == 1, "enc_gemm in {0, 1}"); g_enc_gemm = value; return TRK_OK; }
   if (!strcmp(key, "dw_fast")) { extern int g_dw_fast; TRK_REQUIRE(value == 0 || value == 1, "dw_fast in {0,1}"); g_dw_fast = value; return TRK_OK; }
   if (!strcmp(key, "lsap_dev_lds_kb")) { extern int g_lsap_dev_lds_kb; TRK_REQUIRE(value >= 8 && value <= 156, "lsap_dev_lds_kb in [8, 156]"); g_lsap_dev_lds_kb = value; return TRK_OK; }
   if (!strcmp(key, "roi_vec")) { TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "roi_vec in {0,1,2,4}"); g_roi_vec = value; return TRK_OK; }

@@ -46,15 +46,6 @@ const char* trk_last_error(void);
  *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel
  *   "enc_gemm"       1 (default): pipelined 128x256 DSC / transition GEMMs; 0: the 128x128 /
  *                    128x256 kernels (same math, another f32 summation order)
- *   "enc_gemm_offset" 0 (default): one workgroup per tile; > 0: persistent tile queue
- *   "dsc_split"      1 (default): DSC GEMM tiles compiled per activation (SiLU / Hardswish);
- *                    0: one tile body with a per-element select (same bits)
- *   "g1dw_mode"      first-GEMM + depthwise kernel: 7 (default) 4-wave workgroups with 16x16x32
- *                    MFMAs; 32x32x16 variants (bit-identical to the two-kernel path): 1 DMA after
- *                    the MFMAs, 0 before, 2 interleaved, 4 dedicated DMA waves, 5 256-channel
- *                    tiles, 6 role-split waves
- *   "g1dw_persist"   0 (default); > 0: persistent tile queue; 66: depthwise interleaved into the
- *                    next tile's K loop
  *   "cost_v2"        0 (default): detection-tile cost kernel; 1: bank-resident kernel
  *   "lsap_dev_lds_kb" LDS budget of trk_lsap_dev workgroups (default 24: they fit beside the
  *                    encoder's workgroups instead of waiting for a whole CU) */
