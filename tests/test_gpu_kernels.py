@@ -772,3 +772,31 @@ def test_lsap_prefix_shortcut_vs_oracle(trk, oracle, gpu):
         n = int(res["count"][k])
         assert np.array_equal(res["rows"][k, :n].cpu().numpy(), er)
         assert np.array_equal(res["cols"][k, :n].cpu().numpy(), ec)
+
+
+def test_roi_align_a1_boundary_branches_gpu(trk, oracle, gpu):
+    """The A.1 boundary branches on the GPU, bit-exact vs the oracle (which
+    tests/test_oracle.py pins to the analytic values): the small-bin cases through the
+    generic kernel, and 10x10 / 7x7 ROIs whose samples land exactly on y, x = -1 and
+    y, x = H (W) through the row-sweep kernel (NHWC out, f32 and bf16) and NCHW out."""
+    import test_oracle as TO
+    x = TO._affine_map()
+    for roi, PH, PW, aligned, what in TO.A1_BOUNDARY_ROIS:
+        r = np.array([roi], np.float32)
+        exp = oracle.roi_align(x, r, (PH, PW), 1.0, 2, aligned)
+        got = trk.roi_align(torch.from_numpy(x).to(gpu), torch.from_numpy(r).to(gpu), (PH, PW), 1.0, 2, aligned)
+        assert np.array_equal(got.cpu().numpy(), exp), what
+    rng = np.random.default_rng(40)
+    feat = rng.standard_normal((1, 512, 40, 40)).astype(np.float32)
+    # bin height 0.5 cell: samples at sh + 0.125 + 0.25 k; sh = -1.125 puts k = 0 at y = -1,
+    # sh = 35.125 puts k = 19 at y = 40 = H (and the same along x)
+    rois = np.array([[0, -0.625, -0.625, 4.375, 4.375], [0, 35.625, 35.625, 40.625, 40.625],
+                     [0, -0.625, 35.625, 4.375, 40.625], [0, 35.625, -0.625, 40.625, 4.375],
+                     [0, 38.9, 38.7, 39.6, 39.95], [0, -1.6, -1.7, 0.2, 0.1]], np.float32)
+    for S in (10, 7):
+        exp = oracle.roi_align(feat, rois, (S, S), 1.0, 2, True)
+        ft, rt = torch.from_numpy(feat).to(gpu), torch.from_numpy(rois).to(gpu)
+        assert np.array_equal(trk.roi_align(ft, rt, (S, S), 1.0, 2, True).cpu().numpy(), exp), S
+        for od in (torch.float32, torch.bfloat16):
+            nhwc = trk.roi_align(ft, rt, (S, S), 1.0, 2, True, out_dtype=od, channels_last=True)
+            assert torch.equal(nhwc.float().cpu(), torch.from_numpy(exp).to(od).float()), (S, od)

@@ -237,3 +237,63 @@ def test_tracker_restatement_vs_reference_golden(oracle, name):
         ud = d["um_dets"][d["um_d_off"][f]:d["um_d_off"][f + 1]]
         exp = ([tuple(map(int, x)) for x in m], [int(x) for x in ut], [int(x) for x in ud])
         assert got == exp, f"{name} frame {f}"
+
+
+# ROI Align boundary branches of SURVEY A.1 (torchvision's CPU kernel): a sample at
+# exactly y == -1 or y == H is valid and clamps, one past them contributes 0; a sample
+# in (H-1, H) has yl >= H-1 and reads row H-1 with ly = 0; aligned=False widens a ROI
+# narrower than one cell to rw = 1.  Same for x.  The map is f = 3x + 2y + 1, which
+# bilinear sampling reproduces exactly at the clamped positions.
+def _affine_map(H=8, W=8, C=2):
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    f = (3 * xx + 2 * yy + 1).astype(np.float32)
+    return np.stack([f, -f])[None, :C].astype(np.float32)
+
+
+def _a1_expected(roi, H, W, PH, PW, sr=2, aligned=True):
+    """A.1 in float64 on f = 3x + 2y + 1 (channel 0)"""
+    off = 0.5 if aligned else 0.0
+    sw, sh, ew, eh = roi[1] - off, roi[2] - off, roi[3] - off, roi[4] - off
+    rw, rh = ew - sw, eh - sh
+    if not aligned:
+        rw, rh = max(rw, 1.0), max(rh, 1.0)
+    bh, bw = rh / PH, rw / PW
+    out = np.zeros((PH, PW))
+    for ph in range(PH):
+        for pw in range(PW):
+            acc = 0.0
+            for iy in range(sr):
+                for ix in range(sr):
+                    y = sh + ph * bh + (iy + 0.5) * bh / sr
+                    x = sw + pw * bw + (ix + 0.5) * bw / sr
+                    if y < -1 or y > H or x < -1 or x > W:
+                        continue
+                    y, x = max(y, 0.0), max(x, 0.0)
+                    y = float(H - 1) if int(y) >= H - 1 else y
+                    x = float(W - 1) if int(x) >= W - 1 else x
+                    acc += 3 * x + 2 * y + 1
+            out[ph, pw] = acc / (sr * sr)
+    return out
+
+
+A1_BOUNDARY_ROIS = [
+    # (roi, PH, PW, aligned, what)
+    ((0, 2.0, -0.75, 5.0, 0.25), 1, 1, True, "y samples at exactly -1 (valid, clamps to 0) and -0.5"),
+    ((0, 2.0, -1.0, 5.0, 0.0), 1, 1, True, "y samples at -1.25 (outside: 0) and -0.75"),
+    ((0, 2.0, 8.25, 5.0, 9.25), 1, 1, True, "y samples at exactly H (valid, row H-1) and H + 0.5 (outside)"),
+    ((0, 2.0, 7.0, 5.0, 8.0), 1, 1, True, "y samples in (H-1, H): yl >= H-1, row H-1, ly = 0"),
+    ((0, -0.75, 2.0, 0.25, 5.0), 1, 1, True, "x samples at exactly -1 and -0.5"),
+    ((0, 8.25, 2.0, 9.25, 5.0), 1, 1, True, "x samples at exactly W and W + 0.5"),
+    ((0, 3.0, 3.0, 3.3, 3.2), 2, 2, False, "aligned=False, rw, rh < 1 -> 1"),
+    ((0, 7.6, 7.7, 7.9, 7.95), 3, 3, False, "aligned=False, sub-cell ROI at the far corner"),
+]
+
+
+@pytest.mark.parametrize("k", range(len(A1_BOUNDARY_ROIS)))
+def test_roi_align_a1_boundary_branches(oracle, k):
+    roi, PH, PW, aligned, what = A1_BOUNDARY_ROIS[k]
+    x = _affine_map()
+    out = oracle.roi_align(x, np.array([roi], np.float32), (PH, PW), 1.0, 2, aligned)
+    exp = _a1_expected(np.float32(roi).astype(np.float64), 8, 8, PH, PW, 2, aligned)
+    assert np.max(np.abs(out[0, 0] - exp)) < 1e-4, what
+    assert np.array_equal(out[0, 1], -out[0, 0]), what
