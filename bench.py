@@ -144,12 +144,12 @@ class Pipeline:
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
                            if os.environ.get("TRK_ROI_STREAM", "0") == "1" else None)
         self.roi_pending = {}
-        # NCHW maps: frame f's NCHW -> NHWC copy (roi_align's first kernel) issued on the
-        # tracker's stream two frames ahead, right after frame f-2's tracker step, so the
-        # HBM-bound copy runs beside the encoder's MFMA-bound kernels instead of in front of
-        # the frame's ROI Align on the embedding stream (TRK_MAP_AHEAD=0: inside roi_align)
+        # NCHW maps, TRK_MAP_AHEAD=1: frame f's NCHW -> NHWC copy (roi_align's first kernel)
+        # issued on the tracker's stream two frames ahead, right after frame f-2's tracker
+        # step, beside the encoder's kernels; off by default: 1.613-1.616 vs 1.622-1.625M
+        # ROIs/s with the copy inside roi_align on the embedding stream (two A/B pairs)
         self.map_ahead = (MAP_LAYOUT == "nchw" and self.track_stream is not None and
-                          os.environ.get("TRK_MAP_AHEAD", "1") == "1")
+                          os.environ.get("TRK_MAP_AHEAD", "0") == "1")
         self.map_pending = {}
 
     def _map_ahead(self, f):
