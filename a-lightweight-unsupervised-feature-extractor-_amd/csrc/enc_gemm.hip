@@ -34,11 +34,9 @@
 //   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
 #include "trk_common.h"
 
-#include <utility>
-
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
 int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
-int g_g1dw = 5;      // trk_set_tuning("g1dw"): 5 = g1dw5 (persistent, Y2 stores deferred; default), 4 = g1dw4
+int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
 
@@ -857,59 +855,8 @@ __device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, cons
     }
 }
 
-// the same quadrant, its 25 bf16 pairs returned in registers (g1dw5 stores them later)
-template <int QY, int QX, int YS>
-__device__ __forceinline__ void dw5q_out(const uint32_t* __restrict__ src, const dw_pair_t (&w)[25],
-                                         uint32_t (&out)[25]) {
-  constexpr int OY0 = 5 * QY, X0 = 5 * QX;
-  constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY0 + 6 > G1_S - 1 ? G1_S - 1 : OY0 + 6;
-  constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
-  constexpr int NX = IX1 - IX0 + 1;
-  dw_pair_t acc[5][5];
-#pragma unroll
-  for (int oy = 0; oy < 5; ++oy)
-#pragma unroll
-    for (int ox = 0; ox < 5; ++ox) acc[oy][ox] = dw_pair_t{0.f, 0.f};
-  uint32_t nxt[NX];
-#pragma unroll
-  for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[(IY0 * G1_S + IX0 + ix) * YS];
-#pragma unroll
-  for (int iy = IY0; iy <= IY1; ++iy) {
-    dw_pair_t in[NX];
-#pragma unroll
-    for (int ix = 0; ix < NX; ++ix) in[ix] = dw_pair_t{__uint_as_float(nxt[ix] << 16), __uint_as_float(nxt[ix] & 0xffff0000u)};
-    if (iy < IY1) {
-#pragma unroll
-      for (int ix = 0; ix < NX; ++ix) nxt[ix] = src[((iy + 1) * G1_S + IX0 + ix) * YS];
-    }
-    // groups of up to 5 independent FMAs (the 5 outputs of a row for one tap), each group
-    // closed by an empty asm on its accumulators: left to itself the compiler ran every
-    // output's taps as one dependent chain (an s_nop between dependent v_pk_fma_f32) at 2
-    // waves per SIMD (a sched_barrier alone does not hold: the FMAs have no chain edge)
-#pragma unroll
-    for (int oy = 0; oy < 5; ++oy) {
-      const int ky = iy - (OY0 + oy) + 2;
-      if (ky < 0 || ky > 4) continue;
-#pragma unroll
-      for (int kx = 0; kx < 5; ++kx) {
-#pragma unroll
-        for (int ox = 0; ox < 5; ++ox) {
-          const int ix = X0 + ox + kx - 2;
-          if (ix >= IX0 && ix <= IX1)
-            acc[oy][ox] = __builtin_elementwise_fma(w[ky * 5 + kx], in[ix - IX0], acc[oy][ox]);
-        }
-        asm volatile("" : "+v"(acc[oy][0]), "+v"(acc[oy][1]), "+v"(acc[oy][2]), "+v"(acc[oy][3]), "+v"(acc[oy][4]));
-      }
-    }
-  }
-#pragma unroll
-  for (int oy = 0; oy < 5; ++oy)
-#pragma unroll
-    for (int ox = 0; ox < 5; ++ox) {
-      out[oy * 5 + ox] = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
-    }
-}
 
+template <bool PF>
 __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
                                                         const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
                                                         int M, int N) {
@@ -1038,6 +985,23 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
         }
   }
   __syncthreads();
+  // PF (g1dw 6, the default): L2 prefetch of the A rows of the tile this slot most likely
+  // runs next (xcd_remap's order: logical tile lb + 64 runs on this XCD after lb), an eighth
+  // of its M tile per N tile, issued now so the depthwise below covers its HBM latency
+  // (28 us of 389 isolated); retired by the kernel's end, nothing waits on it before
+  uint32_t pf = 0;
+  if (PF) {
+    const int64_t tn = lb + 64;
+    const int64_t xs = (int64_t)gridDim.x / 8;   // logical tiles per XCD range (remap: contiguous)
+    if (tn / xs == lb / xs && tn < (int64_t)gridDim.x && tid < 208) {
+      const int part = (int)(tn % ntile_n);
+      const int64_t row = min((tn / ntile_n) * (2 * G1_P) + (part * 26 + (tid >> 3)), (int64_t)M - 1);
+      const uint16_t* pa = X + row * K + (tid & 7) * 64;
+      // (an inline-asm load's destination is written when the load returns: pf stays live,
+      // so its register is not reused, until the wait at the end)
+      asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(pa) : "memory");
+    }
+  }
 
   // depthwise 5x5: wave = output quadrant, for each of the two ROIs; lane = channel pair
   const int ldd = N / 2;
@@ -1056,233 +1020,9 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
       default: dw5q_regs<1, 1, G1Q_YS>(src, wreg, dst, l); break;
     }
   }
+  if (PF) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
 }
 
-// ---------------------------------------------------------------------------
-// g1dw5 (default): g1dw4's tile, persistent, with each tile's Y2 stores deferred
-// into the next tile's K loop.  g1dw4's workgroups all reach their Y2 stores
-// together (one 2-ROI tile per workgroup, every CU in step), so the 420 MB of Y2
-// leave in chip-wide bursts at the HBM write rate while the MFMAs idle -- 74 of its
-// 390 us isolated (tools/exp/g1lab.py: storing to one L2-resident tile instead
-// costs 6 us).  Here a workgroup stores its first ROI's outputs beside the second
-// ROI's depthwise FMAs and keeps the second ROI's 25 bf16 pairs per lane in registers
-// (all 50 would spill), issuing them 4 per K step of the next tile (after that step's
-// DMA; the step's counted vmcnt leaves them one step to drain), so half the writes
-// stream beside the MFMAs.  Grid: two workgroups per CU; the workgroups sharing an
-// XCD (blockIdx % 8) walk that XCD's contiguous tile range (xcd_remap's order) with
-// stride = their count, so the 8 N tiles of an M tile still run together on one
-// XCD.  Same arithmetic as g1dw4: bit-identical Y2.
-template <int N_>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
-}
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a loop whose index is a
-// compile-time constant in the body
-template <typename F, int... Is>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N_, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N_>{});
-}
-
-__global__ void __launch_bounds__(256, 2) g1dw5_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
-                                                        const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
-                                                        int M, int N, int ntiles) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* ring = reinterpret_cast<uint4*>(smem);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntile_n = N / G1_BN;
-  constexpr int K = 512, NK = K / BK;
-  const int fr = lane & 15, fc = lane >> 4;
-  const int lterm = fr * 4 + (fc ^ x16(fr));
-  const int aoff = (wr * 112) * 4 + lterm;           // + i * 64
-  const int boff = G1Q_AP + (wc * 64) * 4 + lterm;   // + t * 64
-  const int ntm = wr == 0 ? 7 : 6;
-  const int ldd = N / 2;                             // Y2 row stride in bf16 pairs
-  const int qorg = (5 * (wave >> 1)) * G1_S + 5 * (wave & 1);   // this wave's depthwise quadrant origin
-  // this workgroup's tiles: its XCD's range (xcd_remap), stride = the XCD's workgroups
-  const int nx = 8, x = blockIdx.x % nx, nslot = gridDim.x / nx, slot = blockIdx.x / nx;
-  const int tq = ntiles / nx, tr = ntiles % nx;
-  const int t_lo = x * tq + min(x, tr), t_hi = t_lo + tq + (x < tr ? 1 : 0);
-
-  uint32_t py[25];              // the previous tile's second-ROI Y2 (bf16 pairs), stored during this
-  uint32_t* pdst1 = nullptr;    // tile's K loop; its destination (quadrant origin + lane)
-  bool pend = false;
-
-  for (int t = t_lo + slot; t < t_hi; t += nslot) {
-    const int n0 = (t % ntile_n) * G1_BN;
-    const int64_t m0 = (int64_t)(t / ntile_n) * (2 * G1_P);
-    // DMA sources: a wave-uniform base (SGPRs) + 32-bit per-lane element offsets
-    const uint16_t* xt = X + m0 * K;
-    const uint16_t* wt = W1 + (int64_t)n0 * K;
-    uint32_t aofs[4], bofs[2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int p = min(q * 256 + tid, G1Q_AP - 1), r = p >> 2, c = (p & 3) ^ x16(r);
-      aofs[q] = (uint32_t)(min(m0 + r, (int64_t)M - 1) - m0) * K + c * 8;
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x16(r);
-      bofs[q] = (uint32_t)r * K + c * 8;
-    }
-    auto issue = [&](int kt) {
-      uint4* d = ring + (kt % 3) * G1Q_BUF + wave * 64;
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        __builtin_amdgcn_global_load_lds(GPTR(xt + aofs[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
-      if (wave == 0) __builtin_amdgcn_global_load_lds(GPTR(xt + aofs[3] + kt * BK), LPTR(d + 3 * 256), 16, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        __builtin_amdgcn_global_load_lds(GPTR(wt + bofs[q] + kt * BK), LPTR(d + G1Q_AP + q * 256), 16, 0, 0);
-    };
-
-    f4v acc[7][4];
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[i][q] = f4v{0.f, 0.f, 0.f, 0.f};
-
-    issue(0);
-    issue(1);
-    if (wave == 0) vm_wait<6>();
-    else vm_wait<5>();
-    g4_barrier();
-    static_for<NK>([&](auto kc) {
-      constexpr int kt = decltype(kc)::value;
-      const uint4* buf = ring + (kt % 3) * G1Q_BUF;
-      {
-        const uint32_t bb = lds_addr(buf + boff), ab = lds_addr(buf + aoff);
-        u32x4 bq[4], aq[7];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q] = lds_read128(bb + q * 1024);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) aq[i] = lds_read128(ab + i * 1024);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (i == 0) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(aq[0]));
-          else if (i == 1) asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(aq[1]));
-          else if (i == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(aq[2]));
-          else if (i == 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(aq[3]));
-          else if (i == 4) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(aq[4]));
-          else if (i == 5) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(aq[5]));
-          else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(aq[6]));
-          if (i < ntm) {
-            const bf8v av = __builtin_bit_cast(bf8v, aq[i]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf8v, bq[q]), acc[i][q], 0, 0, 0);
-          }
-        }
-      }
-      if (kt + 2 < NK) {
-        __builtin_amdgcn_sched_barrier(0);
-        issue(kt + 2);
-      }
-      // the previous tile's Y2: 4 stores per step in steps 0..11, 2 in step 12 (after the DMA,
-      // so the wait below -- DMA ops + these stores -- leaves them this whole step to drain)
-      constexpr int S0 = 4 * kt, S1 = (4 * kt + 4 < 25) ? 4 * kt + 4 : 25, NS = S1 > S0 ? S1 - S0 : 0;
-      if (kt + 1 < NK) {
-        if (pend && NS > 0) {
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int q = S0; q < S1; ++q) pdst1[((q / 5) * G1_S + q % 5) * ldd] = py[q];
-          __builtin_amdgcn_sched_barrier(0);
-          if (kt + 2 < NK) {
-            if (wave == 0) vm_wait<6 + NS>();
-            else vm_wait<5 + NS>();
-          } else {
-            vm_wait<0>();
-          }
-        } else {
-          if (kt + 2 < NK) {
-            if (wave == 0) vm_wait<6>();
-            else vm_wait<5>();
-          } else {
-            vm_wait<0>();
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      g4_barrier();
-    });
-    pend = false;
-
-    uint32_t* y1 = reinterpret_cast<uint32_t*>(smem);
-    {
-      const bool odd = fr & 1;
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-        if (i < ntm)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f4v v = acc[i][q];
-            const float x0 = lane_xor1(odd ? v[0] : v[2]);
-            const float x1 = lane_xor1(odd ? v[1] : v[3]);
-            const int rb = wr * 112 + i * 16 + fc * 4 + (odd ? 2 : 0);
-            const int cp = (wc * 64 + q * 16 + fr) >> 1;
-            if (rb < 2 * G1_P) y1[rb * G1Q_YS + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
-            if (rb + 1 < 2 * G1_P) y1[(rb + 1) * G1Q_YS + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
-          }
-    }
-    // depthwise weights (the lane's channel pair, 25 taps) once the accumulators are in LDS
-    dw_pair_t wreg[25];
-#pragma unroll
-    for (int k = 0; k < 25; ++k) wreg[k] = *reinterpret_cast<const dw_pair_t*>(wdw + (int64_t)k * N + n0 + 2 * lane);
-    __syncthreads();
-    // L2 prefetch of the next tile's A rows: the 8 workgroups of an M tile (on this XCD)
-    // each touch one dword per 128-B line of their eighth of its 208 rows, so its K loop
-    // reads A from L2 instead of waiting on HBM at every step (the loads retire during the
-    // depthwise; nothing waits on them before the end-of-tile barrier)
-    // (an inline-asm load's destination is written when the load returns: pf stays live,
-    // so the compiler does not hand its register to anything else, until the vmcnt(0) below)
-    uint32_t pf = 0;
-    if (t + nslot < t_hi && tid < 208) {
-      const int tn = t + nslot, part = tn % ntile_n;
-      const int64_t row = min((int64_t)(tn / ntile_n) * (2 * G1_P) + (part * 26 + (tid >> 3)), (int64_t)M - 1);
-      const uint16_t* pa = X + row * K + (tid & 7) * 64;
-      asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(pa) : "memory");
-    }
-    // depthwise 5x5 (wave = output quadrant, lane = channel pair): the first ROI's outputs
-    // stored at once (beside the second ROI's FMAs), the second ROI's kept in py
-    const bool has1 = m0 + G1_P < M;
-    {
-      const uint32_t* src = y1 + lane;
-      uint32_t* dst = reinterpret_cast<uint32_t*>(Y2 + m0 * N + n0) + lane;
-      int l = ldd;
-      asm volatile("" : "+s"(l));
-      switch (wave) {
-        case 0: dw5q_regs<0, 0, G1Q_YS>(src, wreg, dst, l); break;
-        case 1: dw5q_regs<0, 1, G1Q_YS>(src, wreg, dst, l); break;
-        case 2: dw5q_regs<1, 0, G1Q_YS>(src, wreg, dst, l); break;
-        default: dw5q_regs<1, 1, G1Q_YS>(src, wreg, dst, l); break;
-      }
-    }
-    {  // (one ROI in the last tile: its outputs again, to its own rows -- the same store count)
-      const uint32_t* src = y1 + (has1 ? G1_P * G1Q_YS : 0) + lane;
-      switch (wave) {
-        case 0: dw5q_out<0, 0, G1Q_YS>(src, wreg, py); break;
-        case 1: dw5q_out<0, 1, G1Q_YS>(src, wreg, py); break;
-        case 2: dw5q_out<1, 0, G1Q_YS>(src, wreg, py); break;
-        default: dw5q_out<1, 1, G1Q_YS>(src, wreg, py); break;
-      }
-      pdst1 = reinterpret_cast<uint32_t*>(Y2 + (m0 + (has1 ? G1_P : 0)) * N + n0) + lane + qorg * ldd;
-    }
-    pend = true;
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
-    __syncthreads();  // every wave's Y1 reads are done before the next tile's DMA reuses the LDS
-  }
-  if (pend) {
-#pragma unroll
-    for (int q = 0; q < 25; ++q) pdst1[((q / 5) * G1_S + q % 5) * ldd] = py[q];
-  }
-}
 
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
@@ -1394,25 +1134,19 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_g1_dwconv: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw5_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
     attr = true;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (g_g1dw == 5) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    const int64_t grid = std::max<int64_t>(8, std::min<int64_t>(2 * (int64_t)cus, (nwg + 7) / 8 * 8) / 8 * 8);
-    hipLaunchKernelGGL(g1dw5_kernel, dim3((unsigned)grid), dim3(256), G1Q_LDS, st, (const uint16_t*)X,
-                       (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N, (int)nwg);
-    return trk::check_launch("g1dw5_kernel");
-  }
-  hipLaunchKernelGGL(g1dw4_kernel, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
-                     (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+  if (g_g1dw == 6)
+    hipLaunchKernelGGL(g1dw4_kernel<true>, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
+                       (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+  else
+    hipLaunchKernelGGL(g1dw4_kernel<false>, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
+                       (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
   return trk::check_launch("g1dw4_kernel");
 }
 

@@ -557,14 +557,14 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         X = A.contiguous()
         wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
         Yu = ops.dwconv5_nhwc(ops.enc_gemm(X, W1).view(R, 10, 10, 1024), wdw).view(M, 1024)
-        Y7 = ops.enc_g1_dwconv(X, W1, wdw)   # g1dw5 (the default): persistent, Y2 stores deferred
+        Y7 = ops.enc_g1_dwconv(X, W1, wdw)   # g1dw 6 (the default): + next-round A prefetch
         Y7b = ops.enc_g1_dwconv(X, W1, wdw)
         assert torch.equal(Y7, Y7b)
-        try:  # g1dw4: one workgroup per tile, same tile arithmetic -> same bits
+        try:  # g1dw 4: without the prefetch, the same arithmetic -> the same bits
             assert L.trk_set_tuning(b"g1dw", 4) == 0
             Y4 = ops.enc_g1_dwconv(X, W1, wdw)
         finally:
-            assert L.trk_set_tuning(b"g1dw", 5) == 0
+            assert L.trk_set_tuning(b"g1dw", 6) == 0
         assert torch.equal(Y4, Y7)
         d = (Y7.float() - Yu.float()).abs()
         assert d.max().item() <= 2e-2 * Yu.float().abs().max().item()
