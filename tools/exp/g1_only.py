@@ -1,4 +1,5 @@
-"""g1dw old vs g1dw4 (enc_gemm knob), a few launches each, for PMC collection."""
+"""g1dw under `g1dw` knob values (argv), three launches each, for PMC collection:
+rocprofv3 --pmc FETCH_SIZE -- python3 tools/exp/g1_only.py 4 6"""
 import importlib, os, sys
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -11,10 +12,9 @@ X = torch.randn(M, 512, device=dev, generator=g).bfloat16()
 W1 = (torch.randn(1024, 512, device=dev, generator=g) / 24).bfloat16()
 wdw = torch.randn(25, 1024, device=dev, generator=g) / 5
 L = ops.lib()
-dbg = int(sys.argv[1]) if len(sys.argv) > 1 else 0
-L.trk_set_tuning(b"enc_gemm_dbg", dbg)
-for impl in (0, 1):
-    L.trk_set_tuning(b"enc_gemm", impl)
+for v in (sys.argv[1:] or ["6"]):
+    assert L.trk_set_tuning(b"g1dw", int(v)) == 0
     for _ in range(3):
         ops.enc_g1_dwconv(X, W1, wdw)
 torch.cuda.synchronize()
+print("ok")

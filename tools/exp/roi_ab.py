@@ -8,7 +8,9 @@ trk = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
 F, K = 8, 256
-feat = torch.randn(F, 512, 40, 40, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+feat = torch.randn(F, 512, 40, 40, device=dev, generator=g)
+if os.environ.get("ROI_LAYOUT", "nhwc") == "nhwc":
+    feat = feat.contiguous(memory_format=torch.channels_last)
 xy = torch.rand(F * K, 2, device=dev, generator=g) * 1100
 wh = 20 + torch.rand(F * K, 2, device=dev, generator=g) * 300
 rois = torch.cat([torch.arange(F, device=dev).repeat_interleave(K)[:, None].float(), xy, xy + wh], 1)
@@ -16,14 +18,20 @@ L = trk.lib()
 variants = sys.argv[1:] or ["roi_wlds=0", "roi_wlds=1"]
 
 
+DEFAULTS = {"roi_wlds": 1, "roi_sweep": 1, "roi_fma": 0}
+
+
 def setv(v, reset=False):
     for kv in v.split(","):
         k, x = kv.split("=")
-        L.trk_set_tuning(k.encode(), 0 if reset and k == "roi_wlds" else (1 if reset else int(x)))
+        L.trk_set_tuning(k.encode(), DEFAULTS[k] if reset else int(x))
 
 
 def run():
     return trk.roi_align(feat, rois, (10, 10), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+
+
+print("layout", os.environ.get("ROI_LAYOUT", "nhwc"))
 
 
 ref = run()
