@@ -24,6 +24,8 @@
 //    one frame (batch index) run on one XCD and its NHWC map stays in that L2.
 #include "trk_common.h"
 
+#include <type_traits>
+
 namespace {
 
 struct AxisTab {  // one sample coordinate along y or x (pre_calc restated)
@@ -461,8 +463,11 @@ __device__ __forceinline__ void bload4(__amdgpu_buffer_rsrc_t rs, int voff, int 
   v[1] = f2_t{__uint_as_float(x[2]), __uint_as_float(x[3])};
 }
 
-// t = w1*f1 + w2*f2 + w3*f3 + w4*f4 (torchvision's order, no contraction)
-template <int NH>
+// t = w1*f1 + w2*f2 + w3*f3 + w4*f4 (torchvision's order, no contraction); FMA: the
+// same order with the three additions fused into their products (v_pk_fma_f32: 4
+// instead of 7 packed ops per channel pair; each fused step rounds once instead of
+// twice, so t moves by at most a few f32 ulp -- the bf16 fast path, see launch_sweep)
+template <int NH, bool FMA>
 __device__ __forceinline__ void sample4(f2_t (&t)[NH][2], float w1, float w2, float w3, float w4,
                                         const f2_t (&f1)[NH][2], const f2_t (&f2)[NH][2],
                                         const f2_t (&f3)[NH][2], const f2_t (&f4)[NH][2]) {
@@ -472,11 +477,72 @@ __device__ __forceinline__ void sample4(f2_t (&t)[NH][2], float w1, float w2, fl
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       f2_t s = W1 * f1[h][p];
-      s = s + W2 * f2[h][p];
-      s = s + W3 * f3[h][p];
-      s = s + W4 * f4[h][p];
+      if constexpr (FMA) {
+        s = __builtin_elementwise_fma(W2, f2[h][p], s);
+        s = __builtin_elementwise_fma(W3, f3[h][p], s);
+        s = __builtin_elementwise_fma(W4, f4[h][p], s);
+      } else {
+        s = s + W2 * f2[h][p];
+        s = s + W3 * f3[h][p];
+        s = s + W4 * f4[h][p];
+      }
       t[h][p] = s;
     }
+}
+
+// sample4 for one lane's 4 channels (NH = 1) as one asm block: the weights stay in the
+// {w1, w2} / {w3, w4} pairs the LDS read returned and are broadcast by op_sel (the
+// compiler copied w4 out of its pair before clobbering it, and kept nothing else in
+// place), the two channel pairs' chains interleaved so every dependent packed op has
+// one instruction between it and its producer (the gfx950 wait state the compiler
+// otherwise pads with s_nop).  Same operations in the same order as sample4.
+template <bool FMA>
+__device__ __forceinline__ void sample4_asm(f2_t (&t)[1][2], f2_t w12, f2_t w34, const f2_t (&f1)[1][2],
+                                            const f2_t (&f2)[1][2], const f2_t (&f3)[1][2],
+                                            const f2_t (&f4)[1][2]) {
+  if constexpr (FMA) {
+    asm("v_pk_mul_f32 %0, %2, %4 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %1, %2, %5 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %6, %0 op_sel:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %2, %7, %1 op_sel:[1,0,0]\n\t"
+        "v_pk_fma_f32 %0, %3, %8, %0 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %1, %3, %9, %1 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %0, %3, %10, %0 op_sel:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %3, %11, %1 op_sel:[1,0,0]\n\t"
+        "s_nop 0"
+        : "=&v"(t[0][0]), "=&v"(t[0][1])
+        : "v"(w12), "v"(w34), "v"(f1[0][0]), "v"(f1[0][1]), "v"(f2[0][0]), "v"(f2[0][1]), "v"(f3[0][0]),
+          "v"(f3[0][1]), "v"(f4[0][0]), "v"(f4[0][1]));
+  } else {
+    f2_t p0, p1;
+    asm("v_pk_mul_f32 %0, %4, %6 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %1, %4, %7 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %2, %4, %8 op_sel:[1,0]\n\t"
+        "v_pk_mul_f32 %3, %4, %9 op_sel:[1,0]\n\t"
+        "v_pk_add_f32 %0, %0, %2\n\t"
+        "v_pk_add_f32 %1, %1, %3\n\t"
+        "v_pk_mul_f32 %2, %5, %10 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %3, %5, %11 op_sel_hi:[0,1]\n\t"
+        "v_pk_add_f32 %0, %0, %2\n\t"
+        "v_pk_add_f32 %1, %1, %3\n\t"
+        "v_pk_mul_f32 %2, %5, %12 op_sel:[1,0]\n\t"
+        "v_pk_mul_f32 %3, %5, %13 op_sel:[1,0]\n\t"
+        "v_pk_add_f32 %0, %0, %2\n\t"
+        "v_pk_add_f32 %1, %1, %3\n\t"
+        "s_nop 0"
+        : "=&v"(t[0][0]), "=&v"(t[0][1]), "=&v"(p0), "=&v"(p1)
+        : "v"(w12), "v"(w34), "v"(f1[0][0]), "v"(f1[0][1]), "v"(f2[0][0]), "v"(f2[0][1]), "v"(f3[0][0]),
+          "v"(f3[0][1]), "v"(f4[0][0]), "v"(f4[0][1]));
+  }
+}
+
+// floor(n / d) for n < 2^31, 0 < d < 2^31, m = udiv_magic_m(d) = floor(2^32 / d) + 1:
+// mulhi(n, m) is q or q + 1 (n * (m - 2^32 / d) < 2^31 * 1 < 2^32), one correction step
+__host__ __device__ inline uint32_t udiv_magic_m(uint32_t d) { return (uint32_t)((1ull << 32) / d + 1); }
+__device__ __forceinline__ uint32_t udiv_magic(uint32_t n, uint32_t d, uint32_t m) {
+  uint32_t q = __umulhi(n, m);
+  if (q * d > n) --q;
+  return q;
 }
 
 // Two-column register cache of one sample row: columns ca (a*) and cb (b*)
@@ -497,11 +563,12 @@ __device__ __forceinline__ void cache_load(f2_t (&v0)[NH][2], f2_t (&v1)[NH][2],
   }
 }
 
-template <int NH, bool OUT_BF16, int PW, bool g_sweep_wlds>
+template <int NH, bool OUT_BF16, int PW, bool g_sweep_wlds, bool FMA, bool g_sweep_asm>
 __global__ void __launch_bounds__(256)
 roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
                  int C, int H, int W, const float* __restrict__ rois, float spatial_scale,
-                 int PH, int aligned, void* __restrict__ out, int nchunks, int64_t nitems) {
+                 int PH, int aligned, void* __restrict__ out, int nchunks, int64_t nitems, uint32_t mch,
+                 uint32_t mph) {
   constexpr int CPW = 256 * NH, NS = 2 * PW;
   static_assert(NS <= 64, "one x sample per lane");
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -510,10 +577,14 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
   __shared__ float4 wtab[4][NS][2];
   const int64_t item = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
   if (item >= nitems) return;  // wave-uniform (no barriers below)
-  const int chunk = (int)(item % nchunks);
-  const int64_t t_ = item / nchunks;
-  const int ph = (int)(t_ % PH);
-  const int n = (int)(t_ / PH);
+  // item = (n * PH + ph) * nchunks + chunk < 2^31: scalar divisions by the host's
+  // magic multipliers (udiv_magic) instead of the VALU division sequences
+  const uint32_t it = (uint32_t)item;
+  const uint32_t t_ = udiv_magic(it, (uint32_t)nchunks, mch);
+  const int chunk = (int)(it - t_ * (uint32_t)nchunks);
+  const uint32_t n_ = udiv_magic(t_, (uint32_t)PH, mph);
+  const int ph = (int)(t_ - n_ * (uint32_t)PH);
+  const int n = (int)n_;
 
   const float* r = rois + (int64_t)n * 5;
   const int b = __builtin_amdgcn_readfirstlane((int)r[0]);
@@ -583,10 +654,17 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
   }
   f2_t zero[NH][2];  // pixel (0,0): what torchvision reads for an empty sample
 #pragma unroll
-  for (int h = 0; h < NH; ++h) bload4(rs, voff[h], 0, zero[h]);
+  for (int h = 0; h < NH; ++h) {
+    if (FMA) zero[h][0] = zero[h][1] = f2_t{0.f, 0.f};  // FMA: an empty sample is +0 (no read)
+    else bload4(rs, voff[h], 0, zero[h]);
+  }
 
   ColCache2<NH> kc[2];
   kc[0].ca = kc[0].cb = kc[1].ca = kc[1].cb = -1;
+  // the wave's weight table as an opaque VGPR address: read with immediate offsets, not
+  // rematerialised from its SGPR before every read
+  uint32_t wtab_va = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)&wtab[wave][0][0]);
+  if (g_sweep_asm) asm volatile("" : "+v"(wtab_va));
   const f2_t Z = {0.f, 0.f}, Q = {0.25f, 0.25f};
   f2_t acc[NH][2], hold[NH][2];
   // the wave's output row (PW bins x C channels) as one buffer: the bin's offset is a
@@ -603,97 +681,126 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
       0x00020000);
   int ovoff[NH];
 #pragma unroll
-  for (int h = 0; h < NH; ++h) ovoff[h] = (cbase + h * 256 + lane * 4) * EB;
-
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    const int pk = __builtin_amdgcn_readlane(xpk, j);
-    const int lo = pk & 0xfff, hi = (pk >> 12) & 0xfff, xv = pk >> 24;
-    f2_t t[2][NH][2];
-#pragma unroll
-    for (int iy = 0; iy < 2; ++iy) {
-      if (yv[iy] && xv) {
-        ColCache2<NH>& k = kc[iy];
-        if (lo != k.ca) {
-          if (lo == k.cb) {
-#pragma unroll
-            for (int h = 0; h < NH; ++h)
-#pragma unroll
-              for (int p = 0; p < 2; ++p) { k.a0[h][p] = k.b0[h][p]; k.a1[h][p] = k.b1[h][p]; }
-          } else {
-            cache_load<NH>(k.a0, k.a1, rs, voff, so[iy][0] + lo * colb, so[iy][1] + lo * colb);
-          }
-          k.ca = lo;
-        }
-        if (hi != k.cb) {
-          if (hi == k.ca) {
-#pragma unroll
-            for (int h = 0; h < NH; ++h)
-#pragma unroll
-              for (int p = 0; p < 2; ++p) { k.b0[h][p] = k.a0[h][p]; k.b1[h][p] = k.a1[h][p]; }
-          } else {
-            cache_load<NH>(k.b0, k.b1, rs, voff, so[iy][0] + hi * colb, so[iy][1] + hi * colb);
-          }
-          k.cb = hi;
-        }
-        float w1, w2, w3, w4;
-        if (g_sweep_wlds) {
-          const float4 w = wtab[wave][j][iy];
-          w1 = w.x; w2 = w.y; w3 = w.z; w4 = w.w;
-        } else {
-          w1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][0]), j));
-          w2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][1]), j));
-          w3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][2]), j));
-          w4 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][3]), j));
-        }
-        sample4<NH>(t[iy], w1, w2, w3, w4, k.a0, k.b0, k.a1, k.b1);
-      } else {
-        sample4<NH>(t[iy], 0.f, 0.f, 0.f, 0.f, zero, zero, zero, zero);
-      }
-    }
-    if ((j & 1) == 0) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          acc[h][p] = Z + t[0][h][p];
-          hold[h][p] = t[1][h][p];
-        }
-    } else {
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        float v[4];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          f2_t s = acc[h][p] + t[0][h][p];
-          s = s + hold[h][p];
-          s = s + t[1][h][p];
-          s = s * Q;  // == s / 4 exactly (power of two)
-          v[2 * p] = s.x;
-          v[2 * p + 1] = s.y;
-        }
-        if (act[h]) {
-          const int so_ = __builtin_amdgcn_readfirstlane((j >> 1) * C * EB);
-          if constexpr (OUT_BF16) {
-            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{trk::pack2_bf16(v[0], v[1]), trk::pack2_bf16(v[2], v[3])},
-                                                  ors, ovoff[h], so_, 0);
-          } else {
-            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4_{__float_as_uint(v[0]), __float_as_uint(v[1]),
-                                                          __float_as_uint(v[2]), __float_as_uint(v[3])},
-                                                   ors, ovoff[h], so_, 0);
-          }
-        }
-      }
-    }
+  for (int h = 0; h < NH; ++h) {
+    ovoff[h] = (cbase + h * 256 + lane * 4) * EB;
+    if (g_sweep_asm) asm volatile("" : "+v"(ovoff[h]));  // kept in a VGPR, not recomputed per store
   }
+
+  auto sweep = [&](auto same_c) {
+    constexpr bool SAME = decltype(same_c)::value;
+  #pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int pk = __builtin_amdgcn_readlane(xpk, j);
+      const int lo = pk & 0xfff, hi = (pk >> 12) & 0xfff, xv = pk >> 24;
+      f2_t t[2][NH][2];
+  #pragma unroll
+      for (int iy = 0; iy < 2; ++iy) {
+        if (yv[iy] && xv) {
+          // SAME: both sample rows read the same two map rows -- one column cache serves
+          // both, updated by the first
+          ColCache2<NH>& k = kc[SAME ? 0 : iy];
+          if (!(SAME && iy == 1) && lo != k.ca) {
+            if (lo == k.cb) {
+  #pragma unroll
+              for (int h = 0; h < NH; ++h)
+  #pragma unroll
+                for (int p = 0; p < 2; ++p) { k.a0[h][p] = k.b0[h][p]; k.a1[h][p] = k.b1[h][p]; }
+            } else {
+              cache_load<NH>(k.a0, k.a1, rs, voff, so[iy][0] + lo * colb, so[iy][1] + lo * colb);
+            }
+            k.ca = lo;
+          }
+          if (!(SAME && iy == 1) && hi != k.cb) {
+            if (hi == k.ca) {
+  #pragma unroll
+              for (int h = 0; h < NH; ++h)
+  #pragma unroll
+                for (int p = 0; p < 2; ++p) { k.b0[h][p] = k.a0[h][p]; k.b1[h][p] = k.a1[h][p]; }
+            } else {
+              cache_load<NH>(k.b0, k.b1, rs, voff, so[iy][0] + hi * colb, so[iy][1] + hi * colb);
+            }
+            k.cb = hi;
+          }
+          float w1, w2, w3, w4;
+          if (g_sweep_wlds && NH == 1 && g_sweep_asm) {
+            typedef float f4_t __attribute__((ext_vector_type(4)));
+            const f4_t w = ((const __attribute__((address_space(3))) f4_t*)(uintptr_t)wtab_va)[j * 2 + iy];
+            sample4_asm<FMA>(reinterpret_cast<f2_t (&)[1][2]>(t[iy]), f2_t{w.x, w.y}, f2_t{w.z, w.w},
+                             reinterpret_cast<const f2_t (&)[1][2]>(k.a0), reinterpret_cast<const f2_t (&)[1][2]>(k.b0),
+                             reinterpret_cast<const f2_t (&)[1][2]>(k.a1), reinterpret_cast<const f2_t (&)[1][2]>(k.b1));
+            continue;
+          }
+          if (g_sweep_wlds) {
+            const float4 w = wtab[wave][j][iy];
+            w1 = w.x; w2 = w.y; w3 = w.z; w4 = w.w;
+          } else {
+            w1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][0]), j));
+            w2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][1]), j));
+            w3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][2]), j));
+            w4 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wq[iy][3]), j));
+          }
+          sample4<NH, FMA>(t[iy], w1, w2, w3, w4, k.a0, k.b0, k.a1, k.b1);
+        } else {
+          if (FMA) {
+  #pragma unroll
+            for (int h = 0; h < NH; ++h) t[iy][h][0] = t[iy][h][1] = zero[h][0];
+          } else {
+            sample4<NH, FMA>(t[iy], 0.f, 0.f, 0.f, 0.f, zero, zero, zero, zero);
+          }
+        }
+      }
+      if ((j & 1) == 0) {
+  #pragma unroll
+        for (int h = 0; h < NH; ++h)
+  #pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            acc[h][p] = FMA ? t[0][h][p] : Z + t[0][h][p];  // (0 + t: torchvision's -0 -> +0)
+            hold[h][p] = t[1][h][p];
+          }
+      } else {
+  #pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          float v[4];
+  #pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            f2_t s = acc[h][p] + t[0][h][p];
+            s = s + hold[h][p];
+            s = s + t[1][h][p];
+            s = s * Q;  // == s / 4 exactly (power of two)
+            v[2 * p] = s.x;
+            v[2 * p + 1] = s.y;
+          }
+          if (act[h]) {
+            const int so_ = __builtin_amdgcn_readfirstlane((j >> 1) * C * EB);
+            if constexpr (OUT_BF16) {
+              typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+              __builtin_amdgcn_raw_buffer_store_b64(u32x2{trk::pack2_bf16(v[0], v[1]), trk::pack2_bf16(v[2], v[3])},
+                                                    ors, ovoff[h], so_, 0);
+            } else {
+              typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4_{__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                            __float_as_uint(v[2]), __float_as_uint(v[3])},
+                                                     ors, ovoff[h], so_, 0);
+            }
+          }
+        }
+      }
+    }
+  };
+  // the bin row's two sample rows usually fall between the same two map rows
+  const bool same = yv[0] && yv[1] && so[0][0] == so[1][0] && so[0][1] == so[1][1];
+  if (g_sweep_asm && same) sweep(std::true_type{});
+  else sweep(std::false_type{});
 }
 
 // tuning knobs (trk_set_tuning): LDS window budget per workgroup, channels per lane
 int g_roi_window_kb = 0;   // measured r01: direct L2 taps beat LDS window staging (229 vs 300+ us)
 int g_roi_vec = 0;  // 0 = auto
 int g_roi_sweep = 1;  // NHWC output: row-sweep kernel, 256 (1) or 512 (2) channels per wave
+int g_roi_asm = 1;    // row sweep: the bilinear sample as one asm block (sample4_asm) and one column
+                      // cache for a bin row whose two sample rows share their map rows (92 vs 100 us)
+int g_roi_fma = 1;    // row sweep, bf16 output: fused multiply-adds in the bilinear sample (see sample4;
+                      // 75 vs 92 us; 0 = the exact torchvision arithmetic, as f32 output always is)
 int g_roi_wlds = 1;   // row sweep: sample weights from an LDS table (1: r02 A/B 97 vs 104 us) or readlanes (0)
 
 template <int VEC, bool OUT_BF16, bool OUT_NHWC>
@@ -743,16 +850,25 @@ int launch_sweep(const float* nhwc, int C, int H, int W, const float* rois, int 
   const int nchunks = (C + 256 * NH - 1) / (256 * NH);
   const int64_t nitems = (int64_t)K * PH * nchunks;
   const int64_t nwg = (nitems + 3) / 4;
-  if (nwg > 0x7fffffff) {
+  const uint32_t mch = udiv_magic_m((uint32_t)nchunks), mph = udiv_magic_m((uint32_t)PH);
+  if (nitems >= ((int64_t)1 << 31)) {
     trk::set_error("roi_align: too many workgroups");
     return TRK_EUNSUPPORTED;
   }
-  if (g_roi_wlds)
-    hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW, true>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, C, H,
-                       W, rois, scale, PH, aligned, out, nchunks, nitems);
-  else
-    hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW, false>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, C, H,
-                       W, rois, scale, PH, aligned, out, nchunks, nitems);
+  // roi_fma (bf16 output only; f32 output is always the exact arithmetic)
+#define TRK_SWEEP(WL, F, A)                                                                                    \
+  hipLaunchKernelGGL((roi_sweep_kernel<NH, OUT_BF16, PW, WL, F, A>), dim3((unsigned)nwg), dim3(256), 0, st, nhwc, \
+                     C, H, W, rois, scale, PH, aligned, out, nchunks, nitems, mch, mph)
+  if (OUT_BF16 && g_roi_fma) {
+    if (g_roi_asm) TRK_SWEEP(true, OUT_BF16, true);
+    else TRK_SWEEP(true, OUT_BF16, false);
+  } else if (g_roi_wlds) {
+    if (g_roi_asm) TRK_SWEEP(true, false, true);
+    else TRK_SWEEP(true, false, false);
+  } else {
+    TRK_SWEEP(false, false, false);
+  }
+#undef TRK_SWEEP
   return trk::check_launch("roi_sweep_kernel");
 }
 
@@ -783,6 +899,8 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "roi_sweep")) { TRK_REQUIRE(value >= 0 && value <= 2, "roi_sweep in {0,1,2}"); g_roi_sweep = value; return TRK_OK; }
   if (!strcmp(key, "se_waves")) { extern int g_se_waves; TRK_REQUIRE(value == 8 || value == 16, "se_waves in {8, 16}"); g_se_waves = value; return TRK_OK; }
   if (!strcmp(key, "head_waves")) { extern int g_head_waves; TRK_REQUIRE(value == 8 || value == 16, "head_waves in {8, 16}"); g_head_waves = value; return TRK_OK; }
+  if (!strcmp(key, "roi_asm")) { TRK_REQUIRE(value == 0 || value == 1, "roi_asm in {0, 1}"); g_roi_asm = value; return TRK_OK; }
+  if (!strcmp(key, "roi_fma")) { TRK_REQUIRE(value == 0 || value == 1, "roi_fma in {0, 1}"); g_roi_fma = value; return TRK_OK; }
   if (!strcmp(key, "roi_wlds")) { TRK_REQUIRE(value == 0 || value == 1, "roi_wlds in {0, 1}"); g_roi_wlds = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
   if (!strcmp(key, "g1dw")) { extern int g_g1dw; TRK_REQUIRE(value == 4 || value == 6, "g1dw in {4, 6}"); g_g1dw = value; return TRK_OK; }

@@ -42,11 +42,23 @@ const char* trk_last_error(void);
  * unless noted; the defaults are the fastest measured in the pipelined bench):
  *   "roi_window_kb"  LDS budget (KiB) for staging a ROI's source window; 0 = never stage
  *   "roi_vec"        channels per lane in roi_align (0 = auto, 1, 2, 4)
- *   "roi_sweep"      1 (default): NHWC output through the row-sweep kernel; 0: per-sample taps
+ *   "roi_sweep"      1 (default): NHWC output through the row-sweep kernel (256 channels per
+ *                    wave); 2: 512 channels per wave; 0: per-sample taps
+ *   "roi_wlds"       1 (default): row sweep reads its sample weights from LDS; 0: readlanes
+ *   "roi_asm"        row sweep: the bilinear sample as one asm block (same operations, same
+ *                    order, bit-identical)
+ *   "roi_fma"        row sweep, bf16 output only: the sample's additions fused into its
+ *                    products (NOT bit-identical: within a few f32 roundings before the
+ *                    bf16 rounding; f32 output is always the exact torchvision arithmetic)
  *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel
- *   "enc_gemm"       1 (default): pipelined 128x256 DSC / transition GEMMs; 0: the 128x128 /
- *                    128x256 kernels (same math, another f32 summation order)
- *   "cost_v2"        0 (default): detection-tile cost kernel; 1: bank-resident kernel
+ *   "enc_gemm"       1 (default): pipelined 128x256 DSC / transition GEMMs (gemm4); 0: the
+ *                    128x128 / 128x256 kernels (same math, another f32 summation order)
+ *   "g1dw"           6 (default): fused first GEMM + depthwise with the next round's rows
+ *                    prefetched into L2; 4: without the prefetch
+ *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup
+ *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
+ *                    given (the device tracker), else the detection-tile kernel; 1: the
+ *                    LDS bank-resident cost2 kernel (all bit-identical)
  *   "lsap_dev_lds_kb" LDS budget of trk_lsap_dev workgroups (default 24: they fit beside the
  *                    encoder's workgroups instead of waiting for a whole CU) */
 int trk_set_tuning(const char* key, int value);

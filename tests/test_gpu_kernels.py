@@ -1,6 +1,8 @@
 """Parity of the gfx950 kernels (through the C ABI) against the CPU oracle and
 the reference's golden vectors.  Tolerances are written in each test:
-  roi_align f32: bit-exact;  bf16 output: == bf16(round-to-nearest of f32)
+  roi_align f32: bit-exact;  bf16 output: == bf16(round-to-nearest of f32) with the exact
+    arithmetic (roi_fma=0); the default fused arithmetic (roi_fma=1) within the tolerance
+    of test_roi_align_sweep_variants
   cost: |d| <= 2e-6 (f32 dot-order / logf ulp differences), gate decisions equal
   lsap: indices bit-exact (scipy semantics)
   encoder fp32: <= 1e-4 (north star);  bf16: cosine >= 0.999 vs fp32
@@ -47,7 +49,12 @@ def test_roi_align_bit_exact_vs_oracle(trk, oracle, gpu, N, S):
     nhwc = trk.roi_align(x, r, (S, S), 40 / 1280.0, 2, True, channels_last=True)
     assert nhwc.is_contiguous(memory_format=torch.channels_last)
     assert np.array_equal(nhwc.cpu().numpy(), exp)
-    bf = trk.roi_align(x, r, (S, S), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+    L = trk.lib()
+    try:  # bf16 output with the exact arithmetic (roi_fma=0) == bf16(f32); roi_fma: test_roi_align_sweep_variants
+        assert L.trk_set_tuning(b"roi_fma", 0) == 0
+        bf = trk.roi_align(x, r, (S, S), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+    finally:
+        L.trk_set_tuning(b"roi_fma", 1)
     assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16())
 
 
@@ -102,6 +109,7 @@ def test_roi_align_nhwc_out_paths(trk, oracle, gpu, sweep):
     r = torch.from_numpy(rois).to(gpu)
     try:
         L.trk_set_tuning(b"roi_sweep", sweep)
+        L.trk_set_tuning(b"roi_fma", 0)  # bf16 == bf16(f32) below: the exact arithmetic
         for (ph, pw), sr, al in (((10, 10), 2, True), ((7, 7), 2, True), ((7, 5), 3, False),
                                  ((4, 6), 1, True), ((5, 3), 4, True)):
             exp = oracle.roi_align(feat, rois, (ph, pw), 1 / 32, sr, al)
@@ -111,6 +119,53 @@ def test_roi_align_nhwc_out_paths(trk, oracle, gpu, sweep):
             assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16()), (ph, pw, sr, al)
     finally:
         L.trk_set_tuning(b"roi_sweep", 1)
+        L.trk_set_tuning(b"roi_fma", 1)
+
+
+@pytest.mark.parametrize("knobs", [dict(roi_asm=0, roi_fma=0), dict(roi_asm=1, roi_fma=0),
+                                   dict(roi_asm=0, roi_fma=1), dict(roi_asm=1, roi_fma=1)])
+def test_roi_align_sweep_variants(trk, oracle, gpu, knobs):
+    """Row-sweep variants (both knobs default to 1).  roi_asm: the bilinear sample as
+    one asm block and one column cache for sample rows that share their map rows --
+    the same operations in the same order, bit-exact in f32 and bf16.  roi_fma (bf16
+    output only): the three additions of each sample fused into their products, so a
+    sample moves by at most ~3 f32 roundings of its largest product; tolerance
+    written here: |got - f32 oracle| <= 2^-8 |oracle| (bf16 rounding) + 2^-19 max|map|,
+    and >= 99.9 % of the outputs identical to bf16(oracle).  f32 output stays exact."""
+    L = trk.lib()
+    rng = np.random.default_rng(12)
+    B, N = 4, 200
+    feat = _feat(rng, B)
+    boxes = _boxes(rng, B * N)
+    rois = np.concatenate([np.repeat(np.arange(B), N).astype(np.float32)[:, None], boxes], 1)
+    rois[0, 1:] = [2000, 2000, 2100, 2100]
+    rois[1, 1:] = [-300, -300, 100, 100]
+    rois[2, 1:] = [1200, 1200, 1400, 1500]
+    rois[3, 1:] = [500, 500, 500, 500]
+    rois[4, 1:] = [-50, -50, 1330, 1330]
+    x = torch.from_numpy(feat).to(gpu)
+    r = torch.from_numpy(rois).to(gpu)
+    fma = bool(knobs.get("roi_fma"))
+    try:
+        for k, v in knobs.items():
+            assert L.trk_set_tuning(k.encode(), v) == 0
+        for (ph, pw) in ((10, 10), (7, 7)):
+            exp = oracle.roi_align(feat, rois, (ph, pw), 1 / 32, 2, True)
+            f32 = trk.roi_align(x, r, (ph, pw), 1 / 32, 2, True, channels_last=True)
+            assert np.array_equal(f32.cpu().numpy(), exp), (ph, knobs)
+            bf = trk.roi_align(x, r, (ph, pw), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True).cpu()
+            want = torch.from_numpy(exp).bfloat16()
+            if not fma:
+                assert torch.equal(bf, want), (ph, knobs)
+                continue
+            got = bf.float().numpy()
+            tol = np.abs(exp) * 2.0 ** -8 + 2.0 ** -19 * float(np.abs(feat).max())
+            assert np.all(np.abs(got - exp) <= tol), (ph, float(np.max(np.abs(got - exp) - tol)))
+            same = float((bf.view(torch.int16) == want.view(torch.int16)).float().mean())
+            assert same >= 0.999, (ph, same)
+    finally:
+        for k in knobs:
+            L.trk_set_tuning(k.encode(), 1)  # the defaults
 
 
 def test_roi_align_odd_channels_and_empty(trk, oracle, gpu):
@@ -799,10 +854,15 @@ def test_roi_align_a1_boundary_branches_gpu(trk, oracle, gpu):
     rois = np.array([[0, -0.625, -0.625, 4.375, 4.375], [0, 35.625, 35.625, 40.625, 40.625],
                      [0, -0.625, 35.625, 4.375, 40.625], [0, 35.625, -0.625, 40.625, 4.375],
                      [0, 38.9, 38.7, 39.6, 39.95], [0, -1.6, -1.7, 0.2, 0.1]], np.float32)
+    L = trk.lib()
     for S in (10, 7):
         exp = oracle.roi_align(feat, rois, (S, S), 1.0, 2, True)
         ft, rt = torch.from_numpy(feat).to(gpu), torch.from_numpy(rois).to(gpu)
         assert np.array_equal(trk.roi_align(ft, rt, (S, S), 1.0, 2, True).cpu().numpy(), exp), S
         for od in (torch.float32, torch.bfloat16):
-            nhwc = trk.roi_align(ft, rt, (S, S), 1.0, 2, True, out_dtype=od, channels_last=True)
+            try:  # bf16 with the exact arithmetic (the fused default: test_roi_align_sweep_variants)
+                assert L.trk_set_tuning(b"roi_fma", 0) == 0
+                nhwc = trk.roi_align(ft, rt, (S, S), 1.0, 2, True, out_dtype=od, channels_last=True)
+            finally:
+                L.trk_set_tuning(b"roi_fma", 1)
             assert torch.equal(nhwc.float().cpu(), torch.from_numpy(exp).to(od).float()), (S, od)
