@@ -139,10 +139,12 @@ class Pipeline:
         # on the tracker's stream right before the frame's tracker step, so the next frame's
         # ROI Align and first GEMM (embedding stream) fill the GPU beside it; no extra stream
         self.defer_head = os.environ.get("TRK_HEAD_STREAM", "1") == "1" and self.track_stream is not None
-        # ROI Align of frame f+1 issued on its own stream when frame f's encoder is enqueued
-        # (TRK_ROI_STREAM=1: +0.7..2 % in r02 A/B runs, within run-to-run spread: off by default)
+        # ROI Align of frame f+1 issued on its own stream when frame f's encoder is enqueued,
+        # so the encoder stream runs GEMMs only (TRK_ROI_STREAM, default 1 since r03: with
+        # NCHW maps and the 75-us sweep, 1.674-1.694 vs 1.641-1.682M ROIs/s in three
+        # interleaved pairs; +0.7..2 % with r02's kernels)
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
-                           if os.environ.get("TRK_ROI_STREAM", "0") == "1" else None)
+                           if os.environ.get("TRK_ROI_STREAM", "1") == "1" else None)
         self.roi_pending = {}
         # NCHW maps, TRK_MAP_AHEAD=1: frame f's NCHW -> NHWC copy (roi_align's first kernel)
         # issued on the tracker's stream two frames ahead, right after frame f-2's tracker

@@ -3,6 +3,7 @@
 //   F & 1   every workgroup reads M tile 0's A rows (L2-resident)
 //   F & 2   stop after the K loop          F & 8   no MFMAs     F & 16  no operand DMA
 //   F & 32  prefetch the tile's A rows into L2 (one dword per line) before the K loop
+//   F & 64  no activation (bias only)   F & 128 no ROI sums   F & 256 no output stores
 #include "../../a-lightweight-unsupervised-feature-extractor-_amd/csrc/enc_gemm.hip"
 namespace {
 template <int EPI, bool WIDE, int HSWM, int F>
@@ -195,7 +196,7 @@ __device__ __forceinline__ void g4lab_tile(const EncGemmArgs& a, int64_t lb, uns
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + b2;
-        v = hsw ? hswish2(v) : silu2(v);
+        if (!(F & 64)) v = hsw ? hswish2(v) : silu2(v);
         acc[i][t][2 * h] = v.x;
         acc[i][t][2 * h + 1] = v.y;
       }
@@ -208,7 +209,7 @@ __device__ __forceinline__ void g4lab_tile(const EncGemmArgs& a, int64_t lb, uns
   // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
   // consumer adds llrintf(p0 * 2^24) + llrintf(p1 * 2^24) (the former int64 atomics' sum)
   float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [2][SLOTS][256]
-  {
+  if (!(F & 128)) {
     const int64_t r0w = m0 + wr * 64;
     const int64_t roiw = r0w / a.P;
     const int wslot0 = (int)(roiw - roi_base);
@@ -286,7 +287,7 @@ __device__ __forceinline__ void g4lab_tile(const EncGemmArgs& a, int64_t lb, uns
   }
   __syncthreads();
   if (prof) pst[4] = eg_stamp();
-  {
+  if (!(F & 128)) {
     const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
     const int nslot = (int)(last_row / a.P - roi_base) + 1;
     for (int q = tid; q < nslot * 256; q += 256) {
@@ -298,7 +299,7 @@ __device__ __forceinline__ void g4lab_tile(const EncGemmArgs& a, int64_t lb, uns
     }
   }
   if (prof) pst[5] = eg_stamp();
-  if (EPI == EPI_DSC) {
+  if (EPI == EPI_DSC && !(F & 256)) {
     const uint32_t* stage = reinterpret_cast<const uint32_t*>(smem);
     const int64_t cbase = (int64_t)g * a.N + n0;
 #pragma unroll 4
@@ -349,6 +350,9 @@ static int lab4(const EncGemmArgs& a, void* stream) {
     case 2: return lab4<E, 2>(a, stream); case 3: return lab4<E, 3>(a, stream); \
     case 10: return lab4<E, 10>(a, stream); case 18: return lab4<E, 18>(a, stream); \
     case 32: return lab4<E, 32>(a, stream); case 34: return lab4<E, 34>(a, stream); \
+    case 64: return lab4<E, 64>(a, stream); case 128: return lab4<E, 128>(a, stream); \
+    case 256: return lab4<E, 256>(a, stream); case 192: return lab4<E, 192>(a, stream); \
+    case 448: return lab4<E, 448>(a, stream); \
     default: return -1; }
 
 extern "C" int lab_dsc(int flags, const void* Y2, int64_t M, int64_t P, const void* W2, const float* bias, void* XRN,

@@ -28,7 +28,9 @@ st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 kern = sys.argv[1]
 flags = [int(f) for f in sys.argv[2:]]
 names = {0: "full", 1: "A L2-resident", 2: "K loop only", 3: "K loop only, A L2", 10: "K loop DMA only",
-         18: "K loop MFMA only", 32: "full + A prefetch", 34: "K loop only + A prefetch"}
+         18: "K loop MFMA only", 32: "full + A prefetch", 34: "K loop only + A prefetch",
+         64: "no activation", 128: "no ROI sums", 256: "no output stores", 192: "no act, no sums",
+         448: "no act, no sums, no stores"}
 
 
 def run(f):
