@@ -36,6 +36,8 @@
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
 int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
+int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column sums on the MFMA (DSC
+                     // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
@@ -464,7 +466,7 @@ static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
 
 // WIDE (P >= 64): a wave's 64 rows span at most 2 ROIs and a tile's 128 at most 3, so
 // the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions)
-template <int EPI, bool WIDE, int HSWM>
+template <int EPI, bool WIDE, int HSWM, int SMF>
 __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, unsigned char* smem) {
   uint4* ring = reinterpret_cast<uint4*>(smem);
   // opaque per tile: keeps the compiler from hoisting lane-dependent addresses
@@ -642,7 +644,52 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
   // consumer adds llrintf(p0 * 2^24) + llrintf(p1 * 2^24) (the former int64 atomics' sum)
   float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [2][SLOTS][256]
-  {
+  if constexpr (SMF != 0) {
+    // the same partials on the MFMA: S[slot][col] = sum_rows mask[slot][row] * act[row][col]
+    // as 16x16x32 bf16 MFMAs whose B operand is the accumulator fragments themselves --
+    // lane (fr, fc) holds rows 4 fc + e of row tiles 2p and 2p + 1 for column fr, which
+    // is exactly a B fragment (k = 8 fc + j) once the k -> row order below is used for
+    // the mask too (A: lane (m = fr, fc), k = 8 fc + j -> row tile 2p + j / 4, row
+    // 4 fc + j % 4).  The activations enter as a bf16 pair hi + lo (hi = bf16(x), lo =
+    // bf16(x - hi): 16 significant bits, products with 1.0 exact, f32 accumulation).
+    // Row rl of the tile belongs to slot (off + rl) / P, off = m0 - roi_base * P; P >= 43
+    // so a 128-row tile holds at most 4 slots.  Lanes 0..15 end up with slots 0..3 (e).
+    const int P = a.P;
+    const int off = (int)(m0 - roi_base * P);
+    bf8v mask[2];
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rl = wr * 64 + (2 * p2 + (j >> 2)) * 16 + 4 * fc + (j & 3);
+        const int x = off + rl;
+        const int slot = (x >= P) + (x >= 2 * P) + (x >= 3 * P);
+        const bool on = slot == fr && m0 + rl < (int64_t)a.M;
+        mask[p2][j] = on ? (__bf16)1.0f : (__bf16)0.0f;
+      }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      f4v sacc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p2 = 0; p2 < 2; ++p2) {
+        const f4v u = acc[2 * p2][t], v = acc[2 * p2 + 1][t];
+        bf8v hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hi[e] = (__bf16)u[e];
+          hi[4 + e] = (__bf16)v[e];
+          lo[e] = (__bf16)(u[e] - (float)hi[e]);
+          lo[4 + e] = (__bf16)(v[e] - (float)hi[4 + e]);
+        }
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mask[p2], hi, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mask[p2], lo, sacc, 0, 0, 0);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int ts = 0; ts < G4_SLOTS; ++ts) part[(wr * G4_SLOTS + ts) * 256 + colq + t * 16] = sacc[ts];
+      }
+    }
+  } else {
     const int64_t r0w = m0 + wr * 64;
     const int64_t roiw = r0w / a.P;
     const int wslot0 = (int)(roiw - roi_base);
@@ -759,12 +806,12 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 // one workgroup per tile (XCD-remapped); a DSC tile's group (SiLU / Hardswish) is a
 // template argument of its body, so each body is straight-line (a per-element select
 // was compiled into 64 branches of nop-padded exp / rcp chains)
-template <int EPI, bool WIDE>
+template <int EPI, bool WIDE, int SMF>
 __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t lb = xcd_remap(blockIdx.x, ntiles);
-  if (EPI == EPI_DSC && (lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1>(a, lb, smem);
-  else gemm4_tile<EPI, WIDE, 0>(a, lb, smem);
+  if (EPI == EPI_DSC && (lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1, SMF>(a, lb, smem);
+  else gemm4_tile<EPI, WIDE, 0, SMF>(a, lb, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -1030,18 +1077,23 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm4: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, false, 0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, true, 0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
+
     attr = true;
   }
   EncGemmArgs b = a;
   b.prof = g_enc_prof;
-  if (a.P >= 64)
-    hipLaunchKernelGGL((gemm4_kernel<EPI, true>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
+  if (g_enc_sums == 1)  // ROI sums on the MFMA (any P >= 43)
+    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 1>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
+  else if (a.P >= 64)
+    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 0>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
   else
-    hipLaunchKernelGGL((gemm4_kernel<EPI, false>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
+    hipLaunchKernelGGL((gemm4_kernel<EPI, false, 0>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
   return trk::check_launch("gemm4_kernel");
 }
 

@@ -53,6 +53,9 @@ const char* trk_last_error(void);
  *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel
  *   "enc_gemm"       1 (default): pipelined 128x256 DSC / transition GEMMs (gemm4); 0: the
  *                    128x128 / 128x256 kernels (same math, another f32 summation order)
+ *   "enc_sums"       1 (default): gemm4's per-ROI column sums (SE squeeze, GAP) as MFMAs of a
+ *                    slot mask with the activations split bf16 hi + lo (sums within ~1e-6
+ *                    relative of the lane-reduction sums, 0)
  *   "g1dw"           6 (default): fused first GEMM + depthwise with the next round's rows
  *                    prefetched into L2; 4: without the prefetch
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup

@@ -48,7 +48,7 @@ for v in variants:
     o = out if isinstance(out, torch.Tensor) else torch.cat([t.flatten().float() for t in out])
     if ref is None:
         ref = o.clone()
-    d = (o.double() - ref.double()).abs()
+    d = (o.double() - ref.double()).abs().flatten()
     print(json.dumps({"variant": v, "identical_to_first": bool(torch.equal(o, ref)),
                       "max_abs_diff": d.max().item(), "n_diff": int((d > 0).sum().item()),
                       "first_diff": int((d > 0).nonzero()[0].item()) if bool((d > 0).any()) else -1,
