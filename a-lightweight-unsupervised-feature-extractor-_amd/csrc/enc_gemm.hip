@@ -36,6 +36,7 @@
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
 int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
+int g_enc_lds_tight = 1;  // trk_set_tuning("enc_lds_tight"): gemm4 launched with the LDS its tile uses (1) or 80 KiB
 int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column sums on the MFMA (DSC
                      // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
@@ -516,9 +517,12 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   if constexpr (EPI == EPI_TRANS) {
     const int per = a.kscale / 4;
     const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
+    // only the slots a tile can span (ceil(127 / P) + 1): the launch sizes LDS for them
+    const int tslots = min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
 #pragma unroll
     for (int q = 0; q < G4_SQ; ++q) {
       const int p = q * 256 + tid;
+      if (p >= tslots * per) continue;
       const int slot = min(p / per, G4_SLOTS - 1);
       const int64_t roi = min(roi_base + slot, nroi - 1);
       const float* src = a.scale + roi * a.kscale + (p % per) * 4;
@@ -1088,12 +1092,20 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   }
   EncGemmArgs b = a;
   b.prof = g_enc_prof;
+  // dynamic LDS: what the tile uses, not the 80 KiB maximum, so the tracker's and ROI
+  // Align's workgroups fit beside two gemm4 workgroups on a CU instead of waiting for one
+  // to retire (DSC: ring or staging + partials, 74 KiB; transition: ring + the SE scales
+  // of the slots a 128-row tile can span, 78 KiB at P = 100)
+  const int tslots = std::min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
+  const size_t lds = !g_enc_lds_tight ? G4_LDS
+                    : EPI == EPI_DSC  ? std::max(G4_RING, G4_STAGE + G4_RED)
+                                      : std::max(G4_RING + (size_t)tslots * a.kscale * 4, (size_t)G4_RED);
   if (g_enc_sums == 1)  // ROI sums on the MFMA (any P >= 43)
-    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 1>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
+    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 1>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
   else if (a.P >= 64)
-    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 0>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
+    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 0>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
   else
-    hipLaunchKernelGGL((gemm4_kernel<EPI, false, 0>), dim3((unsigned)nwg), dim3(256), G4_LDS, st, b, nwg);
+    hipLaunchKernelGGL((gemm4_kernel<EPI, false, 0>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
   return trk::check_launch("gemm4_kernel");
 }
 

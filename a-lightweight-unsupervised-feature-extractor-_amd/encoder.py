@@ -215,6 +215,8 @@ class Model(nn.Module):
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
+    stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
+                         # enqueued (a caller can record an event there to place other streams' work)
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
@@ -232,6 +234,8 @@ class Model(nn.Module):
                  h2 % 32 == 0 and Co % 256 == 0)
         if fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_dwconv:
             Y2 = enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])               # first 1x1 convs + depthwise 5x5, one kernel
+            if self.stage_hook is not None:
+                self.stage_hook("g1")
         else:
             if fused:
                 Y1 = enc_gemm(X, W["w1_nk"]).view(N, S1, S2, h4)     # 4 first 1x1 convs, one GEMM
@@ -242,6 +246,8 @@ class Model(nn.Module):
             # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
             # + SiLU + GAP in another: the [M, 512] intermediates are written once (x_r|x_n)
             XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
+            if self.stage_hook is not None:
+                self.stage_hook("dsc")
             if self.fused_tail:
                 # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
                 m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])

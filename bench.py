@@ -146,6 +146,17 @@ class Pipeline:
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
                            if os.environ.get("TRK_ROI_STREAM", "1") == "1" else None)
         self.roi_pending = {}
+        # TRK_ROI_AFTER=g1|dsc: frame f+1's ROI Align waits for frame f's first GEMM / DSC GEMM
+        # (an event recorded through encoder.Model.stage_hook), so it runs beside the
+        # encoder's later kernels instead of as soon as it is enqueued
+        self.roi_after = os.environ.get("TRK_ROI_AFTER", "") if self.roi_stream is not None else ""
+        self.roi_gate = None
+        if self.roi_after:
+            def hook(name):
+                if name == self.roi_after:
+                    self.roi_gate = torch.cuda.Event()
+                    self.roi_gate.record(torch.cuda.current_stream())
+            self.model.stage_hook = hook
         # NCHW maps, TRK_MAP_AHEAD=1: frame f's NCHW -> NHWC copy (roi_align's first kernel)
         # issued on the tracker's stream two frames ahead, right after frame f-2's tracker
         # step, beside the encoder's kernels; off by default: 1.613-1.616 vs 1.622-1.625M
@@ -246,6 +257,9 @@ class Pipeline:
         if self.roi_stream is None or f in self.roi_pending or f >= len(self.sc["rois"]):
             return
         with torch.cuda.stream(self.roi_stream):
+            if self.roi_gate is not None:
+                self.roi_stream.wait_event(self.roi_gate)
+                self.roi_gate = None
             roi = self.stage_roi(f)
             ev = torch.cuda.Event()
             ev.record(self.roi_stream)
@@ -718,7 +732,8 @@ def main():
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
     rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
-                     "roi_stream": pipe.roi_stream is not None, "track_prio": pipe.track_stream is not None,
+                     "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
+                     "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,
                      "tuning": os.environ.get("TRK_TUNE") or None}
     step_us = el / args.steps * 1e6
