@@ -643,12 +643,22 @@ def _partials(total, P, parts=3):
     return out
 
 
+@pytest.mark.parametrize("hw", [16, 8])
 @pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_se_head_vs_torch_fp32(trk, gpu, R):
+def test_enc_se_head_vs_torch_fp32(trk, gpu, R, hw):
     """trk_enc_se / trk_enc_head vs the same math in torch fp32 (the encoder's own
     _se / _head on the reference weights).  Means: bit-identical (same ops);
     s: 2e-6; embeddings (unit rows): 2e-5 -- the f32 MFMA sums in another order.
-    R = 1 / 37: partial 16-ROI workgroups."""
+    R = 1 / 37: partial 16-ROI workgroups; 16- and 8-wave head workgroups."""
+    L = trk.lib()
+    assert L.trk_set_tuning(b"head_waves", hw) == 0
+    try:
+        _se_head_case(trk, gpu, R)
+    finally:
+        L.trk_set_tuning(b"head_waves", 16)
+
+
+def _se_head_case(trk, gpu, R):
     from importlib import import_module
     ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
     m = trk.Model(512, 512, 10, 128).eval()
