@@ -1075,6 +1075,344 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
 }
 
 
+// ---------------------------------------------------------------------------
+// rmb_front: one DSC of the RMB end to end for one 10x10 ROI per workgroup
+// (card.py:28-57: the branch's first 1x1 convs, the depthwise 5x5, depth.2 +
+// point.2 with eval-BN folded, the activation, and the ROI's column sums).  Y1 and
+// Y2 live only in LDS, so the [M, 1024] Y2 that g1dw4 wrote (419 MB per 2048
+// ROIs) and gemm4<DSC> read back (530 MB) never reaches HBM; HBM sees X once and
+// XRN once.  Workgroup (roi, g): g = 0 reinforce (SiLU), 1 normal (Hardswish).
+//
+// 8 waves, one workgroup per CU (126 KiB of LDS).  Wave w owns output columns
+// 64 w .. 64 w + 63 of the group's 512 in BOTH GEMMs and all 112 rows (7 row
+// tiles of 16; rows 100..111 are padding whose results are dropped): a 112 x 64
+// wave tile of 16x16x32 MFMAs, 112 accumulator registers.  No B element is used
+// by two waves, so B does not go through LDS: the weights are pre-packed on the
+// host in MFMA fragment order ([g][k step][16-col tile][lane] x 16 B), and a
+// wave's four fragments of a K step are one contiguous 4 KiB read straight into
+// VGPRs, two steps ahead.  A (the ROI's X rows, shared by the 8 waves) is staged by
+// LDS-DMA into a 3-buffer ring (g1dw4's image: row r chunk c at 16-B slot
+// r*4 + (c ^ x16(r))).  Y is kept as 16 K blocks of 32 channels in that same
+// image (100 rows x 64 B per block, block stride 6464 B so the depthwise's
+// 4-B channel-pair reads of two blocks fall on different banks), so GEMM2 reads
+// its A fragments from Y exactly as GEMM1 reads the ring.  Same MFMA shape, K order
+// and roundings (Y1 and Y2 to bf16) as g1dw4 + gemm4<DSC>: XRN is bit-identical
+// to the two-kernel path; the column sums add the same f32 activations in another
+// order (exact f32 lane sums, one partial per ROI).
+constexpr int RF_S = 100;                                      // rows per ROI
+constexpr int RF_STAGE = 512;                                  // A stage: 128 rows x 4 16-B chunks
+constexpr size_t RF_RING = (size_t)3 * RF_STAGE * 16;          // 24 KiB
+constexpr int RF_KBS = 1616;                                   // Y block stride (dwords): 6400 B + 64
+constexpr size_t RF_Y = (size_t)15 * RF_KBS * 4 + 112 * 64;    // row tile 6 of block 15 reads rows ..111
+constexpr int RF_OS = 260;                                     // output staging row stride (dwords)
+constexpr size_t RF_LDS = RF_RING + RF_Y;
+static_assert((size_t)RF_S * RF_OS * 4 <= RF_Y, "output staging reuses the Y image");
+static_assert(RF_LDS <= 160 * 1024, "one rmb_front workgroup per CU");
+
+struct RfArgs {
+  const uint16_t* X;    // [R * 100][512] bf16 NHWC ROI rows
+  const uint4* W1p;     // [2][16][32][64] 16-B fragments of W1 (group g: rows 512 g ..)
+  const float* wdw;     // [25][1024] depthwise taps
+  const uint4* W2p;     // [2][16][32][64] fragments of the BN-folded DSC weights
+  const float* bias;    // [1024] BN-folded bias
+  uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
+  long long* sums;      // [R][kPart][1024] int64 x 2^24: partial 0 = the ROI's sum, the rest 0
+};
+
+// Y dword of (pixel s, channel pair at column col of the group): block col / 32,
+// chunk (col % 32) / 8 swizzled by x16(s), dword (col % 8) / 2
+__device__ __forceinline__ int rf_yaddr(int s, int col) {
+  const int kb = col >> 5, c = (col & 31) >> 3, d = (col & 7) >> 1;
+  return kb * RF_KBS + s * 16 + ((c ^ x16(s)) << 2) + d;
+}
+
+// depthwise 5x5 of output quadrant (QY, QX) for the lane's channel pair, results
+// held as packed bf16 pairs (the caller writes them back in place after a barrier);
+// same per-output FMA order as dw5q_regs.  Pixel s sits at dword b1 + 16 s when
+// x16(s) != 0, else b0 + 16 s (s is a constant after unrolling).
+template <int QY, int QX>
+__device__ __forceinline__ void rf_dw5q(const uint32_t* y, int b0, int b1, const dw_pair_t (&w)[25],
+                                        uint32_t (&out)[25]) {
+  constexpr int OY0 = 5 * QY, X0 = 5 * QX;
+  constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY0 + 6 > G1_S - 1 ? G1_S - 1 : OY0 + 6;
+  constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
+  constexpr int NX = IX1 - IX0 + 1;
+  auto at = [&](int s) { return y[(((s >> 3) & 1) ? b1 : b0) + s * 16]; };
+  dw_pair_t acc[5][5];
+#pragma unroll
+  for (int oy = 0; oy < 5; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) acc[oy][ox] = dw_pair_t{0.f, 0.f};
+  uint32_t nxt[NX];
+#pragma unroll
+  for (int ix = 0; ix < NX; ++ix) nxt[ix] = at(IY0 * G1_S + IX0 + ix);
+#pragma unroll
+  for (int iy = IY0; iy <= IY1; ++iy) {
+    dw_pair_t in[NX];
+#pragma unroll
+    for (int ix = 0; ix < NX; ++ix) in[ix] = dw_pair_t{__uint_as_float(nxt[ix] << 16), __uint_as_float(nxt[ix] & 0xffff0000u)};
+    if (iy < IY1) {
+#pragma unroll
+      for (int ix = 0; ix < NX; ++ix) nxt[ix] = at((iy + 1) * G1_S + IX0 + ix);
+    }
+#pragma unroll
+    for (int oy = 0; oy < 5; ++oy) {
+      const int ky = iy - (OY0 + oy) + 2;
+      if (ky < 0 || ky > 4) continue;
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx) {
+#pragma unroll
+        for (int ox = 0; ox < 5; ++ox) {
+          const int ix = X0 + ox + kx - 2;
+          if (ix >= IX0 && ix <= IX1)
+            acc[oy][ox] = __builtin_elementwise_fma(w[ky * 5 + kx], in[ix - IX0], acc[oy][ox]);
+        }
+        asm volatile("" : "+v"(acc[oy][0]), "+v"(acc[oy][1]), "+v"(acc[oy][2]), "+v"(acc[oy][3]), "+v"(acc[oy][4]));
+      }
+    }
+  }
+#pragma unroll
+  for (int oy = 0; oy < 5; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) out[oy * 5 + ox] = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
+}
+template <int QY, int QX>
+__device__ __forceinline__ void rf_dw5q_store(uint32_t* y, int b0, int b1, const uint32_t (&out)[25]) {
+#pragma unroll
+  for (int oy = 0; oy < 5; ++oy)
+#pragma unroll
+    for (int ox = 0; ox < 5; ++ox) {
+      const int s = (5 * QY + oy) * G1_S + 5 * QX + ox;
+      y[(((s >> 3) & 1) ? b1 : b0) + s * 16] = out[oy * 5 + ox];
+    }
+}
+
+__device__ __forceinline__ void rf_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g4_barrier();
+}
+
+// the wave's four B fragments of k step kt (4 KiB contiguous): asm loads, so the issue order
+// is the program order and the caller's counted vmcnt waits are exact
+__device__ __forceinline__ void rf_loadB(const uint4* bp, int kt, u32x4 (&d)[4]) {
+  const uint4* p = bp + kt * 32 * 64;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d[0]) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:1024" : "=v"(d[1]) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:2048" : "=v"(d[2]) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:3072" : "=v"(d[3]) : "v"(p) : "memory");
+}
+
+// one K step of the 112 x 64 wave tile: the 7 A fragments (row tile i at byte ab + 1024 i of
+// an LDS image) read up front, then each row tile's 4 MFMAs behind a counted lgkmcnt wait
+// for its own fragment (as g1dw4)
+__device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f4v (&acc)[7][4]) {
+  u32x4 aq[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) aq[i] = lds_read128(ab + i * 1024);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (i == 0) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(aq[0]));
+    else if (i == 1) asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(aq[1]));
+    else if (i == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(aq[2]));
+    else if (i == 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(aq[3]));
+    else if (i == 4) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(aq[4]));
+    else if (i == 5) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(aq[5]));
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(aq[6]));
+    const bf8v af = __builtin_bit_cast(bf8v, aq[i]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf8v, b[t]), acc[i][t], 0, 0, 0);
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned char* smem) {
+  uint4* ring = reinterpret_cast<uint4*>(smem);
+  uint32_t* Y = reinterpret_cast<uint32_t*>(smem + RF_RING);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fc = lane >> 4;
+  const int64_t r0 = roi * RF_S;
+  constexpr int NK = 512 / BK;
+
+  // GEMM1 A: slot tid = row tid >> 2 (rows >= 100 repeat row 99), chunk (tid & 3) ^ x16(row)
+  const int ar = tid >> 2;
+  const uint16_t* asrc = a.X + (r0 + min(ar, RF_S - 1)) * 512 + ((tid & 3) ^ x16(ar)) * 8;
+  auto issueA = [&](int kt) {
+    __builtin_amdgcn_global_load_lds(GPTR(asrc + kt * BK), LPTR(ring + (kt % 3) * RF_STAGE + wave * 64), 16, 0, 0);
+  };
+  // fragment (k step kt, col tile t) of the wave at [(g * 16 + kt) * 32 + 4 wave + t][lane]
+  const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
+  const uint4* b2p = a.W2p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
+  u32x4 bq[3][4];
+  const int lterm = fr * 4 + (fc ^ x16(fr));
+  const uint32_t ring_a = lds_addr(ring + lterm), y_a = lds_addr(Y) + lterm * 16;
+
+  f4v acc[7][4];
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // ---- GEMM1: Y1[112 x 64 per wave] = X . W1^T, K = 512.  Every load of the K loops is an
+  // asm statement (issue order fixed, no compiler waits): per step one DMA piece + four
+  // fragment loads, so vmcnt(5) at step kt retires step kt's and leaves kt + 1's in flight
+  issueA(0);
+  rf_loadB(b1p, 0, bq[0]);
+  issueA(1);
+  rf_loadB(b1p, 1, bq[1]);
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    u32x4(&b)[4] = bq[kt % 3];
+    if (kt + 1 < NK) asm volatile("s_waitcnt vmcnt(5)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+    else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+    g4_barrier();  // stage kt landed for every wave; stage (kt + 2) % 3 was last read in step kt - 1
+    if (kt + 2 < NK) {
+      issueA(kt + 2);
+      rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
+    }
+    rf_mfma_step(ring_a + (kt % 3) * RF_STAGE * 16, b, acc);
+  }
+
+  // depthwise taps of the lane's channel pair and GEMM2's first two B steps, in flight
+  // during the Y1 writes and the depthwise
+  const int cg = wave >> 1;  // the wave's 128 depthwise channels
+  dw_pair_t wreg[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k)
+    wreg[k] = *reinterpret_cast<const dw_pair_t*>(a.wdw + k * 1024 + G * 512 + cg * 128 + 2 * lane);
+  rf_loadB(b2p, 0, bq[0]);
+  rf_loadB(b2p, 1, bq[1]);
+
+  // ---- Y1 -> LDS as bf16 pairs (lane pairs trade values as in g1dw4)
+  {
+    const bool odd = fr & 1;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4v v = acc[i][t];
+        const float x0 = lane_xor1(odd ? v[0] : v[2]);
+        const float x1 = lane_xor1(odd ? v[1] : v[3]);
+        const int rb = i * 16 + fc * 4 + (odd ? 2 : 0);
+        const int col = wave * 64 + t * 16 + (fr & ~1);
+        if (rb < RF_S) Y[rf_yaddr(rb, col)] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
+        if (rb + 1 < RF_S) Y[rf_yaddr(rb + 1, col)] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+      }
+  }
+  rf_lds_barrier();
+
+  // ---- depthwise 5x5 in place: wave = (128-channel group, output half); both quadrants
+  // of the half are computed before anyone overwrites Y1
+  {
+    const int kb0 = cg * 4 + (lane >> 4), c0 = (lane & 15) >> 2, d0 = lane & 3;
+    const int yb0 = kb0 * RF_KBS + (c0 << 2) + d0, yb1 = kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0;
+    uint32_t o0[25], o1[25];
+    if ((wave & 1) == 0) {
+      rf_dw5q<0, 0>(Y, yb0, yb1, wreg, o0);
+      rf_dw5q<0, 1>(Y, yb0, yb1, wreg, o1);
+      rf_lds_barrier();
+      rf_dw5q_store<0, 0>(Y, yb0, yb1, o0);
+      rf_dw5q_store<0, 1>(Y, yb0, yb1, o1);
+    } else {
+      rf_dw5q<1, 0>(Y, yb0, yb1, wreg, o0);
+      rf_dw5q<1, 1>(Y, yb0, yb1, wreg, o1);
+      rf_lds_barrier();
+      rf_dw5q_store<1, 0>(Y, yb0, yb1, o0);
+      rf_dw5q_store<1, 1>(Y, yb0, yb1, o1);
+    }
+  }
+  rf_lds_barrier();
+
+  // ---- GEMM2: x = Y2 . W2^T (K = 512), A fragments from the resident Y image
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    u32x4(&b)[4] = bq[kt % 3];
+    if (kt + 1 < NK) asm volatile("s_waitcnt vmcnt(4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+    else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+    if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
+    rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
+  }
+
+  // ---- epilogue: BN-folded bias + activation
+  float bias4[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bias4[t] = a.bias[G * 512 + wave * 64 + t * 16 + fr];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f2v b2 = {bias4[t], bias4[t]};
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + b2;
+        v = G == 1 ? hswish2(v) : silu2(v);
+        acc[i][t][2 * h] = v.x;
+        acc[i][t][2 * h + 1] = v.y;
+      }
+  }
+  // column sums over the ROI's 100 rows (row tile 6 holds rows 96..111: lanes fc = 0 only)
+  {
+    const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) s += (acc[i][t][0] + acc[i][t][1]) + (acc[i][t][2] + acc[i][t][3]);
+      if (fc == 0) s += (acc[6][t][0] + acc[6][t][1]) + (acc[6][t][2] + acc[6][t][3]);
+      s = sum_xor16(s);
+      s = sum_xor32(s);
+      if (lane < 16) {
+        long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fr;
+        o[0] = llrintf(s * kFix);
+        for (int j = 1; j < cnt; ++j) o[j * 1024] = 0;
+      }
+    }
+  }
+  rf_lds_barrier();  // every wave's GEMM2 reads of Y are done: stage the output over it
+  {
+    uint32_t* stg = Y;
+    const bool odd = fr & 1;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4v v = acc[i][t];
+        const float x0 = lane_xor1(odd ? v[0] : v[2]);
+        const float x1 = lane_xor1(odd ? v[1] : v[3]);
+        const int rb = i * 16 + fc * 4 + (odd ? 2 : 0);
+        const int cp = (wave * 64 + t * 16 + fr) >> 1;
+        if (rb < RF_S) stg[rb * RF_OS + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
+        if (rb + 1 < RF_S) stg[(rb + 1) * RF_OS + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+      }
+  }
+  rf_lds_barrier();
+  {
+    const uint32_t* stg = Y;
+    uint16_t* dst = a.XRN + r0 * 1024 + G * 512;
+#pragma unroll 4
+    for (int q = tid; q < RF_S * 64; q += 512) {
+      const int row = q >> 6, c = q & 63;
+      *reinterpret_cast<uint4*>(dst + (int64_t)row * 1024 + c * 8) =
+          *reinterpret_cast<const uint4*>(stg + row * RF_OS + c * 4);
+    }
+  }
+}
+
+// workgroup (roi, g) = logical id 2 roi + g, XCD-remapped: a ROI's two groups run on one
+// XCD, so the second reads the ROI's X rows from L2
+__global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  if (lb & 1) rf_body<1>(a, lb >> 1, smem);
+  else rf_body<0>(a, lb >> 1, smem);
+}
+
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
@@ -1212,6 +1550,34 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
     hipLaunchKernelGGL(g1dw4_kernel<false>, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
                        (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
   return trk::check_launch("g1dw4_kernel");
+}
+
+extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                                 const float* bias, void* XRN, long long* sums, void* stream) {
+  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
+  if (M == 0) return TRK_OK;
+  TRK_REQUIRE(X && W1p && wdw && W2p && bias && XRN && sums && aligned16(X) && aligned16(W1p) && aligned16(W2p) &&
+                  aligned16(XRN) && aligned16(wdw),
+              "enc_rmb_front: null or unaligned pointer");
+  const int64_t nwg = M / RF_S * 2;
+  TRK_REQUIRE(nwg < 0x7fffffff, "enc_rmb_front: too many workgroups");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF_LDS);
+    attr = true;
+  }
+  RfArgs a;
+  a.X = (const uint16_t*)X;
+  a.W1p = (const uint4*)W1p;
+  a.wdw = wdw;
+  a.W2p = (const uint4*)W2p;
+  a.bias = bias;
+  a.XRN = (uint16_t*)XRN;
+  a.sums = sums;
+  hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
+                     a);
+  return trk::check_launch("rmb_front_kernel");
 }
 
 // diagnostics: gemm4 per-workgroup phase stamps (8 u64 per workgroup); nullptr

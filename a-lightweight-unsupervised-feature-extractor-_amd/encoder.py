@@ -165,6 +165,10 @@ class Model(nn.Module):
                 w2nk.append(w2 * scale[:, None])                                     # [C, 2h]
             w["w2_nk"] = torch.stack(w2nk, 0).contiguous().to(device, torch.bfloat16)  # [2, C, 2h]
             w["w1_nk"] = w1.contiguous().to(device, torch.bfloat16)                  # [4h, C]
+            if tuple(w["w1_nk"].shape) == (1024, 512) and tuple(w["w2_nk"].shape) == (2, 512, 512):
+                from .ops import enc_pack_fragments                                  # rmb_front operands
+                w["w1_pk"] = enc_pack_fragments(w["w1_nk"])
+                w["w2_pk"] = enc_pack_fragments(w["w2_nk"])
             w["b2"] = torch.cat([w["br"].float(), w["bn"].float()]).to(device, torch.float32)
             w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
             w["bt_f"] = r.transition[0].bias.float().to(device)
@@ -213,6 +217,8 @@ class Model(nn.Module):
     # fp32 (the parity path) keeps hipBLASLt GEMMs + the separate act/mean passes
     fused_gemm = True
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
+    fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel
+                         # (enc_rmb_front; Y2 never reaches HBM); False: enc_g1_dwconv + enc_dsc_gemm
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
     stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
@@ -221,7 +227,7 @@ class Model(nn.Module):
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
+                          enc_rmb_front, enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -232,7 +238,14 @@ class Model(nn.Module):
         Co = W["w2r"].shape[1]
         fused = (self.fused_gemm and dt == torch.bfloat16 and ss >= 32 and C % 32 == 0 and h4 % 256 == 0 and
                  h2 % 32 == 0 and Co % 256 == 0)
-        if fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_dwconv:
+        front = (fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_front and
+                 "w1_pk" in W and Co == 512)
+        if front:
+            XRN, sums = enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
+            if self.stage_hook is not None:
+                self.stage_hook("g1")
+                self.stage_hook("dsc")
+        elif fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_dwconv:
             Y2 = enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])               # first 1x1 convs + depthwise 5x5, one kernel
             if self.stage_hook is not None:
                 self.stage_hook("g1")
@@ -245,9 +258,10 @@ class Model(nn.Module):
         if fused:
             # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
             # + SiLU + GAP in another: the [M, 512] intermediates are written once (x_r|x_n)
-            XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
-            if self.stage_hook is not None:
-                self.stage_hook("dsc")
+            if not front:
+                XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
+                if self.stage_hook is not None:
+                    self.stage_hook("dsc")
             if self.fused_tail:
                 # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
                 m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])

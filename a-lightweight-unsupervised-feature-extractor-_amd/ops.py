@@ -185,6 +185,37 @@ def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor,
     return XRN, f[:, :Ng], f[:, Ng:]
 
 
+def enc_pack_fragments(W: torch.Tensor) -> torch.Tensor:
+    """[2*512, 512] (or [2, 512, 512]) bf16 weights [N][K] -> the 16x16x32 MFMA
+    fragment order trk_enc_rmb_front reads: [2][16 k steps][32 col tiles][64 lanes][8],
+    element (g, s, n, l, j) = W[g*512 + 16n + l%16][32s + 8(l//16) + j]."""
+    W = W.reshape(2, 32, 16, 16, 4, 8)                 # g, n, fr, s, fc, j
+    return W.permute(0, 3, 1, 4, 2, 5).contiguous()    # g, s, n, fc, fr, j  (lane = 16 fc + fr)
+
+
+def enc_rmb_front(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
+                  bias: torch.Tensor):
+    """bf16, 10x10 ROIs of 512 channels: enc_g1_dwconv + enc_dsc_gemm in one kernel
+    (Y2 stays in LDS).  X [R*100, 512], W1p / W2p from enc_pack_fragments, wdw [25, 1024]
+    f32, bias [1024] f32 -> (XRN [R*100, 1024], raw sums [R, TRK_ENC_PARTS, 1024])."""
+    _need_gpu(X, "enc_rmb_front")
+    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
+        raise TypeError("enc_rmb_front: bf16 operands required")
+    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
+        raise ValueError("enc_rmb_front: X must be contiguous [R*100, 512]")
+    if W1p.numel() != 1024 * 512 or W2p.numel() != 1024 * 512 or not (W1p.is_contiguous() and W2p.is_contiguous()):
+        raise ValueError("enc_rmb_front: W1p / W2p must be packed [2, 16, 32, 4, 16, 8] fragments")
+    if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
+        raise ValueError("enc_rmb_front: wdw [25, 1024] f32 and bias [1024] required")
+    M = X.shape[0]
+    XRN = torch.empty((M, 1024), device=X.device, dtype=torch.bfloat16)
+    sums = torch.empty((M // 100, _lib.TRK_ENC_PARTS, 1024), device=X.device, dtype=torch.int64)
+    check(lib().trk_enc_rmb_front(_ptr(X), M, _ptr(W1p), _ptr(wdw.contiguous()), _ptr(W2p),
+                                  _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(sums),
+                                  _stream(X.device)), "enc_rmb_front")
+    return XRN, sums
+
+
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
                         bias: torch.Tensor, raw: bool = False) -> torch.Tensor:
     """sum over each ROI's P rows of SiLU([x_f * s | x_n] . Wt^T + bias):

@@ -236,6 +236,18 @@ int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64_t N, const
                       void* stream);
 int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2, const float* bias,
                      int64_t Ng, void* XRN, long long* sums, void* stream);
+/* trk_enc_rmb_front: trk_enc_g1_dwconv followed by trk_enc_dsc_gemm in ONE kernel
+ *   for 10x10 ROIs of C = 512 channels (M = ROIs x 100, 4h = 1024, Ng = Kg = 512;
+ *   card.py:28-57): each workgroup runs one DSC (reinforce or normal) of one ROI with
+ *   Y1 and Y2 kept in LDS, so Y2 never reaches HBM.  Weights in MFMA fragment
+ *   order: W1p = W1 [1024][512] and W2p = W2 [2][512][512] each as
+ *   [2 groups][16 k steps][32 col tiles][64 lanes][8] bf16, element (g, s, n, l, j)
+ *   = W[g*512 + 16n + (l % 16)][32 s + 8 (l / 16) + j] (trk.ops.enc_pack_fragments);
+ *   wdw [25][1024] f32, bias [1024] f32 (BN-folded).  XRN is bit-identical to the
+ *   two-kernel path; sums (same layout as trk_enc_dsc_gemm's, ld 1024) hold the
+ *   ROI's whole sum in partial 0 and 0 in its other partials. */
+int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                      const float* bias, void* XRN, long long* sums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
 

@@ -626,6 +626,34 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         assert (d == 0).float().mean().item() >= 0.9
 
 
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R):
+    """trk_enc_rmb_front (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
+    LDS) vs enc_g1_dwconv -> enc_dsc_gemm: the same MFMA shape, K order and bf16
+    roundings, so XRN must be bit-identical; the ROI sums add the same f32 activations in
+    another order (tol 1e-5 of the largest sum).  R = 2048 is the bench's c3 launch."""
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(R)
+    M, P = R * 100, 100
+    X = torch.randn(M, 512, generator=g).to(gpu).bfloat16()
+    W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
+    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
+    W2 = (torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16()
+    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
+    Y2 = ops.enc_g1_dwconv(X, W1, wdw)
+    XRN2, s2 = ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True)
+    W1p, W2p = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2)
+    # the packing is a permutation: fragment (g, s, n, lane) holds W[g*512+16n+lane%16][32s+8(lane//16)+j]
+    assert W1p[1, 3, 5, 2, 7, 4].item() == W1[512 + 16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
+    XRN1, s1 = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    assert torch.equal(XRN1, XRN2)
+    f1, f2 = ops.enc_sums_reduce(s1, P), ops.enc_sums_reduce(s2, P)
+    assert (f1 - f2).abs().max().item() <= 1e-5 * f2.abs().max().item()
+    XRN1b, s1b = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)  # deterministic
+    assert torch.equal(XRN1, XRN1b) and torch.equal(ops.enc_sums_reduce(s1b, P), f1)
+
+
 def _partials(total, P, parts=3):
     """split int64 per-ROI totals [R, ld] into the GEMMs' partial layout
     [R, parts, ld] (one entry per 128-row tile covering the ROI; the rest junk)"""
