@@ -1117,6 +1117,7 @@ struct RfArgs {
   const float* bias;    // [1024] BN-folded bias
   uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
   long long* sums;      // [R][kPart][1024] int64 x 2^24: partial 0 = the ROI's sum, the rest 0
+  unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
 };
 
 // Y dword of (pixel s, channel pair at column col of the group): block col / 32,
@@ -1227,7 +1228,11 @@ __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f
 }
 
 template <int G>
-__device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned char* smem) {
+__device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned char* smem) {
+  const int64_t roi = lb >> 1;
+  unsigned long long pst[8];
+  const bool prof = a.prof != nullptr;
+  if (prof) pst[0] = eg_stamp();
   uint4* ring = reinterpret_cast<uint4*>(smem);
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem + RF_RING);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1275,6 +1280,10 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
     rf_mfma_step(ring_a + (kt % 3) * RF_STAGE * 16, b, acc);
   }
 
+  if (prof) {
+    asm volatile("" ::"v"(acc[6][3][3]));
+    pst[1] = eg_stamp();
+  }
   // depthwise taps of the lane's channel pair and GEMM2's first two B steps, in flight
   // during the Y1 writes and the depthwise
   const int cg = wave >> 1;  // the wave's 128 depthwise channels
@@ -1302,6 +1311,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
       }
   }
   rf_lds_barrier();
+  if (prof) pst[2] = eg_stamp();
 
   // ---- depthwise 5x5 in place: wave = (128-channel group, output half); both quadrants
   // of the half are computed before anyone overwrites Y1
@@ -1324,6 +1334,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
     }
   }
   rf_lds_barrier();
+  if (prof) pst[3] = eg_stamp();
 
   // ---- GEMM2: x = Y2 . W2^T (K = 512), A fragments from the resident Y image
 #pragma unroll
@@ -1339,6 +1350,10 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
     rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
   }
 
+  if (prof) {
+    asm volatile("" ::"v"(acc[6][3][3]));
+    pst[4] = eg_stamp();
+  }
   // ---- epilogue: BN-folded bias + activation
   float bias4[4];
 #pragma unroll
@@ -1374,6 +1389,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
       }
     }
   }
+  if (prof) pst[5] = eg_stamp();
   rf_lds_barrier();  // every wave's GEMM2 reads of Y are done: stage the output over it
   {
     uint32_t* stg = Y;
@@ -1392,6 +1408,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
       }
   }
   rf_lds_barrier();
+  if (prof) pst[6] = eg_stamp();
   {
     const uint32_t* stg = Y;
     uint16_t* dst = a.XRN + r0 * 1024 + G * 512;
@@ -1402,6 +1419,15 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
           *reinterpret_cast<const uint4*>(stg + row * RF_OS + c * 4);
     }
   }
+  if (prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pst[7] = eg_stamp();
+    if (tid == 0) {
+      unsigned long long* o = a.prof + lb * 8;
+      for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
+      o[7] = pst[7] - pst[0];
+    }
+  }
 }
 
 // workgroup (roi, g) = logical id 2 roi + g, XCD-remapped: a ROI's two groups run on one
@@ -1409,8 +1435,8 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t roi, unsigned c
 __global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  if (lb & 1) rf_body<1>(a, lb >> 1, smem);
-  else rf_body<0>(a, lb >> 1, smem);
+  if (lb & 1) rf_body<1>(a, lb, smem);
+  else rf_body<0>(a, lb, smem);
 }
 
 template <int EPI>
@@ -1575,6 +1601,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.bias = bias;
   a.XRN = (uint16_t*)XRN;
   a.sums = sums;
+  a.prof = g_enc_prof;
   hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
                      a);
   return trk::check_launch("rmb_front_kernel");
