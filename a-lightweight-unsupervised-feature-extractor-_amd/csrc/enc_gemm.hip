@@ -1086,28 +1086,51 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
 // 8 waves, one workgroup per CU (126 KiB of LDS).  Wave w owns output columns
 // 64 w .. 64 w + 63 of the group's 512 in BOTH GEMMs and all 112 rows (7 row
 // tiles of 16; rows 100..111 are padding whose results are dropped): a 112 x 64
-// wave tile of 16x16x32 MFMAs, 112 accumulator registers.  No B element is used
-// by two waves, so B does not go through LDS: the weights are pre-packed on the
-// host in MFMA fragment order ([g][k step][16-col tile][lane] x 16 B), and a
-// wave's four fragments of a K step are one contiguous 4 KiB read straight into
-// VGPRs, two steps ahead.  A (the ROI's X rows, shared by the 8 waves) is staged by
-// LDS-DMA into a 3-buffer ring (g1dw4's image: row r chunk c at 16-B slot
-// r*4 + (c ^ x16(r))).  Y is kept as 16 K blocks of 32 channels in that same
-// image (100 rows x 64 B per block, block stride 6464 B so the depthwise's
-// 4-B channel-pair reads of two blocks fall on different banks), so GEMM2 reads
-// its A fragments from Y exactly as GEMM1 reads the ring.  Same MFMA shape, K order
-// and roundings (Y1 and Y2 to bf16) as g1dw4 + gemm4<DSC>: XRN is bit-identical
-// to the two-kernel path; the column sums add the same f32 activations in another
-// order (exact f32 lane sums, one partial per ROI).
+// wave tile of 16x16x32 MFMAs, 112 accumulator registers.  No weight element is used
+// by two waves, so weights do not go through LDS: they are pre-packed on the host in
+// MFMA fragment order ([g][k step][16-col tile][lane] x 16 B), and a wave's four
+// fragments of a K step are one contiguous 4 KiB read straight into VGPRs, two steps
+// ahead.  The ROI's X rows (shared by the 8 waves) are staged by LDS-DMA into the same
+// LDS image Y1 and Y2 use later: 16 K blocks of 32 channels, 100 rows x 64 B per block
+// (row r's 16-B chunk c at slot r*4 + (c ^ sw(r)), sw(r) = (r >> 1) & 3: conflict-free
+// ds_read_b128 fragment reads, 2-way 8-B row writes), block stride 6464 B so the
+// depthwise's 4-B channel-pair reads of two blocks fall on different banks.  X arrives in
+// four groups of four blocks, each issued four K steps ahead: GEMM1 waits at 4 barriers
+// instead of one per K step (a per-step barrier kept the 8 waves' LDS reads in lockstep:
+// GEMM1 ran 2.3x GEMM2's time for the same MFMAs).  Both GEMMs are computed transposed
+// (weights = A operand), so a lane holds 4 consecutive channels of one pixel.  Same
+// MFMA shape, K order and roundings (Y1 and Y2 to bf16) as g1dw4 + gemm4<DSC>: XRN is
+// bit-identical to the two-kernel path; the column sums add the same f32 activations
+// in another order (f32 lane sums, one partial per ROI).
 constexpr int RF_S = 100;                                      // rows per ROI
-constexpr int RF_STAGE = 512;                                  // A stage: 128 rows x 4 16-B chunks
-constexpr size_t RF_RING = (size_t)3 * RF_STAGE * 16;          // 24 KiB
-constexpr int RF_KBS = 1616;                                   // Y block stride (dwords): 6400 B + 64
+constexpr int RF_KBS = 1616;                                   // block stride (dwords): 6400 B + 64
 constexpr size_t RF_Y = (size_t)15 * RF_KBS * 4 + 112 * 64;    // row tile 6 of block 15 reads rows ..111
 constexpr int RF_OS = 260;                                     // output staging row stride (dwords)
-constexpr size_t RF_LDS = RF_RING + RF_Y;
+constexpr size_t RF_LDS = RF_Y;
 static_assert((size_t)RF_S * RF_OS * 4 <= RF_Y, "output staging reuses the Y image");
 static_assert(RF_LDS <= 160 * 1024, "one rmb_front workgroup per CU");
+
+// GEMM1 issue order: X group 0 (blocks 0..3, one DMA op per block per wave), B(0), B(1);
+// step kt issues X group kt / 4 + 1 when kt % 4 == 0 (4 ops), then B(kt + 2).  Ops issued
+// after B(kt) when step kt starts = the vmcnt that retires B(kt) and every older X group
+constexpr int rf_vm_after_b(int kt) {
+  constexpr int NK = 16;
+  if (kt == 0) return 4;
+  if (kt == 1) return 4 + 4;
+  return ((kt - 1) % 4 == 0 && (kt - 1) / 4 + 1 < 4 ? 4 : 0) + (kt + 1 < NK ? 4 : 0);
+}
+
+// s_waitcnt vmcnt(n) for a (compile-time after unrolling) n, tied to the four fragment registers
+__device__ __forceinline__ void rf_vmwait(int n, u32x4 (&b)[4]) {
+#define RF_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory"); break;
+  switch (n) {
+    RF_VMW(1) RF_VMW(2) RF_VMW(3) RF_VMW(4) RF_VMW(5) RF_VMW(6) RF_VMW(7) RF_VMW(8) RF_VMW(9) RF_VMW(10)
+    RF_VMW(11) RF_VMW(12) RF_VMW(13) RF_VMW(14) RF_VMW(15)
+    default: asm volatile("s_waitcnt vmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+  }
+#undef RF_VMW
+}
 
 struct RfArgs {
   const uint16_t* X;    // [R * 100][512] bf16 NHWC ROI rows
@@ -1117,28 +1140,30 @@ struct RfArgs {
   const float* bias;    // [1024] BN-folded bias
   uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
   long long* sums;      // [R][kPart][1024] int64 x 2^24: partial 0 = the ROI's sum, the rest 0
+  int64_t R;            // ROIs
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
 };
 
+__device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
 // Y dword of (pixel s, channel pair at column col of the group): block col / 32,
-// chunk (col % 32) / 8 swizzled by x16(s), dword (col % 8) / 2
+// chunk (col % 32) / 8 swizzled by rf_sw(s), dword (col % 8) / 2
 __device__ __forceinline__ int rf_yaddr(int s, int col) {
   const int kb = col >> 5, c = (col & 31) >> 3, d = (col & 7) >> 1;
-  return kb * RF_KBS + s * 16 + ((c ^ x16(s)) << 2) + d;
+  return kb * RF_KBS + s * 16 + ((c ^ rf_sw(s)) << 2) + d;
 }
 
 // depthwise 5x5 of output quadrant (QY, QX) for the lane's channel pair, results
 // held as packed bf16 pairs (the caller writes them back in place after a barrier);
-// same per-output FMA order as dw5q_regs.  Pixel s sits at dword b1 + 16 s when
-// x16(s) != 0, else b0 + 16 s (s is a constant after unrolling).
+// same per-output FMA order as dw5q_regs.  Pixel s sits at dword b[rf_sw(s)] + 16 s (s is
+// a constant after unrolling).
 template <int QY, int QX>
-__device__ __forceinline__ void rf_dw5q(const uint32_t* y, int b0, int b1, const dw_pair_t (&w)[25],
+__device__ __forceinline__ void rf_dw5q(const uint32_t* y, const int (&b)[4], const dw_pair_t (&w)[25],
                                         uint32_t (&out)[25]) {
   constexpr int OY0 = 5 * QY, X0 = 5 * QX;
   constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY0 + 6 > G1_S - 1 ? G1_S - 1 : OY0 + 6;
   constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
   constexpr int NX = IX1 - IX0 + 1;
-  auto at = [&](int s) { return y[(((s >> 3) & 1) ? b1 : b0) + s * 16]; };
+  auto at = [&](int s) { return y[b[rf_sw(s)] + s * 16]; };
   dw_pair_t acc[5][5];
 #pragma unroll
   for (int oy = 0; oy < 5; ++oy)
@@ -1178,13 +1203,13 @@ __device__ __forceinline__ void rf_dw5q(const uint32_t* y, int b0, int b1, const
     for (int ox = 0; ox < 5; ++ox) out[oy * 5 + ox] = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
 }
 template <int QY, int QX>
-__device__ __forceinline__ void rf_dw5q_store(uint32_t* y, int b0, int b1, const uint32_t (&out)[25]) {
+__device__ __forceinline__ void rf_dw5q_store(uint32_t* y, const int (&b)[4], const uint32_t (&out)[25]) {
 #pragma unroll
   for (int oy = 0; oy < 5; ++oy)
 #pragma unroll
     for (int ox = 0; ox < 5; ++ox) {
       const int s = (5 * QY + oy) * G1_S + 5 * QX + ox;
-      y[(((s >> 3) & 1) ? b1 : b0) + s * 16] = out[oy * 5 + ox];
+      y[b[rf_sw(s)] + s * 16] = out[oy * 5 + ox];
     }
 }
 
@@ -1196,6 +1221,7 @@ __device__ __forceinline__ void rf_lds_barrier() {
 // the wave's four B fragments of k step kt (4 KiB contiguous): asm loads, so the issue order
 // is the program order and the caller's counted vmcnt waits are exact
 __device__ __forceinline__ void rf_loadB(const uint4* bp, int kt, u32x4 (&d)[4]) {
+  asm volatile("" : "+v"(bp));  // per call: keeps the compiler from hoisting all 32 step addresses
   const uint4* p = bp + kt * 32 * 64;
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d[0]) : "v"(p) : "memory");
   asm volatile("global_load_dwordx4 %0, %1, off offset:1024" : "=v"(d[1]) : "v"(p) : "memory");
@@ -1203,13 +1229,21 @@ __device__ __forceinline__ void rf_loadB(const uint4* bp, int kt, u32x4 (&d)[4])
   asm volatile("global_load_dwordx4 %0, %1, off offset:3072" : "=v"(d[3]) : "v"(p) : "memory");
 }
 
-// one K step of the 112 x 64 wave tile: the 7 A fragments (row tile i at byte ab + 1024 i of
-// an LDS image) read up front, then each row tile's 4 MFMAs behind a counted lgkmcnt wait
-// for its own fragment (as g1dw4)
+// one K step of the wave's 64-channel x 112-pixel tile, computed transposed (C = W . X^T:
+// the weight fragments are the A operand, the activation rows the B operand, so lane
+// (fr, fc) of tile (i, t) ends up with channels 16 t + 4 fc .. + 3 of pixel 16 i + fr, four
+// consecutive channels of one pixel = one 8-B LDS store).  The 7 pixel-tile fragments
+// (tile i at byte ab + 1024 i of an LDS image) are read up front, then each tile's 4 MFMAs
+// wait (counted lgkmcnt) for its own fragment only, as g1dw4
 __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f4v (&acc)[7][4]) {
   u32x4 aq[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) aq[i] = lds_read128(ab + i * 1024);
+  asm volatile("ds_read_b128 %0, %1" : "=v"(aq[0]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(aq[1]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(aq[2]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(aq[3]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(aq[4]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(aq[5]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(aq[6]) : "v"(ab) : "memory");
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     __builtin_amdgcn_sched_barrier(0);
@@ -1220,10 +1254,10 @@ __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f
     else if (i == 4) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(aq[4]));
     else if (i == 5) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(aq[5]));
     else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(aq[6]));
-    const bf8v af = __builtin_bit_cast(bf8v, aq[i]);
+    const bf8v xf = __builtin_bit_cast(bf8v, aq[i]);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf8v, b[t]), acc[i][t], 0, 0, 0);
+      acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, b[t]), xf, acc[i][t], 0, 0, 0);
   }
 }
 
@@ -1233,26 +1267,32 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
   unsigned long long pst[8];
   const bool prof = a.prof != nullptr;
   if (prof) pst[0] = eg_stamp();
-  uint4* ring = reinterpret_cast<uint4*>(smem);
-  uint32_t* Y = reinterpret_cast<uint32_t*>(smem + RF_RING);
+  uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fc = lane >> 4;
   const int64_t r0 = roi * RF_S;
   constexpr int NK = 512 / BK;
 
-  // GEMM1 A: slot tid = row tid >> 2 (rows >= 100 repeat row 99), chunk (tid & 3) ^ x16(row)
-  const int ar = tid >> 2;
-  const uint16_t* asrc = a.X + (r0 + min(ar, RF_S - 1)) * 512 + ((tid & 3) ^ x16(ar)) * 8;
-  auto issueA = [&](int kt) {
-    __builtin_amdgcn_global_load_lds(GPTR(asrc + kt * BK), LPTR(ring + (kt % 3) * RF_STAGE + wave * 64), 16, 0, 0);
+  // X -> the LDS image: wave w's lanes < 50 move pieces 50 w + lane (row p >> 2, slot p & 3)
+  // of every block, one DMA op per block
+  const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
+  const uint16_t* xsrc = a.X + (r0 + xr) * 512 + (((xp & 3) ^ rf_sw(xr)) * 8);
+  auto issueX = [&](int grp) {
+    if (lane < 50) {
+      const uint16_t* xs = xsrc;
+      asm volatile("" : "+v"(xs));  // per group: the 16 block addresses are not all hoisted
+#pragma unroll
+      for (int kb = 4 * grp; kb < 4 * grp + 4; ++kb)
+        __builtin_amdgcn_global_load_lds(GPTR(xs + kb * BK), LPTR(Y + kb * RF_KBS + 200 * wave), 16, 0, 0);
+    }
   };
   // fragment (k step kt, col tile t) of the wave at [(g * 16 + kt) * 32 + 4 wave + t][lane]
   const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
   const uint4* b2p = a.W2p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
   u32x4 bq[3][4];
-  const int lterm = fr * 4 + (fc ^ x16(fr));
-  const uint32_t ring_a = lds_addr(ring + lterm), y_a = lds_addr(Y) + lterm * 16;
+  const int lterm = fr * 4 + (fc ^ rf_sw(fr));
+  const uint32_t y_a = lds_addr(Y) + lterm * 16;
 
   f4v acc[7][4];
 #pragma unroll
@@ -1260,26 +1300,22 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  // ---- GEMM1: Y1[112 x 64 per wave] = X . W1^T, K = 512.  Every load of the K loops is an
-  // asm statement (issue order fixed, no compiler waits): per step one DMA piece + four
-  // fragment loads, so vmcnt(5) at step kt retires step kt's and leaves kt + 1's in flight
-  issueA(0);
+  // ---- GEMM1: Y1^T[64 x 112 per wave] = W1 . X^T, K = 512.  Every load of the K loops is
+  // an asm statement or the DMA builtin in program order (no compiler waits)
+  issueX(0);
   rf_loadB(b1p, 0, bq[0]);
-  issueA(1);
   rf_loadB(b1p, 1, bq[1]);
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
     u32x4(&b)[4] = bq[kt % 3];
-    if (kt + 1 < NK) asm volatile("s_waitcnt vmcnt(5)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
-    else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
-    g4_barrier();  // stage kt landed for every wave; stage (kt + 2) % 3 was last read in step kt - 1
-    if (kt + 2 < NK) {
-      issueA(kt + 2);
-      rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
+    rf_vmwait(rf_vm_after_b(kt), b);
+    if (kt % 4 == 0) {
+      g4_barrier();  // X group kt / 4 landed for every wave
+      if (kt / 4 + 1 < 4) issueX(kt / 4 + 1);
     }
-    rf_mfma_step(ring_a + (kt % 3) * RF_STAGE * 16, b, acc);
+    if (kt + 2 < NK) rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
+    rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
   }
-
   if (prof) {
     asm volatile("" ::"v"(acc[6][3][3]));
     pst[1] = eg_stamp();
@@ -1293,22 +1329,33 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     wreg[k] = *reinterpret_cast<const dw_pair_t*>(a.wdw + k * 1024 + G * 512 + cg * 128 + 2 * lane);
   rf_loadB(b2p, 0, bq[0]);
   rf_loadB(b2p, 1, bq[1]);
+  // L2 prefetch (reinforce workgroups) of the X rows of ROI + 16: the XCD's 32 CUs run
+  // 16 ROIs at a time, so that ROI starts about when this one ends; its first DMA group
+  // then hits L2.  Two 4-B loads per thread = the ROI's 800 128-B lines; retired by
+  // GEMM2's third wait
+  constexpr int NPF = G == 0 ? 2 : 0;
+  uint32_t pf0 = 0, pf1 = 0;
+  if (G == 0) {
+    const int64_t rn = min(roi + 16, a.R - 1);
+    const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
+    const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
+    asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "+v"(pf1) : "v"(pb) : "memory");
+  }
 
-  // ---- Y1 -> LDS as bf16 pairs (lane pairs trade values as in g1dw4)
-  {
-    const bool odd = fr & 1;
+  rf_lds_barrier();  // every wave's GEMM1 reads of X are done: Y1 overwrites the image
+  // ---- Y1 -> LDS: each lane stores its 4 channels of a pixel as one 8-B write
 #pragma unroll
-    for (int i = 0; i < 7; ++i)
+  for (int i = 0; i < 7; ++i) {
+    const int px = i * 16 + fr;
+    if (px < RF_S) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const f4v v = acc[i][t];
-        const float x0 = lane_xor1(odd ? v[0] : v[2]);
-        const float x1 = lane_xor1(odd ? v[1] : v[3]);
-        const int rb = i * 16 + fc * 4 + (odd ? 2 : 0);
-        const int col = wave * 64 + t * 16 + (fr & ~1);
-        if (rb < RF_S) Y[rf_yaddr(rb, col)] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
-        if (rb + 1 < RF_S) Y[rf_yaddr(rb + 1, col)] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+        *reinterpret_cast<uint2*>(Y + rf_yaddr(px, wave * 64 + t * 16 + fc * 4)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       }
+    }
   }
   rf_lds_barrier();
   if (prof) pst[2] = eg_stamp();
@@ -1317,20 +1364,21 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
   // of the half are computed before anyone overwrites Y1
   {
     const int kb0 = cg * 4 + (lane >> 4), c0 = (lane & 15) >> 2, d0 = lane & 3;
-    const int yb0 = kb0 * RF_KBS + (c0 << 2) + d0, yb1 = kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0;
+    const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
+                       kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
     uint32_t o0[25], o1[25];
     if ((wave & 1) == 0) {
-      rf_dw5q<0, 0>(Y, yb0, yb1, wreg, o0);
-      rf_dw5q<0, 1>(Y, yb0, yb1, wreg, o1);
+      rf_dw5q<0, 0>(Y, yb, wreg, o0);
+      rf_dw5q<0, 1>(Y, yb, wreg, o1);
       rf_lds_barrier();
-      rf_dw5q_store<0, 0>(Y, yb0, yb1, o0);
-      rf_dw5q_store<0, 1>(Y, yb0, yb1, o1);
+      rf_dw5q_store<0, 0>(Y, yb, o0);
+      rf_dw5q_store<0, 1>(Y, yb, o1);
     } else {
-      rf_dw5q<1, 0>(Y, yb0, yb1, wreg, o0);
-      rf_dw5q<1, 1>(Y, yb0, yb1, wreg, o1);
+      rf_dw5q<1, 0>(Y, yb, wreg, o0);
+      rf_dw5q<1, 1>(Y, yb, wreg, o1);
       rf_lds_barrier();
-      rf_dw5q_store<1, 0>(Y, yb0, yb1, o0);
-      rf_dw5q_store<1, 1>(Y, yb0, yb1, o1);
+      rf_dw5q_store<1, 0>(Y, yb, o0);
+      rf_dw5q_store<1, 1>(Y, yb, o1);
     }
   }
   rf_lds_barrier();
@@ -1344,8 +1392,8 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
     u32x4(&b)[4] = bq[kt % 3];
-    if (kt + 1 < NK) asm volatile("s_waitcnt vmcnt(4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
-    else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+    rf_vmwait(kt + 1 < NK ? 4 + (kt < 2 ? NPF : 0) : 0, b);
+    if (kt == 2 && G == 0) asm volatile("" : "+v"(pf0), "+v"(pf1));  // retired by the wait above
     if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
     rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
   }
@@ -1354,58 +1402,69 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     asm volatile("" ::"v"(acc[6][3][3]));
     pst[4] = eg_stamp();
   }
-  // ---- epilogue: BN-folded bias + activation
-  float bias4[4];
+  // ---- epilogue: BN-folded bias + activation (lane: channels 16 t + 4 fc + e)
+  float4 bias4[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) bias4[t] = a.bias[G * 512 + wave * 64 + t * 16 + fr];
+  for (int t = 0; t < 4; ++t)
+    bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const f2v b2 = {bias4[t], bias4[t]};
+    const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
 #pragma unroll
     for (int i = 0; i < 7; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + b2;
+        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
         v = G == 1 ? hswish2(v) : silu2(v);
         acc[i][t][2 * h] = v.x;
         acc[i][t][2 * h + 1] = v.y;
       }
   }
-  // column sums over the ROI's 100 rows (row tile 6 holds rows 96..111: lanes fc = 0 only)
+  // column sums over the ROI's 100 pixels: per lane over its pixel tiles (tile 6 holds
+  // pixels 96..111: fr < 4 only), then over the 16 pixel lanes fr of each channel group
   {
     const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      float s = 0.f;
+      float sv[4];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) s += (acc[i][t][0] + acc[i][t][1]) + (acc[i][t][2] + acc[i][t][3]);
-      if (fc == 0) s += (acc[6][t][0] + acc[6][t][1]) + (acc[6][t][2] + acc[6][t][3]);
-      s = sum_xor16(s);
-      s = sum_xor32(s);
-      if (lane < 16) {
-        long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fr;
-        o[0] = llrintf(s * kFix);
-        for (int j = 1; j < cnt; ++j) o[j * 1024] = 0;
+      for (int e = 0; e < 4; ++e) {
+        float x = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) x += acc[i][t][e];
+        if (fr < 4) x += acc[6][t][e];
+        sv[e] = x;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sv[e] += lane_xor1(sv[e]);
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
+        sv[e] += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(sv[e]), 0x101F));          // ^4
+        sv[e] += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(sv[e]), 0x201F));          // ^8
+      }
+      if (fr == 0) {
+        long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[e] * kFix);
+        for (int j = 1; j < cnt; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[j * 1024 + e] = 0;
       }
     }
   }
   if (prof) pst[5] = eg_stamp();
   rf_lds_barrier();  // every wave's GEMM2 reads of Y are done: stage the output over it
-  {
-    uint32_t* stg = Y;
-    const bool odd = fr & 1;
 #pragma unroll
-    for (int i = 0; i < 7; ++i)
+  for (int i = 0; i < 7; ++i) {
+    const int px = i * 16 + fr;
+    if (px < RF_S) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const f4v v = acc[i][t];
-        const float x0 = lane_xor1(odd ? v[0] : v[2]);
-        const float x1 = lane_xor1(odd ? v[1] : v[3]);
-        const int rb = i * 16 + fc * 4 + (odd ? 2 : 0);
-        const int cp = (wave * 64 + t * 16 + fr) >> 1;
-        if (rb < RF_S) stg[rb * RF_OS + cp] = odd ? pack_bf16x2(x0, v[2]) : pack_bf16x2(v[0], x0);
-        if (rb + 1 < RF_S) stg[(rb + 1) * RF_OS + cp] = odd ? pack_bf16x2(x1, v[3]) : pack_bf16x2(v[1], x1);
+        *reinterpret_cast<uint2*>(Y + px * RF_OS + ((wave * 64 + t * 16 + fc * 4) >> 1)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       }
+    }
   }
   rf_lds_barrier();
   if (prof) pst[6] = eg_stamp();
@@ -1601,6 +1660,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.bias = bias;
   a.XRN = (uint16_t*)XRN;
   a.sums = sums;
+  a.R = M / RF_S;
   a.prof = g_enc_prof;
   hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
                      a);
