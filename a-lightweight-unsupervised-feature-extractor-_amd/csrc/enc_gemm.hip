@@ -1385,6 +1385,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
   if (prof) pst[3] = eg_stamp();
 
   // ---- GEMM2: x = Y2 . W2^T (K = 512), A fragments from the resident Y image
+  float4 bias4[4];
 #pragma unroll
   for (int i = 0; i < 7; ++i)
 #pragma unroll
@@ -1395,6 +1396,11 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     rf_vmwait(kt + 1 < NK ? 4 + (kt < 2 ? NPF : 0) : 0, b);
     if (kt == 2 && G == 0) asm volatile("" : "+v"(pf0), "+v"(pf1));  // retired by the wait above
     if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
+    if (kt == NK - 3) {  // the epilogue's bias, three steps before it is needed (L2 latency)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
+    }
     rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
   }
 
@@ -1403,10 +1409,6 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     pst[4] = eg_stamp();
   }
   // ---- epilogue: BN-folded bias + activation (lane: channels 16 t + 4 fc + e)
-  float4 bias4[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};

@@ -69,3 +69,25 @@ def test_encoder_fused_graph_fp32_vs_reference_golden(trk, s):
     with torch.no_grad():
         z = m(x).numpy()
     assert np.max(np.abs(z - d[f"z_s{s}"])) < 1e-5
+
+
+def test_rmb_front_fragment_packing_and_argument_errors(trk):
+    """enc_pack_fragments is the exact permutation trk_enc_rmb_front reads (element
+    (g, s, n, l, j) = W[g*512 + 16n + l%16][32s + 8(l//16) + j]); the entry point rejects
+    M % 100 != 0 and null pointers on the host."""
+    import torch
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    W = torch.arange(1024 * 512, dtype=torch.int64).view(1024, 512)
+    P = ops.enc_pack_fragments(W).view(2, 16, 32, 64, 8)
+    g, s, n, l, j = torch.meshgrid(*[torch.arange(k) for k in (2, 16, 32, 64, 8)], indexing="ij")
+    ref = W[g * 512 + 16 * n + l % 16, 32 * s + 8 * (l // 16) + j]
+    assert torch.equal(P, ref)
+    assert torch.equal(ops.enc_pack_fragments(W.view(2, 512, 512)), ops.enc_pack_fragments(W))
+    L = trk.lib()
+    assert L.trk_enc_rmb_front(ctypes.c_void_p(16), 150, ctypes.c_void_p(16), ctypes.c_void_p(16),
+                               ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16),
+                               ctypes.c_void_p(16), None) == -1
+    assert b"M % 100" in L.trk_last_error()
+    assert L.trk_enc_rmb_front(None, 100, None, None, None, None, None, None, None) == -1
+    assert L.trk_enc_rmb_front(None, 0, None, None, None, None, None, None, None) == 0
