@@ -434,7 +434,8 @@ __device__ __forceinline__ f2v silu2(f2v v) {
 }
 __device__ __forceinline__ f2v hswish2(f2v v) {
   const f2v c = v + f2v{3.0f, 3.0f};
-  const f2v r = f2v{fminf(fmaxf(c.x, 0.0f), 6.0f), fminf(fmaxf(c.y, 0.0f), 6.0f)};
+  // v_med3_f32 (one op) = min(max(c, 0), 6) for every non-NaN c
+  const f2v r = f2v{__builtin_amdgcn_fmed3f(c.x, 0.0f, 6.0f), __builtin_amdgcn_fmed3f(c.y, 0.0f, 6.0f)};
   return (v * r) * f2v{1.0f / 6.0f, 1.0f / 6.0f};
 }
 
@@ -1320,29 +1321,9 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     asm volatile("" ::"v"(acc[6][3][3]));
     pst[1] = eg_stamp();
   }
-  // depthwise taps of the lane's channel pair and GEMM2's first two B steps, in flight
-  // during the Y1 writes and the depthwise
-  const int cg = wave >> 1;  // the wave's 128 depthwise channels
-  dw_pair_t wreg[25];
-#pragma unroll
-  for (int k = 0; k < 25; ++k)
-    wreg[k] = *reinterpret_cast<const dw_pair_t*>(a.wdw + k * 1024 + G * 512 + cg * 128 + 2 * lane);
-  rf_loadB(b2p, 0, bq[0]);
-  rf_loadB(b2p, 1, bq[1]);
-  // L2 prefetch (reinforce workgroups) of the X rows of ROI + 16: the XCD's 32 CUs run
-  // 16 ROIs at a time, so that ROI starts about when this one ends; its first DMA group
-  // then hits L2.  Two 4-B loads per thread = the ROI's 800 128-B lines; retired by
-  // GEMM2's third wait
-  constexpr int NPF = G == 0 ? 2 : 0;
-  uint32_t pf0 = 0, pf1 = 0;
-  if (G == 0) {
-    const int64_t rn = min(roi + 16, a.R - 1);
-    const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
-    const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
-    asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "+v"(pf1) : "v"(pb) : "memory");
-  }
-
+  // the compiler puts an s_waitcnt vmcnt(0) before the first LDS access after an LDS-DMA
+  // (alias safety): nothing but retired GEMM1 loads may be in flight there, so every load
+  // below is issued after the Y1 writes, and the L2 prefetch after the depthwise's reads
   rf_lds_barrier();  // every wave's GEMM1 reads of X are done: Y1 overwrites the image
   // ---- Y1 -> LDS: each lane stores its 4 channels of a pixel as one 8-B write
 #pragma unroll
@@ -1357,25 +1338,60 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
       }
     }
   }
+  // depthwise taps of the lane's channel pair (asm loads, waited for below with a count that
+  // leaves GEMM2's first two B steps in flight)
+  const int cg = wave >> 1;  // the wave's 128 depthwise channels
+  dw_pair_t wreg[25];
+  {
+    const float* wp = a.wdw + G * 512 + cg * 128 + 2 * lane;
+#pragma unroll
+    for (int k = 0; k < 25; ++k)
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(wreg[k]) : "v"(wp + k * 1024) : "memory");
+  }
+  rf_loadB(b2p, 0, bq[0]);
+  rf_loadB(b2p, 1, bq[1]);
   rf_lds_barrier();
+  if (prof) pst[2] = eg_stamp();
+  asm volatile("s_waitcnt vmcnt(8)" : "+v"(wreg[0]), "+v"(wreg[1]), "+v"(wreg[2]), "+v"(wreg[3]), "+v"(wreg[4]),
+               "+v"(wreg[5]), "+v"(wreg[6]), "+v"(wreg[7]), "+v"(wreg[8]), "+v"(wreg[9]), "+v"(wreg[10]),
+               "+v"(wreg[11]), "+v"(wreg[12])::"memory");
+  asm volatile("" : "+v"(wreg[13]), "+v"(wreg[14]), "+v"(wreg[15]), "+v"(wreg[16]), "+v"(wreg[17]), "+v"(wreg[18]),
+               "+v"(wreg[19]), "+v"(wreg[20]), "+v"(wreg[21]), "+v"(wreg[22]), "+v"(wreg[23]), "+v"(wreg[24]));
   if (prof) pst[2] = eg_stamp();
 
   // ---- depthwise 5x5 in place: wave = (128-channel group, output half); both quadrants
   // of the half are computed before anyone overwrites Y1
+  constexpr int NPF = G == 0 ? 2 : 0;
+  uint32_t pf0 = 0, pf1 = 0;
   {
     const int kb0 = cg * 4 + (lane >> 4), c0 = (lane & 15) >> 2, d0 = lane & 3;
     const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
                        kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
     uint32_t o0[25], o1[25];
+    // L2 prefetch (reinforce workgroups) of the X rows of ROI + 16: the XCD's 32 CUs run
+    // 16 ROIs at a time, so that ROI starts about when this one ends; its first DMA group
+    // then hits L2.  Two 4-B loads per thread = the ROI's 800 128-B lines; retired by
+    // GEMM2's third wait
+    auto prefetch = [&]() {
+      if (G == 0) {
+        const int64_t rn = min(roi + 16, a.R - 1);
+        const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
+        const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
+        asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
+        asm volatile("global_load_dword %0, %1, off" : "+v"(pf1) : "v"(pb) : "memory");
+      }
+    };
     if ((wave & 1) == 0) {
       rf_dw5q<0, 0>(Y, yb, wreg, o0);
       rf_dw5q<0, 1>(Y, yb, wreg, o1);
+      prefetch();
       rf_lds_barrier();
       rf_dw5q_store<0, 0>(Y, yb, o0);
       rf_dw5q_store<0, 1>(Y, yb, o1);
     } else {
       rf_dw5q<1, 0>(Y, yb, wreg, o0);
       rf_dw5q<1, 1>(Y, yb, wreg, o1);
+      prefetch();
       rf_lds_barrier();
       rf_dw5q_store<1, 0>(Y, yb, o0);
       rf_dw5q_store<1, 1>(Y, yb, o1);
@@ -1441,8 +1457,8 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
       for (int e = 0; e < 4; ++e) {
         sv[e] += lane_xor1(sv[e]);
         sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
-        sv[e] += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(sv[e]), 0x101F));          // ^4
-        sv[e] += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(sv[e]), 0x201F));          // ^8
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
       }
       if (fr == 0) {
         long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
@@ -1455,22 +1471,22 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     }
   }
   if (prof) pst[5] = eg_stamp();
-  rf_lds_barrier();  // every wave's GEMM2 reads of Y are done: stage the output over it
+  {
+    rf_lds_barrier();  // every wave's GEMM2 reads of Y are done: stage the output over it
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int px = i * 16 + fr;
-    if (px < RF_S) {
+    for (int i = 0; i < 7; ++i) {
+      const int px = i * 16 + fr;
+      if (px < RF_S) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const f4v v = acc[i][t];
-        *reinterpret_cast<uint2*>(Y + px * RF_OS + ((wave * 64 + t * 16 + fc * 4) >> 1)) =
-            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        for (int t = 0; t < 4; ++t) {
+          const f4v v = acc[i][t];
+          *reinterpret_cast<uint2*>(Y + px * RF_OS + ((wave * 64 + t * 16 + fc * 4) >> 1)) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
       }
     }
-  }
-  rf_lds_barrier();
-  if (prof) pst[6] = eg_stamp();
-  {
+    rf_lds_barrier();
+    if (prof) pst[6] = eg_stamp();
     const uint32_t* stg = Y;
     uint16_t* dst = a.XRN + r0 * 1024 + G * 512;
 #pragma unroll 4
@@ -1483,8 +1499,8 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pst[7] = eg_stamp();
-    if (tid == 0) {
-      unsigned long long* o = a.prof + lb * 8;
+    if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
+      unsigned long long* o = a.prof + (lb * 8 + wave) * 8;
       for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
       o[7] = pst[7] - pst[0];
     }

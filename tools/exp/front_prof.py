@@ -1,10 +1,14 @@
 """rmb_front phase cycles (s_memtime stamps of wave 0 per workgroup, trk_enc_set_prof):
-GEMM1, Y1 -> LDS, depthwise, GEMM2, activation + sums, output staging, stores, total."""
-import importlib, json, os, sys
+GEMM1, Y1 -> LDS, depthwise, GEMM2, activation + sums, output staging, stores, total;
+medians per DSC group (wave 0) and per wave (0 reinforce / SiLU, 1 normal / Hardswish) and isolated launch time,
+for each tuning variant given ("k=v;k=v", "" = defaults).
+usage: python tools/exp/front_prof.py [variant ...]"""
+import ctypes, importlib, json, os, statistics, sys
 import torch
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 ops = importlib.import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
-R = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+variants = sys.argv[1:] or [""]
+R = 2048
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
 X = torch.randn(R * 100, 512, device=dev, generator=g).bfloat16()
@@ -13,18 +17,43 @@ wdw = torch.randn(25, 1024, device=dev, generator=g) / 5
 W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, device=dev, generator=g) / 24).bfloat16())
 b2 = torch.randn(1024, device=dev, generator=g) / 10
 L = ops.lib()
-buf = torch.zeros(2 * R * 8, dtype=torch.int64, device=dev)
-for _ in range(3):
-    ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-import ctypes
 L.trk_enc_set_prof.argtypes = [ctypes.c_void_p]
-L.trk_enc_set_prof(ctypes.c_void_p(buf.data_ptr()))
-ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-torch.cuda.synchronize()
-L.trk_enc_set_prof(None)
-p = buf.view(-1, 8).double().cpu()
+buf = torch.zeros(2 * R * 8 * 8, dtype=torch.int64, device=dev)
 names = ["gemm1", "y1_store", "depthwise", "gemm2", "act_sums", "staging", "stores", "total"]
-med = p.median(0).values.tolist()
-print(json.dumps({n: round(v) for n, v in zip(names, med)}), flush=True)
-# s_memtime counts at 100 MHz on gfx950? report the ratio to the total
-print(json.dumps({n: round(v / med[-1], 3) for n, v in zip(names, med)}), flush=True)
+
+
+def apply(v, reset=False):
+    for kv in filter(None, v.split(";")):
+        k, x = kv.split("=")
+        L.trk_set_tuning(k.encode(), 0 if reset else int(x))
+
+
+ref = None
+for v in variants:
+    apply(v)
+    out = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = out
+    same = torch.equal(out[0], ref[0])
+    L.trk_enc_set_prof(ctypes.c_void_p(buf.data_ptr()))
+    ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    torch.cuda.synchronize()
+    L.trk_enc_set_prof(None)
+    p = buf.view(R, 2, 8, 8).double().cpu()   # [roi][group][wave][phase]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(5):
+        ev[0].record()
+        for _ in range(5):
+            ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+        ev[1].record()
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]) * 200)
+    apply(v, reset=True)
+    print(json.dumps({"variant": v, "xrn_equal_first": same, "us": round(statistics.median(ts), 1),
+                      "g0": {n: round(x) for n, x in zip(names, p[:, 0, 0].median(0).values.tolist())},
+                      "g1": {n: round(x) for n, x in zip(names, p[:, 1, 0].median(0).values.tolist())}}), flush=True)
+    # per wave (group 0): median of each phase, and the spread of GEMM1 end times
+    print(json.dumps({"per_wave_g0": {n: [round(x) for x in p[:, 0, :, k].median(0).values.tolist()]
+                                      for k, n in enumerate(names)}}), flush=True)
