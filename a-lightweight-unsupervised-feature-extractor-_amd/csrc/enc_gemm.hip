@@ -1519,178 +1519,6 @@ __global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
   else rf_body<0>(a, lb, smem);
 }
 
-// ---------------------------------------------------------------------------
-// trans_front: the RMB transition (card.py:78 + :138-139: T = [x_f * s | x_n] . Wt^T + b,
-// SiLU, then only T's per-ROI column sums) for one 10x10 ROI per workgroup, with
-// rmb_front's machinery: 8 waves, wave w owns output channels 64 w .. + 63 for all 112
-// (padded) pixels, computed transposed (weights = A operand) from fragments pre-packed in
-// K-step order ([32 k steps][32 col tiles][64 lanes] x 16 B) and loaded two steps ahead
-// into VGPRs.  The ROI's XRN rows (K = 1024 = 32 blocks of 32 channels, 200 KB) do not fit
-// LDS at once: they arrive by LDS-DMA in four groups of 8 blocks into two alternating
-// 51 KB images (group g + 1 issued when group g starts, 8 K steps ahead).  The SE scale
-// is applied in LDS to groups 0 and 1 (the x_f columns) exactly as gemm4<TRANS> applies it
-// to its staged tiles (bf16(x * s)), so T is bit-identical; the epilogue is bias + SiLU
-// and the column sums (f32 lane sums, one int64 partial per ROI).  T is never stored.
-constexpr int TF_NK = 32;
-constexpr size_t TF_BUF = (size_t)8 * RF_KBS * 4;       // one 8-block group image (51,712 B)
-constexpr size_t TF_LDS = 2 * TF_BUF + 112 * 64;        // + row tile 6's reads past block 7 of image 1
-static_assert(TF_LDS <= 160 * 1024, "one trans_front workgroup per CU");
-
-// issue order: s pairs, group 0 (8 DMA ops), B(0), B(1); step kt issues group kt / 8 + 1 when
-// kt % 8 == 0 (8 ops), then B(kt + 2): ops issued after B(kt) when step kt starts
-constexpr int tf_vm_after_b(int kt) {
-  if (kt == 0) return 4;
-  if (kt == 1) return 8 + 4;
-  // + the four L2-prefetch loads issued at step 9 after B(11) (younger than B(10) and B(11))
-  return ((kt - 1) % 8 == 0 && (kt - 1) / 8 + 1 < 4 ? 8 : 0) + (kt + 1 < TF_NK ? 4 : 0) + (kt == 10 || kt == 11 ? 4 : 0);
-}
-static_assert(tf_vm_after_b(1) <= 15 && tf_vm_after_b(9) <= 15, "rf_vmwait immediates");
-
-struct TfArgs {
-  const uint16_t* XRN;  // [R * 100][1024] = [x_f | x_n]
-  const float* s;       // [R][512] SE scale of the x_f columns
-  const uint4* Wtp;     // [32][32][64] 16-B fragments of Wt [512][1024]
-  const float* bias;    // [512]
-  long long* sums;      // [R][kPart][512] int64 x 2^24: partial 0 = the ROI's sum of SiLU(T), the rest 0
-};
-
-__global__ void __launch_bounds__(512, 1) trans_front_kernel(TfArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t roi = xcd_remap(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fc = lane >> 4;
-  const int64_t r0 = roi * RF_S;
-  uint32_t* img[2] = {reinterpret_cast<uint32_t*>(smem), reinterpret_cast<uint32_t*>(smem + TF_BUF)};
-
-  // SE scale pairs for this thread's transform share (channel pair cp of a group's 256
-  // channels, both x_f groups), asm loads issued first so every later wait retires them
-  const int cp = tid & 127, rs = tid >> 7;
-  f2v sv[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(sv[g]) : "v"(a.s + roi * 512 + g * 256 + 2 * cp) : "memory");
-
-  // XRN -> group images: wave w's lanes < 50 move pieces 50 w + lane of every block
-  const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
-  const uint16_t* xsrc = a.XRN + (r0 + xr) * 1024 + (((xp & 3) ^ rf_sw(xr)) * 8);
-  auto issueX = [&](int grp) {
-    if (lane < 50) {
-      const uint16_t* xs = xsrc;
-      asm volatile("" : "+v"(xs));
-      uint32_t* dst = img[grp & 1] + 200 * wave;
-#pragma unroll
-      for (int b = 0; b < 8; ++b)
-        __builtin_amdgcn_global_load_lds(GPTR(xs + (8 * grp + b) * BK), LPTR(dst + b * RF_KBS), 16, 0, 0);
-    }
-  };
-  // bf16(x * s) in place on a landed x_f group: the thread's channel pair, rows rs + 4 j
-  auto scale_group = [&](int grp) {
-    uint32_t base = lds_addr(img[grp & 1]);
-    asm volatile("" : "+v"(base));  // per call: no address state hoisted into the K loop
-    const f2v s2 = sv[grp];
-    const int col = 2 * cp;  // column of the group's 256 (block col / 32)
-#pragma unroll 1
-    for (int j0 = 0; j0 < 25; j0 += 5) {  // five rows in flight per wait
-      uint32_t ad[5], v[5];
-#pragma unroll
-      for (int u = 0; u < 5; ++u) {
-        ad[u] = base + 4 * rf_yaddr(rs + 4 * (j0 + u), col);
-        asm volatile("ds_read_b32 %0, %1" : "=v"(v[u]) : "v"(ad[u]) : "memory");
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4])::"memory");
-#pragma unroll
-      for (int u = 0; u < 5; ++u) {
-        const uint32_t w = pack_bf16x2(__uint_as_float(v[u] << 16) * s2.x, __uint_as_float(v[u] & 0xffff0000u) * s2.y);
-        asm volatile("ds_write_b32 %0, %1" ::"v"(ad[u]), "v"(w) : "memory");
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-
-  const uint4* bp = a.Wtp + (size_t)(wave * 4) * 64 + lane;
-  u32x4 bq[3][4];
-  const int lterm = fr * 4 + (fc ^ rf_sw(fr));
-  const uint32_t img_a[2] = {lds_addr(img[0]) + lterm * 16, lds_addr(img[1]) + lterm * 16};
-  f4v acc[7][4];
-#pragma unroll
-  for (int i = 0; i < 7; ++i)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
-
-  issueX(0);
-  rf_loadB(bp, 0, bq[0]);
-  rf_loadB(bp, 1, bq[1]);
-  float4 bias4[4];
-  uint32_t pf[4] = {0u, 0u, 0u, 0u};  // L2 prefetch of the ROI that starts when this one ends
-#pragma clang loop unroll(full)  // every kt a constant: bq[kt % 3] must stay in registers
-  for (int kt = 0; kt < TF_NK; ++kt) {
-    u32x4(&b)[4] = bq[kt % 3];
-    rf_vmwait(kt % 8 == 0 ? 0 : tf_vm_after_b(kt), b);  // group boundary: vmcnt(0) (as rmb_front)
-    if (kt == 0) asm volatile("" : "+v"(sv[0]), "+v"(sv[1]));  // retired by the wait above
-    if (kt % 8 == 0) {
-      g4_barrier();  // group kt / 8 landed; the other image's last reads (group kt / 8 - 1) done
-      if (kt / 8 < 2) {  // x_f group: SE scale in place first (fewer registers live: B(kt + 2) not yet loaded)
-        scale_group(kt / 8);
-        g4_barrier();
-      }
-      if (kt / 8 + 1 < 4) issueX(kt / 8 + 1);
-    }
-    if (kt + 2 < TF_NK) rf_loadB(bp, kt + 2, bq[(kt + 2) % 3]);
-    if (kt == 9) {
-      // XRN rows of ROI + 32 (the XCD's 32 CUs hold 32 ROIs at a time): 1600 128-B lines,
-      // four 4-B loads per thread, issued after B(11); retired by step 16's vmcnt(0)
-      const int64_t rn = min(roi + 32, (int64_t)gridDim.x - 1);
-      const uint16_t* pb = a.XRN + rn * RF_S * 1024;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        asm volatile("global_load_dword %0, %1, off" : "+v"(pf[u]) : "v"(pb + (int64_t)min(tid + 512 * u, 1599) * 64)
-                     : "memory");
-    }
-    if (kt == 16) asm volatile("" : "+v"(pf[0]), "+v"(pf[1]), "+v"(pf[2]), "+v"(pf[3]));  // retired by step 16's wait
-    if (kt == TF_NK - 2) {  // B(kt + 2) is no longer loaded: its buffer's registers hold the bias
-#pragma unroll
-      for (int t = 0; t < 4; ++t) bias4[t] = *reinterpret_cast<const float4*>(a.bias + wave * 64 + t * 16 + fc * 4);
-    }
-    uint32_t ab = img_a[(kt / 8) & 1];
-    asm volatile("" : "+v"(ab));  // per step: the 32 step addresses are not all hoisted
-    rf_mfma_step(ab + (kt % 8) * RF_KBS * 4, b, acc);
-  }
-
-  // bias + SiLU, column sums over the 100 pixels (row tile 6: fr < 4), one partial per ROI
-  const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
-    float sm[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f2v v = silu2(f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01));
-        if (i < 6 || fr < 4) {
-          sm[2 * h] += v.x;
-          sm[2 * h + 1] += v.y;
-        }
-      }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      sm[e] += lane_xor1(sm[e]);
-      sm[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sm[e]), 0x4E, 0xF, 0xF, true));   // ^2
-      sm[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sm[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
-      sm[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sm[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
-    }
-    if (fr == 0) {
-      long long* o = a.sums + roi * kPart * 512 + wave * 64 + t * 16 + fc * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = llrintf(sm[e] * kFix);
-      for (int j = 1; j < cnt; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[j * 512 + e] = 0;
-    }
-  }
-}
-
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
@@ -1828,31 +1656,6 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
     hipLaunchKernelGGL(g1dw4_kernel<false>, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
                        (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
   return trk::check_launch("g1dw4_kernel");
-}
-
-extern "C" int trk_enc_transition_roi(const void* XRN, int64_t M, const float* s, const void* Wtp, const float* bias,
-                                      long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_transition_roi: 10x10 ROIs (M %% 100 == 0), K = 1024, N = 512");
-  if (M == 0) return TRK_OK;
-  TRK_REQUIRE(XRN && s && Wtp && bias && sums && aligned16(XRN) && aligned16(Wtp) && aligned16(bias) &&
-                  ((uintptr_t)s & 7) == 0,
-              "enc_transition_roi: null or unaligned pointer");
-  TRK_REQUIRE(M / RF_S < 0x7fffffff, "enc_transition_roi: too many workgroups");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(trans_front_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)TF_LDS);
-    attr = true;
-  }
-  TfArgs a;
-  a.XRN = (const uint16_t*)XRN;
-  a.s = s;
-  a.Wtp = (const uint4*)Wtp;
-  a.bias = bias;
-  a.sums = sums;
-  hipLaunchKernelGGL(trans_front_kernel, dim3((unsigned)(M / RF_S)), dim3(512), TF_LDS,
-                     reinterpret_cast<hipStream_t>(stream), a);
-  return trk::check_launch("trans_front_kernel");
 }
 
 extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,

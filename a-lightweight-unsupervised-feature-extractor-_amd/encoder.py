@@ -171,9 +171,6 @@ class Model(nn.Module):
                 w["w2_pk"] = enc_pack_fragments(w["w2_nk"])
             w["b2"] = torch.cat([w["br"].float(), w["bn"].float()]).to(device, torch.float32)
             w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
-            if tuple(w["wt_nk"].shape) == (512, 1024):
-                from .ops import enc_pack_fragments_nk                               # transition_roi operand
-                w["wt_pk"] = enc_pack_fragments_nk(w["wt_nk"])
             w["bt_f"] = r.transition[0].bias.float().to(device)
             w["bt"] = r.transition[0].bias.to(device, dtype)
             # f32 operands of the per-ROI tail kernels (enc_se / enc_head)
@@ -222,8 +219,6 @@ class Model(nn.Module):
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
     fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel
                          # (enc_rmb_front; Y2 never reaches HBM); False: enc_g1_dwconv + enc_dsc_gemm
-    fused_trans = False  # with fused_front: the transition one ROI per workgroup (enc_transition_roi);
-                         # equal to gemm4<TRANS> in isolation (283.6 vs 284.6 us), so off by default
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
     stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
@@ -232,7 +227,7 @@ class Model(nn.Module):
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_rmb_front, enc_transition_roi, enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
+                          enc_rmb_front, enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -270,10 +265,7 @@ class Model(nn.Module):
             if self.fused_tail:
                 # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
                 m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
-                if front and self.fused_trans and "wt_pk" in W:
-                    tsums = enc_transition_roi(XRN, s, W["wt_pk"], W["bt_f"])  # one ROI per workgroup
-                else:
-                    tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
+                tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
                 head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                         self.head.net[1].eps, W["h4"], W["h4b"])
                 if not self.defer_head:

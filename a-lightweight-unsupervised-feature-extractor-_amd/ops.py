@@ -216,35 +216,6 @@ def enc_rmb_front(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: to
     return XRN, sums
 
 
-def enc_pack_fragments_nk(W: torch.Tensor) -> torch.Tensor:
-    """[N, K] bf16 weights -> the 16x16x32 MFMA fragment order trk_enc_transition_roi reads:
-    [K/32 k steps][N/16 col tiles][64 lanes][8], element (s, n, l, j) = W[16n + l%16][32s + 8(l//16) + j]."""
-    N, K = W.shape
-    return W.reshape(N // 16, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).contiguous()
-
-
-def enc_transition_roi(XRN: torch.Tensor, s: torch.Tensor, Wtp: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-    """bf16, 10x10 ROIs: the transition (one ROI per workgroup): raw int64 sums [R, TRK_ENC_PARTS,
-    512] of SiLU([x_f * s | x_n] . Wt^T + bias) over each ROI's 100 rows (== enc_transition_gemm(raw=True)
-    up to the f32 summation order).  XRN [R*100, 1024], s [R, 512] f32, Wtp = enc_pack_fragments_nk(Wt)."""
-    _need_gpu(XRN, "enc_transition_roi")
-    if XRN.dtype != torch.bfloat16 or Wtp.dtype != torch.bfloat16:
-        raise TypeError("enc_transition_roi: bf16 operands required")
-    if XRN.dim() != 2 or not XRN.is_contiguous() or XRN.shape[1] != 1024 or XRN.shape[0] % 100:
-        raise ValueError("enc_transition_roi: XRN must be contiguous [R*100, 1024]")
-    R = XRN.shape[0] // 100
-    if Wtp.numel() != 512 * 1024 or not Wtp.is_contiguous() or bias.numel() != 512:
-        raise ValueError("enc_transition_roi: Wtp [32, 32, 4, 16, 8] fragments and bias [512] required")
-    s = s.to(torch.float32).contiguous()
-    if s.shape != (R, 512):
-        raise ValueError("enc_transition_roi: s must be [R, 512]")
-    sums = torch.empty((R, _lib.TRK_ENC_PARTS, 512), device=XRN.device, dtype=torch.int64)
-    check(lib().trk_enc_transition_roi(_ptr(XRN), XRN.shape[0], _ptr(s), _ptr(Wtp),
-                                       _ptr(bias.to(torch.float32).contiguous()), _ptr(sums),
-                                       _stream(XRN.device)), "enc_transition_roi")
-    return sums
-
-
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
                         bias: torch.Tensor, raw: bool = False) -> torch.Tensor:
     """sum over each ROI's P rows of SiLU([x_f * s | x_n] . Wt^T + bias):

@@ -334,7 +334,7 @@ class LiveProbe:
 
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_nchw_to_nhwc": "map_nhwc", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
-             "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_transition_roi": "enc_trans_roi",
+             "trk_enc_rmb_front": "enc_rmb_front",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
              "trk_step_begin": "step_begin", "trk_step_mid": "step_mid", "trk_step_end": "step_end",
@@ -440,8 +440,6 @@ def kernel_pass(pipe, f, reps=10):
     with torch.no_grad():
         s_se = m._se(sum_r / 100)
     timed("enc_gemm_trans", lambda: ops.enc_transition_gemm(XRN, 100, s_se, W["wt_nk"], W["bt_f"]))
-    if "wt_pk" in W:
-        timed("enc_trans_roi", lambda: ops.enc_transition_roi(XRN, s_se, W["wt_pk"], W["bt_f"]))
     timed("encoder", lambda: pipe.stage_embed(roi))
     emb = pipe.stage_embed(roi)
     # tracker kernels on the current track table (rows = all live tracks)
@@ -620,8 +618,6 @@ def main():
     # TRK_FRONT=0: the two-kernel encoder front (g1dw4 -> Y2 in HBM -> gemm4<DSC>) instead of
     # rmb_front (one kernel, Y2 in LDS)
     model.fused_front = os.environ.get("TRK_FRONT", "1") == "1"
-    # TRK_TRANS=1: the transition one ROI per workgroup (trans_front) instead of gemm4 (128 x 256 tiles)
-    model.fused_trans = os.environ.get("TRK_TRANS", "0") == "1"
 
     # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
     # the syncs around the timed region make it do exactly `steps` embeddings (those of
@@ -673,7 +669,6 @@ def main():
         "enc_gemm_dsc": (R * 1024 * 2 * 2 + 2 * 512 * 512 * 2 + K * 1024 * 8, 2.0 * R * 1024 * 512,
                          BF16_PEAK_TFLOPS),
         "enc_gemm_trans": (R * 1024 * 2 + 512 * 1024 * 2 + K * 512 * 12, 2.0 * R * 512 * 1024, BF16_PEAK_TFLOPS),
-        "enc_trans_roi": (R * 1024 * 2 + 512 * 1024 * 2 + K * 512 * 12, 2.0 * R * 512 * 1024, BF16_PEAK_TFLOPS),
         # first 1x1 convs + depthwise + both DSC GEMMs in one kernel: X in, XRN + sums out
         "enc_rmb_front": (R * 512 * 2 + R * 1024 * 2 + 2 * 1024 * 512 * 2 + 25 * 1024 * 4 + K * 1024 * 8,
                           2.0 * R * 1024 * 512 * 2 + 2.0 * R * 1024 * 25, BF16_PEAK_TFLOPS),
@@ -683,10 +678,8 @@ def main():
     # the encoder path not taken in the timed region is still timed isolated (kernel_pass);
     # the dominant kernel is chosen among the ones the timed region ran
     front = pipe.model.fused_front and "enc_rmb_front" in kt
-    troi = front and pipe.model.fused_trans and "enc_trans_roi" in kt
     ran = {k for k in algo if k in kt and (k not in ("enc_g1_dwconv", "enc_gemm_dsc") or not front)
-           and (k != "enc_rmb_front" or front) and (k != "enc_gemm_trans" or not troi)
-           and (k != "enc_trans_roi" or troi)}
+           and (k != "enc_rmb_front" or front)}
     per = {}
     for k, (byt, fl, mpeak) in algo.items():
         if k not in kt:

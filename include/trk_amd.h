@@ -250,16 +250,6 @@ int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wd
                       const float* bias, void* XRN, long long* sums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
-/* trk_enc_transition_roi: trk_enc_transition_gemm for 10x10 ROIs of K = 1024, N = 512,
- *   kscale = 512 with one ROI per workgroup (card.py:78, :138-139): the ROI's XRN rows
- *   staged in LDS in four groups, bf16(x_f * s) applied in LDS, T = . Wt^T + bias never
- *   stored; sums [R][TRK_ENC_PARTS][512] of SiLU(T) hold the ROI's whole sum in partial 0
- *   and 0 in its other partials.  Wtp = Wt [512][1024] in fragment order [32 k steps][32
- *   col tiles][64 lanes][8] bf16, element (s, n, l, j) = Wt[16n + l%16][32s + 8(l/16) + j]
- *   (trk.ops.enc_pack_fragments_nk).  s [R][512] f32 (8-B aligned), bias [512] f32. */
-int trk_enc_transition_roi(const void* XRN, int64_t M, const float* s, const void* Wtp, const float* bias,
-                           long long* sums, void* stream);
-
 /* Per-ROI tail of the encoder (f32, 16 ROIs per workgroup, f32-input MFMA).
  * trk_enc_se: squeeze means and SE excitation (card.py:59-78) from the partial
  *   sums of trk_enc_dsc_gemm ([R][TRK_ENC_PARTS][ld_sums], ld_sums >= 2C: C sums

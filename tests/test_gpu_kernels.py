@@ -654,28 +654,6 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R):
     assert torch.equal(XRN1, XRN1b) and torch.equal(ops.enc_sums_reduce(s1b, P), f1)
 
 
-@pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_transition_roi_vs_gemm4(trk, gpu, R):
-    """trk_enc_transition_roi (one ROI per workgroup, XRN staged in LDS, SE scale applied in
-    LDS) vs trk_enc_transition_gemm: the same bf16(x_f * s) operand and K order, so T is the
-    same; the SiLU column sums are added in another order (tol 1e-5 of the largest sum)."""
-    from importlib import import_module
-    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
-    g = torch.Generator().manual_seed(R + 1)
-    M, P = R * 100, 100
-    XRN = torch.randn(M, 1024, generator=g).to(gpu).bfloat16()
-    s = torch.rand(R, 512, generator=g).to(gpu)
-    Wt = (torch.randn(512, 1024, generator=g) / 32).to(gpu).bfloat16()
-    bt = (torch.randn(512, generator=g) / 4).to(gpu)
-    ref = ops.enc_sums_reduce(ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True), P)
-    Wtp = ops.enc_pack_fragments_nk(Wt)
-    assert Wtp[3, 5, 2, 7, 4].item() == Wt[16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
-    got = ops.enc_sums_reduce(ops.enc_transition_roi(XRN, s, Wtp, bt), P)
-    assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-    again = ops.enc_sums_reduce(ops.enc_transition_roi(XRN, s, Wtp, bt), P)
-    assert torch.equal(got, again)
-
-
 def _partials(total, P, parts=3):
     """split int64 per-ROI totals [R, ld] into the GEMMs' partial layout
     [R, parts, ld] (one entry per 128-row tile covering the ROI; the rest junk)"""

@@ -10,5 +10,5 @@ for cfg in "$@"; do
   grep '^{' "$OUT/ab_$i.log" | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read()); r=d['roofline']
-print('$cfg', d['value'], d['ms_per_step'], d['identity_rate'], {k: round(v) for k, v in r['kernel_us'].items() if k in ('cost','lsap','enc_g1_dwconv','enc_gemm_dsc','enc_gemm_trans','enc_rmb_front','enc_trans_roi','roi_stage')})"
+print('$cfg', d['value'], d['ms_per_step'], d['identity_rate'], {k: round(v) for k, v in r['kernel_us'].items() if k in ('cost','lsap','enc_g1_dwconv','enc_gemm_dsc','enc_gemm_trans','enc_rmb_front','roi_stage')})"
 done
