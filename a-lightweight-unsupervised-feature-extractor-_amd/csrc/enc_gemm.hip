@@ -39,6 +39,8 @@ int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the
 int g_enc_lds_tight = 1;  // trk_set_tuning("enc_lds_tight"): gemm4 launched with the LDS its tile uses (1) or 80 KiB
 int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column sums on the MFMA (DSC
                      // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
+int g_rf_pf = 1;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + 16 (GEMM1
+                  // 19.2K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
@@ -1142,6 +1144,7 @@ struct RfArgs {
   uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
   long long* sums;      // [R][kPart][1024] int64 x 2^24: partial 0 = the ROI's sum, the rest 0
   int64_t R;            // ROIs
+  int pf;               // trk_set_tuning("rf_pf"): L2 prefetch of ROI + 16's X rows (1) or none (0)
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
 };
 
@@ -1364,7 +1367,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
 
   // ---- depthwise 5x5 in place: wave = (128-channel group, output half); both quadrants
   // of the half are computed before anyone overwrites Y1
-  constexpr int NPF = G == 0 ? 2 : 0;
+  const int NPF = (G == 0 && a.pf) ? 2 : 0;
   uint32_t pf0 = 0, pf1 = 0;
   {
     const int kb0 = cg * 4 + (lane >> 4), c0 = (lane & 15) >> 2, d0 = lane & 3;
@@ -1376,7 +1379,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     // then hits L2.  Two 4-B loads per thread = the ROI's 800 128-B lines; retired by
     // GEMM2's third wait
     auto prefetch = [&]() {
-      if (G == 0) {
+      if (G == 0 && a.pf) {
         const int64_t rn = min(roi + 16, a.R - 1);
         const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
         const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
@@ -1682,6 +1685,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.XRN = (uint16_t*)XRN;
   a.sums = sums;
   a.R = M / RF_S;
+  a.pf = g_rf_pf;
   a.prof = g_enc_prof;
   hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
                      a);
