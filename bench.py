@@ -149,7 +149,12 @@ class Pipeline:
         # TRK_ROI_AFTER=g1|dsc: frame f+1's ROI Align waits for frame f's first GEMM / DSC GEMM
         # (an event recorded through encoder.Model.stage_hook), so it runs beside the
         # encoder's later kernels instead of as soon as it is enqueued
-        self.roi_after = os.environ.get("TRK_ROI_AFTER", "") if self.roi_stream is not None else ""
+        # Default "dsc" since rmb_front (r03): rmb_front fills a CU's VGPRs (two 248-register
+        # waves per SIMD), so a ROI Align running beside it only gets CUs between its
+        # workgroups; gated behind it, it runs beside the transition GEMM instead (1.910 /
+        # 1.917M vs 1.887 / 1.882M ROIs/s ungated, 1.801 / 1.807M on the embedding stream;
+        # rmb_front live 657 vs 741 us)
+        self.roi_after = os.environ.get("TRK_ROI_AFTER", "dsc") if self.roi_stream is not None else ""
         self.roi_gate = None
         if self.roi_after:
             def hook(name):
