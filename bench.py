@@ -396,15 +396,20 @@ class LiveProbe:
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for v in self.ev.values() for a, b in v) * 1e3 / max(steps, 1)
 
-    def embed_gaps_us(self, n_side=1, head_deferred=False):
+    def embed_gaps_us(self, n_side=1, head_deferred=False, roi_own_stream=False):
         """mean time between one frame's last launch on the embedding stream ending
         (enc_head, or the transition GEMM when the head is deferred to the tracker's
-        stream) and the next frame's roi stage starting on it: the embedding stream's
+        stream) and the next frame's first launch on it starting (the roi stage, or the
+        encoder front when ROI Align has a stream of its own): the embedding stream's
         idle time per frame (None with several embedding streams: frames then overlap
         on purpose)"""
         if n_side != 1:
             return None
-        ends, starts = self.ev["enc_gemm_trans" if head_deferred else "enc_head"], self.ev["roi_stage"]
+        ends = self.ev["enc_gemm_trans" if head_deferred else "enc_head"]
+        first = "roi_stage"
+        if roi_own_stream:
+            first = "enc_rmb_front" if self.ev.get("enc_rmb_front") else "enc_g1_dwconv"
+        starts = self.ev[first]
         gaps = [e1.elapsed_time(s0) * 1e3 for (_, e1), (s0, _) in zip(ends, starts[1:])]
         return float(np.mean(gaps)) if gaps else None
 
@@ -646,7 +651,7 @@ def main():
     kernel_sum = probe.sum_per_step_us(args.steps)
     live = probe.means_us()
     live = {k: v for k, v in live.items() if not k.endswith("_live")}
-    side_gap = probe.embed_gaps_us(len(pipe.sides), pipe.defer_head)
+    side_gap = probe.embed_gaps_us(len(pipe.sides), pipe.defer_head, pipe.roi_stream is not None)
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
