@@ -22,10 +22,35 @@ buf = torch.zeros(2 * R * 8 * 8, dtype=torch.int64, device=dev)
 names = ["gemm1", "y1_store", "depthwise", "gemm2", "act_sums", "staging", "stores", "total"]
 
 
+DEFAULTS = {"rf_pf": 1}  # knobs whose default is not 0
+
+
 def apply(v, reset=False):
     for kv in filter(None, v.split(";")):
         k, x = kv.split("=")
-        L.trk_set_tuning(k.encode(), 0 if reset else int(x))
+        rc = L.trk_set_tuning(k.encode(), DEFAULTS.get(k, 0) if reset else int(x))
+        assert rc == 0, (k, x, reset)
+
+
+def launch_us(v):
+    apply(v)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(5):
+        ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    ev[1].record()
+    torch.cuda.synchronize()
+    apply(v, reset=True)
+    return ev[0].elapsed_time(ev[1]) * 200
+
+
+for v in variants:  # warm every variant once
+    launch_us(v)
+# interleaved timing rounds: launch-time drift hits every variant alike
+times = {v: [] for v in variants}
+for _ in range(7):
+    for v in variants:
+        times[v].append(launch_us(v))
 
 
 ref = None
@@ -41,16 +66,8 @@ for v in variants:
     torch.cuda.synchronize()
     L.trk_enc_set_prof(None)
     p = buf.view(R, 2, 8, 8).double().cpu()   # [roi][group][wave][phase]
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ts = []
-    for _ in range(5):
-        ev[0].record()
-        for _ in range(5):
-            ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-        ev[1].record()
-        torch.cuda.synchronize()
-        ts.append(ev[0].elapsed_time(ev[1]) * 200)
     apply(v, reset=True)
+    ts = times[v]
     print(json.dumps({"variant": v, "xrn_equal_first": same, "us": round(statistics.median(ts), 1),
                       "g0": {n: round(x) for n, x in zip(names, p[:, 0, 0].median(0).values.tolist())},
                       "g1": {n: round(x) for n, x in zip(names, p[:, 1, 0].median(0).values.tolist())}}), flush=True)
