@@ -39,8 +39,8 @@ int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the
 int g_enc_lds_tight = 1;  // trk_set_tuning("enc_lds_tight"): gemm4 launched with the LDS its tile uses (1) or 80 KiB
 int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column sums on the MFMA (DSC
                      // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
-int g_rf_pf = 1;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + 16 (GEMM1
-                  // 19.2K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
+int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + rf_pf, 0: none (GEMM1
+                  // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
@@ -1374,13 +1374,14 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
     const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
                        kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
     uint32_t o0[25], o1[25];
-    // L2 prefetch (reinforce workgroups) of the X rows of ROI + 16: the XCD's 32 CUs run
-    // 16 ROIs at a time, so that ROI starts about when this one ends; its first DMA group
-    // then hits L2.  Two 4-B loads per thread = the ROI's 800 128-B lines; retired by
-    // GEMM2's third wait
+    // L2 prefetch (reinforce workgroups) of the X rows of ROI + a.pf (default 8): the XCD's
+    // 32 CUs run 16 ROIs at a time, so that ROI starts about half a workgroup lifetime after
+    // this point, early enough for its first DMA group to find the rows near (16 ahead: the
+    // rows leave L2 first, 701 vs 662 MB fetched per launch, pipeline 0.6-0.9 % slower).
+    // Two 4-B loads per thread = the ROI's 800 128-B lines; retired by GEMM2's third wait
     auto prefetch = [&]() {
       if (G == 0 && a.pf) {
-        const int64_t rn = min(roi + 16, a.R - 1);
+        const int64_t rn = min(roi + a.pf, a.R - 1);
         const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
         const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
         asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");

@@ -58,8 +58,8 @@ const char* trk_last_error(void);
  *                    relative of the lane-reduction sums, 0)
  *   "g1dw"           6 (default): fused first GEMM + depthwise with the next round's rows
  *                    prefetched into L2; 4: without the prefetch
- *   "rf_pf"          1 (default): trk_enc_rmb_front prefetches the X rows of ROI + 16 into L2;
- *                    0: no prefetch
+ *   "rf_pf"          8 (default): trk_enc_rmb_front prefetches the X rows of ROI + rf_pf into
+ *                    L2 (0..64; 0: no prefetch)
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
  *                    given (the device tracker), else the detection-tile kernel; 1: the
