@@ -36,6 +36,7 @@ constexpr int kMaxTopk = 8;
 constexpr int kRowsPerWave = 4;
 constexpr int kWavesPerWG = 4;
 constexpr int kRowsPerWG = kRowsPerWave * kWavesPerWG;
+constexpr int kCost3Rows = 256;  // cost3 rows per frame in one pass of its grid (one wave each)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -469,108 +470,112 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // track terms below: scalar loads
   const int M = A.dev_M ? min(A.dev_M[f], A.Mmax) : A.M[f];
   const int N = A.dev_N ? min(A.dev_N[f], A.Nmax) : A.N[f];
-  const int i = blockIdx.x * 4 + wave;
-  if (i >= M || N == 0) return;  // no barriers below
-  const int col = lane & 31, h = lane >> 5;
-  const int64_t slot = A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.rs_ld + i] : (int64_t)f * A.Mmax + i;
-  const int T = min(A.bank_len[slot], A.Tmax);
-  unsigned long long p0 = 0, p1 = 0, pc = 0, pe = 0, pt = 0;
-  if (w.prof) p0 = c3_stamp();
-  float a[64];
-  load_a_frag(A.bank + (slot * A.Tmax + col) * D + 64 * h, col < T, a);
-  if (w.prof) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    p1 = pt = c3_stamp();
-  }
-  const int topk = A.p.topk;
-  const bool gate = A.p.gate && A.gate_on[slot];
-  // the track's box / conf / gate terms, hoisted out of the tile loop into scalar
-  // registers (wave-uniform; readfirstlane tells the compiler so)
-  auto uni_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-  auto uni_d = [](double v) {
-    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-  };
-  float tb[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) tb[q] = uni_f(A.pbox[slot * 4 + q]);
-  const float tconf = uni_f(A.conf_prev[slot]);
-  double tg[4] = {0.0, 0.0, 0.0, 0.0}, tS[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) tS[q] = 0.0;
-  if (gate) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tg[q] = uni_d(A.gmean[slot * 4 + q]);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tS[q] = uni_d(A.gsinv[slot * 16 + q]);
-  }
-  const float* dnf = w.dn + (int64_t)f * A.Nmax * D;
-  const DetTerms* dtf = w.dt + (int64_t)f * A.Nmax;
-  float* Ct = A.C_total ? A.C_total + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
-  float* Ca = A.C_app ? A.C_app + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
-  // one 32-detection tile, straight-line: the tile's detection terms are loaded first,
-  // then the next tile's B fragments (into the other buffer), then the MFMA chain, so
-  // the epilogue's wait for the terms leaves the prefetch in flight
-  auto tile = [&](int j0, const float (&b)[64], float (&bn)[64]) {
-    const int j = j0 + col;
-    const DetTerms t = dtf[min(j, N - 1)];
-    load_b_tile(dnf, j + 32, N, h, bn);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
-    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
-    float tk[kMaxTopk];
-#pragma unroll
-    for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
-    bool nan = false;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float x = tr < T ? acc[r] : -INFINITY;
-      nan |= __builtin_isnan(x);
-      topk_insert_k<KT>(tk, x);
-    }
-    float other[KT];
-#pragma unroll
-    for (int q = 0; q < KT; ++q) other[q] = __shfl_xor(tk[q], 32);
-#pragma unroll
-    for (int q = 0; q < KT; ++q) topk_insert_k<KT>(tk, other[q]);
-    const int k = min(topk, T);
-    float sum = 0.f;
-#pragma unroll
-    for (int q = 0; q < KT; ++q)
-      if (q < k) sum = sum + tk[q];
-    const float app = app_nan(k <= 0 ? 1.0f : 1.0f - sum / (float)k, nan && k > 0, col);
+  if (N == 0) return;  // no barriers below
+  // grid-stride over the frame's rows: the grid is sized for the usual count (kCost3Rows),
+  // not the launch's bound (live tracks + detections in flight), so a bound 4x the live
+  // count costs no idle waves; a frame with more rows than the grid loops
+  for (int i = blockIdx.x * 4 + wave; i < M; i += gridDim.x * 4) {
+    const int col = lane & 31, h = lane >> 5;
+    const int64_t slot = A.row_slot ? (int64_t)A.row_slot[(int64_t)f * A.rs_ld + i] : (int64_t)f * A.Mmax + i;
+    const int T = min(A.bank_len[slot], A.Tmax);
+    unsigned long long p0 = 0, p1 = 0, pc = 0, pe = 0, pt = 0;
+    if (w.prof) p0 = c3_stamp();
+    float a[64];
+    load_a_frag(A.bank + (slot * A.Tmax + col) * D + 64 * h, col < T, a);
     if (w.prof) {
-      asm volatile("" ::"v"(app));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      p1 = pt = c3_stamp();
+    }
+    const int topk = A.p.topk;
+    const bool gate = A.p.gate && A.gate_on[slot];
+    // the track's box / conf / gate terms, hoisted out of the tile loop into scalar
+    // registers (wave-uniform; readfirstlane tells the compiler so)
+    auto uni_f = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    auto uni_d = [](double v) {
+      const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+      const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+      const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+      return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    };
+    float tb[4];
+  #pragma unroll
+    for (int q = 0; q < 4; ++q) tb[q] = uni_f(A.pbox[slot * 4 + q]);
+    const float tconf = uni_f(A.conf_prev[slot]);
+    double tg[4] = {0.0, 0.0, 0.0, 0.0}, tS[16];
+  #pragma unroll
+    for (int q = 0; q < 16; ++q) tS[q] = 0.0;
+    if (gate) {
+  #pragma unroll
+      for (int q = 0; q < 4; ++q) tg[q] = uni_d(A.gmean[slot * 4 + q]);
+  #pragma unroll
+      for (int q = 0; q < 16; ++q) tS[q] = uni_d(A.gsinv[slot * 16 + q]);
+    }
+    const float* dnf = w.dn + (int64_t)f * A.Nmax * D;
+    const DetTerms* dtf = w.dt + (int64_t)f * A.Nmax;
+    float* Ct = A.C_total ? A.C_total + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
+    float* Ca = A.C_app ? A.C_app + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
+    // one 32-detection tile, straight-line: the tile's detection terms are loaded first,
+    // then the next tile's B fragments (into the other buffer), then the MFMA chain, so
+    // the epilogue's wait for the terms leaves the prefetch in flight
+    auto tile = [&](int j0, const float (&b)[64], float (&bn)[64]) {
+      const int j = j0 + col;
+      const DetTerms t = dtf[min(j, N - 1)];
+      load_b_tile(dnf, j + 32, N, h, bn);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
+      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+      float tk[kMaxTopk];
+  #pragma unroll
+      for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
+      bool nan = false;
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float x = tr < T ? acc[r] : -INFINITY;
+        nan |= __builtin_isnan(x);
+        topk_insert_k<KT>(tk, x);
+      }
+      float other[KT];
+  #pragma unroll
+      for (int q = 0; q < KT; ++q) other[q] = __shfl_xor(tk[q], 32);
+  #pragma unroll
+      for (int q = 0; q < KT; ++q) topk_insert_k<KT>(tk, other[q]);
+      const int k = min(topk, T);
+      float sum = 0.f;
+  #pragma unroll
+      for (int q = 0; q < KT; ++q)
+        if (q < k) sum = sum + tk[q];
+      const float app = app_nan(k <= 0 ? 1.0f : 1.0f - sum / (float)k, nan && k > 0, col);
+      if (w.prof) {
+        asm volatile("" ::"v"(app));
+        const unsigned long long t1 = c3_stamp();
+        pc += t1 - pt;
+        pt = t1;
+      }
+      float cen, scl, cf;
+      const float tot = combine(A.p, app, tb, tconf, t.ccx, t.ccy, t.Ac, t.ccv, gate, tg, tS, t.z0, t.z1, t.z2, t.z3,
+                                cen, scl, cf);
+      if (h == 0 && j < N) {
+        if (Ct) Ct[j] = tot;
+        if (Ca) Ca[j] = app;
+      }
+    };
+    float b0[64], b1[64];
+    load_b_tile(dnf, col, N, h, b0);
+    for (int j0 = 0; j0 < N; j0 += 64) {
+      tile(j0, b0, b1);
+      if (j0 + 32 >= N) break;
+      tile(j0 + 32, b1, b0);
+    }
+    if (w.prof) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned long long t1 = c3_stamp();
-      pc += t1 - pt;
-      pt = t1;
-    }
-    float cen, scl, cf;
-    const float tot = combine(A.p, app, tb, tconf, t.ccx, t.ccy, t.Ac, t.ccv, gate, tg, tS, t.z0, t.z1, t.z2, t.z3,
-                              cen, scl, cf);
-    if (h == 0 && j < N) {
-      if (Ct) Ct[j] = tot;
-      if (Ca) Ca[j] = app;
-    }
-  };
-  float b0[64], b1[64];
-  load_b_tile(dnf, col, N, h, b0);
-  for (int j0 = 0; j0 < N; j0 += 64) {
-    tile(j0, b0, b1);
-    if (j0 + 32 >= N) break;
-    tile(j0 + 32, b1, b0);
-  }
-  if (w.prof) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long t1 = c3_stamp();
-    pe = t1 - p1 - pc;
-    if (lane == 0) {
-      unsigned long long* o = w.prof + ((int64_t)(f * gridDim.x + blockIdx.x) * 4 + wave) * 4;
-      o[0] = p0; o[1] = p1 - p0; o[2] = pc; o[3] = pe;
+      pe = t1 - p1 - pc;
+      if (lane == 0) {
+        unsigned long long* o = w.prof + ((int64_t)(f * gridDim.x + blockIdx.x) * 4 + wave) * 4;
+        o[0] = p0; o[1] = p1 - p0; o[2] = pc; o[3] = pe;
+      }
     }
   }
 }
@@ -747,10 +752,11 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
       w.dt += f0 * Nmax;
       hipLaunchKernelGGL(det_prep_kernel, dim3((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf), dim3(256), 0, st, a, w);
       if (int e = trk::check_launch("det_prep_kernel")) return e;
+      const unsigned c3x = (unsigned)std::min<int64_t>((Mmax + 3) / 4, kCost3Rows / 4);
       if (host_params->topk <= 5)
-        hipLaunchKernelGGL(cost3_kernel<5>, dim3((unsigned)((Mmax + 3) / 4), (unsigned)nf), dim3(256), 0, st, a, w);
+        hipLaunchKernelGGL(cost3_kernel<5>, dim3(c3x, (unsigned)nf), dim3(256), 0, st, a, w);
       else
-        hipLaunchKernelGGL(cost3_kernel<kMaxTopk>, dim3((unsigned)((Mmax + 3) / 4), (unsigned)nf), dim3(256), 0, st, a, w);
+        hipLaunchKernelGGL(cost3_kernel<kMaxTopk>, dim3(c3x, (unsigned)nf), dim3(256), 0, st, a, w);
       if (int e = trk::check_launch("cost3_kernel")) return e;
       continue;
     }

@@ -1144,7 +1144,7 @@ struct RfArgs {
   uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
   long long* sums;      // [R][kPart][1024] int64 x 2^24: partial 0 = the ROI's sum, the rest 0
   int64_t R;            // ROIs
-  int pf;               // trk_set_tuning("rf_pf"): L2 prefetch of ROI + 16's X rows (1) or none (0)
+  int pf;               // trk_set_tuning("rf_pf"): L2 prefetch distance in ROIs (X rows of ROI + pf), 0 = none
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
 };
 

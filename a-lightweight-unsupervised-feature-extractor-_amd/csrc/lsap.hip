@@ -143,34 +143,16 @@ __device__ __forceinline__ void wave_argmin(double& v, int& key, int& col) {
   col = __builtin_amdgcn_readlane(col, 63);
 }
 
+// One matrix's solve with KS column slots per lane (nc <= 64 * KS).  lsap_kernel
+// picks the smallest KS that holds the matrix, so a launch sized for a larger bound
+// (trk_lsap_dev: live tracks + detections in flight) pays only for the columns the
+// matrix has: every per-column loop below is unrolled over KS.
 template <typename T, int KS>
-__global__ void __launch_bounds__(256)
-lsap_kernel(const LsapArgs A) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int f = blockIdx.x;
+__device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem, const int f, const int nr0,
+                                          const int nc0, const T* C, int32_t* assign, int64_t* orows,
+                                          int64_t* ocols) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int nr0 = A.nr[f], nc0 = A.nc[f];
-  const T* C = reinterpret_cast<const T*>(A.C) + (int64_t)f * A.batch_stride;
-  int32_t* assign = A.assign ? A.assign + (int64_t)f * A.nr_max : nullptr;
-  int64_t* orows = A.rows + (int64_t)f * A.kmax;
-  int64_t* ocols = A.cols + (int64_t)f * A.kmax;
-  if (A.dev_nr) {
-    nr0 = A.dev_nr[f];
-    nc0 = A.dev_nc[f];
-    if (nr0 < 0 || nc0 < 0 || nr0 > A.nr_bound || nc0 > A.nc_bound) {  // outside the launch's sizing
-      if (assign)
-        for (int r = threadIdx.x; r < A.nr_bound; r += blockDim.x) assign[r] = -1;
-      if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = -4; }
-      return;
-    }
-  }
-  if (nr0 == 0 || nc0 == 0) {
-    if (assign)
-      for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
-    if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = 0; }
-    return;
-  }
   const bool tr = nc0 < nr0;
   const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;  // working problem: nr <= nc
   const int64_t ld = A.ld;
@@ -209,7 +191,7 @@ lsap_kernel(const LsapArgs A) {
   // longest prefix of rows with a unique finite minimum in a column no earlier
   // row's minimum took is solved in one parallel pass with exactly the state
   // the sequential algorithm reaches; the solver continues after it.
-  const int ks = (nc + 63) >> 6;  // column slots in use (KS is the launch's bound)
+  const int ks = (nc + 63) >> 6;  // column slots in use (<= KS)
   int* firstrow = reinterpret_cast<int*>(ring);  // [nc]: the ring is idle until the loaders start
   for (int j = threadIdx.x; j < nc; j += blockDim.x) firstrow[j] = 0x7fffffff;
   if (threadIdx.x == 0) ctl[3] = nr;
@@ -511,6 +493,52 @@ lsap_kernel(const LsapArgs A) {
       }
   }
   if (threadIdx.x == 0) { A.count[f] = nr; A.status[f] = 0; }
+}
+
+constexpr int lsap_ks_next(int k) { return k == 1 ? 4 : 2 * k; }
+
+template <typename T, int KS, int KSMAX>
+__device__ __forceinline__ void lsap_pick(const int ks, const LsapArgs& A, unsigned char* smem, const int f,
+                                          const int nr0, const int nc0, const T* C, int32_t* assign,
+                                          int64_t* orows, int64_t* ocols) {
+  if constexpr (KS >= KSMAX) {
+    lsap_body<T, KSMAX>(A, smem, f, nr0, nc0, C, assign, orows, ocols);
+  } else {
+    if (ks <= KS) lsap_body<T, KS>(A, smem, f, nr0, nc0, C, assign, orows, ocols);
+    else lsap_pick<T, lsap_ks_next(KS), KSMAX>(ks, A, smem, f, nr0, nc0, C, assign, orows, ocols);
+  }
+}
+
+// one workgroup per matrix; KSMAX = the column slots the launch's widest (bound) matrix
+// needs, the body run = the smallest of 1 / 4 / 8 / 16 / 32 slots this matrix fits
+template <typename T, int KSMAX>
+__global__ void __launch_bounds__(256)
+lsap_kernel(const LsapArgs A) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int f = blockIdx.x;
+  int nr0 = A.nr[f], nc0 = A.nc[f];
+  const T* C = reinterpret_cast<const T*>(A.C) + (int64_t)f * A.batch_stride;
+  int32_t* assign = A.assign ? A.assign + (int64_t)f * A.nr_max : nullptr;
+  int64_t* orows = A.rows + (int64_t)f * A.kmax;
+  int64_t* ocols = A.cols + (int64_t)f * A.kmax;
+  if (A.dev_nr) {
+    nr0 = A.dev_nr[f];
+    nc0 = A.dev_nc[f];
+    if (nr0 < 0 || nc0 < 0 || nr0 > A.nr_bound || nc0 > A.nc_bound) {  // outside the launch's sizing
+      if (assign)
+        for (int r = threadIdx.x; r < A.nr_bound; r += blockDim.x) assign[r] = -1;
+      if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = -4; }
+      return;
+    }
+  }
+  if (nr0 == 0 || nc0 == 0) {
+    if (assign)
+      for (int r = threadIdx.x; r < nr0; r += blockDim.x) assign[r] = -1;
+    if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = 0; }
+    return;
+  }
+  const int ks = (max(nr0, nc0) + 63) >> 6;  // the working problem's column slots (nc = max)
+  lsap_pick<T, 1, KSMAX>(ks, A, smem, f, nr0, nc0, C, assign, orows, ocols);
 }
 
 template <typename T>

@@ -537,9 +537,14 @@ __device__ __forceinline__ void sample4_asm(f2_t (&t)[1][2], f2_t w12, f2_t w34,
 }
 
 // floor(n / d) for n < 2^31, 0 < d < 2^31, m = udiv_magic_m(d) = floor(2^32 / d) + 1:
-// mulhi(n, m) is q or q + 1 (n * (m - 2^32 / d) < 2^31 * 1 < 2^32), one correction step
-__host__ __device__ inline uint32_t udiv_magic_m(uint32_t d) { return (uint32_t)((1ull << 32) / d + 1); }
+// mulhi(n, m) is q or q + 1 (n * (m - 2^32 / d) < 2^31 * 1 < 2^32), one correction step.
+// d == 1 has no 32-bit multiplier (2^32 + 1 truncates to 1), so it is a separate
+// (wave-uniform, scalar) branch; its m is unused.
+__host__ __device__ inline uint32_t udiv_magic_m(uint32_t d) {
+  return d > 1 ? (uint32_t)((1ull << 32) / d + 1) : 0u;
+}
 __device__ __forceinline__ uint32_t udiv_magic(uint32_t n, uint32_t d, uint32_t m) {
+  if (d == 1) return n;
   uint32_t q = __umulhi(n, m);
   if (q * d > n) --q;
   return q;
@@ -654,9 +659,15 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
   }
   f2_t zero[NH][2];  // pixel (0,0): what torchvision reads for an empty sample
 #pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    if (FMA) zero[h][0] = zero[h][1] = f2_t{0.f, 0.f};  // FMA: an empty sample is +0 (no read)
-    else bload4(rs, voff[h], 0, zero[h]);
+  for (int h = 0; h < NH; ++h) bload4(rs, voff[h], 0, zero[h]);
+  if (FMA) {
+    // FMA: an empty sample is 0 * pixel(0,0) + 0: +0 for a finite pixel, NaN for a NaN / Inf
+    // one, as torchvision's 0-weight sum of four pixel(0,0) reads (after its `0 + t`)
+    const f2_t Z0 = {0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) zero[h][p] = zero[h][p] * Z0 + Z0;
   }
 
   ColCache2<NH> kc[2];
@@ -743,7 +754,7 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
         } else {
           if (FMA) {
   #pragma unroll
-            for (int h = 0; h < NH; ++h) t[iy][h][0] = t[iy][h][1] = zero[h][0];
+            for (int h = 0; h < NH; ++h) { t[iy][h][0] = zero[h][0]; t[iy][h][1] = zero[h][1]; }
           } else {
             sample4<NH, FMA>(t[iy], 0.f, 0.f, 0.f, 0.f, zero, zero, zero, zero);
           }

@@ -203,8 +203,9 @@ def enc_rmb_front(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: to
         raise TypeError("enc_rmb_front: bf16 operands required")
     if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
         raise ValueError("enc_rmb_front: X must be contiguous [R*100, 512]")
-    if W1p.numel() != 1024 * 512 or W2p.numel() != 1024 * 512 or not (W1p.is_contiguous() and W2p.is_contiguous()):
-        raise ValueError("enc_rmb_front: W1p / W2p must be packed [2, 16, 32, 4, 16, 8] fragments")
+    pk = (2, 16, 32, 4, 16, 8)  # enc_pack_fragments' layout (an unpacked [1024, 512] has the same numel)
+    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or not (W1p.is_contiguous() and W2p.is_contiguous()):
+        raise ValueError("enc_rmb_front: W1p / W2p must be enc_pack_fragments output [2, 16, 32, 4, 16, 8]")
     if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
         raise ValueError("enc_rmb_front: wdw [25, 1024] f32 and bias [1024] required")
     M = X.shape[0]

@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[2]): each GPU runs
 frame of every stream, the full per-frame tracker hot path:
   [8,512,40,40] fp32 SPP-CSPC maps (SiLU(randn), resident) + 256 boxes/frame
   -> trk roi_align      (HIP: NCHW f32 in, NHWC bf16 out, 10x10 bins)
-  -> encoder            (PyTorch-ROCm GEMMs + HIP depthwise/act kernels, bf16)
+  -> encoder            (HIP: rmb_front = 1x1 convs + depthwise + DSC GEMM fused,
+                         SE, transition GEMM, projection head; bf16 MFMA)
   -> MultiStreamTracker.step:
        KF predict + gate inputs (HIP) -> fused cost: top-5 of a 30-deep memory
        bank (f32 MFMA), bbox, conf, Mahalanobis gate (HIP) -> scipy-exact LSAP +
@@ -13,20 +14,84 @@ frame of every stream, the full per-frame tracker hot path:
        bank push (HIP), births, purge.
 Boxes move at constant velocity (bouncing), detections arrive shuffled; a
 30-frame pre-roll fills the memory banks before warm-up.  All inputs are in
-HBM before timing starts.  Multi-GPU: one process per GPU (torchrun), each
-with its own 8 streams, no data-path collective; one barrier + MAX(elapsed)
-all-reduce per report ("scaling": "weak").
+HBM before timing starts.  Multi-GPU: one process per GPU, each with its own 8
+streams, no data-path collective; one barrier + MAX(elapsed) all-reduce per
+report ("scaling": "weak").  The ranks come from torchrun (RANK / WORLD_SIZE in
+the environment, which must agree with --gpus) or, for `bench.py --gpus N`
+started alone, from N child processes this script starts before anything
+touches the GPU (_spawn_ranks).
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
+import os
+import sys
+
+
+def _spawn_ranks():
+    """`python bench.py --gpus N` with N > 1 and no WORLD_SIZE: start N rank
+    processes (this script again, as children: RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set), wait for them and exit with the
+    first failing child's status (the others are then stopped).  Rank 0 prints
+    the JSON line on the inherited stdout.  Runs before torch or the library is
+    imported, so this process never initialises the GPU (and never re-execs).
+    With WORLD_SIZE already set (torchrun) it only checks that --gpus agrees."""
+    import argparse
+    import socket
+    import subprocess
+    import time as _time
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} disagrees with WORLD_SIZE={ws} "
+                             f"(launch with torchrun --nproc-per-node {a.gpus}, or without torchrun)")
+        return
+    if a.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {a.gpus}")
+    if a.gpus == 1:
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            break
+        _time.sleep(0.2)
+    for p in procs:  # a failed rank leaves the others in a collective: stop them (exact PIDs)
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        if rc == 0 and p.returncode != 0:
+            rc = p.returncode
+    print(f"bench.py: {a.gpus} ranks finished, exit {rc}", file=sys.stderr, flush=True)
+    sys.exit(rc if rc > 0 else (1 if rc else 0))
+
+
+if __name__ == "__main__":
+    _spawn_ranks()
+
 import argparse
 import ctypes
 import importlib
 import json
-import os
-import sys
 import time
 
 import numpy as np
@@ -389,6 +454,14 @@ class LiveProbe:
         torch.cuda.synchronize()
         return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e3 for k, v in self.ev.items() if v}
 
+    def stage_means_us(self, key):
+        """the tracker's cost / LSAP launches alternate stage 1 (main rows) and stage 2
+        (ReID-only rows): mean device time of each, per launch"""
+        torch.cuda.synchronize()
+        v = [a.elapsed_time(b) * 1e3 for a, b in self.ev.get(key, [])]
+        return {"stage1": round(float(np.mean(v[0::2])), 2) if v[0::2] else None,
+                "stage2": round(float(np.mean(v[1::2])), 2) if v[1::2] else None}
+
     def sum_per_step_us(self, steps):
         """summed device time of every probed launch per step: compared with
         ms_per_step it shows whether streams overlapped (sum > step) or the GPU
@@ -566,9 +639,10 @@ def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
                                              "cost_ms": round(med(t_lit) * 1e3, 1)}})
 
 
-def timed_region(step, steps, dist, sync, red_dev, finish=None):
+def timed_region(step, steps, dist, sync, red_dev, finish=None, own=None):
     """Run `steps` steps between a barrier + device sync on both sides; return
-    the MAX elapsed time over ranks (one all_reduce) and the step outputs."""
+    the MAX elapsed time over ranks (one all_reduce) and the step outputs
+    (this rank's own elapsed time is appended to `own` if given)."""
     if dist is not None:
         dist.barrier()
     sync()
@@ -578,6 +652,8 @@ def timed_region(step, steps, dist, sync, red_dev, finish=None):
         finish()  # every frame's assignment indices read on the host
     sync()
     el = time.perf_counter() - t0
+    if own is not None:
+        own.append(el)
     if dist is not None:
         t = torch.tensor([el], device=red_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -603,20 +679,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
     dist = None
+    red_dev = None
     if world > 1:
         import torch.distributed as dist
         # RCCL ("nccl") over xGMI; TRK_DIST_BACKEND=gloo rehearses the multi-rank path with
         # several ranks on one device (RCCL refuses two ranks per GPU)
         backend = os.environ.get("TRK_DIST_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
         if backend != "nccl":
-            local %= max(1, torch.cuda.device_count())
+            local %= max(1, ndev)
+        elif local >= ndev:
+            raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but {ndev} are visible "
+                             f"(TRK_DIST_BACKEND=gloo shares devices between ranks)")
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+            red_dev = torch.device("cpu")  # gloo reduces host tensors
     dev = torch.device("cuda", local)
+    if red_dev is None:
+        red_dev = dev
     torch.cuda.set_device(dev)
 
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
@@ -645,12 +731,15 @@ def main():
     probe = LiveProbe(pool=max(1024, 2 * 20 * (args.steps + 2)))
     probe.on = True
     pipe.tracker.sync_wait_s = 0.0
+    own = []
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
-                               torch.cuda.synchronize, dev, finish=pipe.tracker.drain)
+                               torch.cuda.synchronize, red_dev, finish=pipe.tracker.drain, own=own)
+    el_own = own[0]
     probe.on = False
     kernel_sum = probe.sum_per_step_us(args.steps)
     live = probe.means_us()
     live = {k: v for k, v in live.items() if not k.endswith("_live")}
+    tracker_live = {"lsap": probe.stage_means_us("lsap_live"), "cost": probe.stage_means_us("cost_live")}
     side_gap = probe.embed_gaps_us(len(pipe.sides), pipe.defer_head, pipe.roi_stream is not None)
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
@@ -661,6 +750,12 @@ def main():
     # per-launch device time: live (timed region) where probed, else isolated
     kt = dict(iso)
     kt.update(live)
+    per_rank = [{"rank": rank, "device": str(dev), "elapsed_s": round(el_own, 6), "identity_rate": round(ident, 5),
+                 "rois": args.steps * sc["streams"] * sc["N"]}]
+    if dist is not None:  # after the timed region: which rank ran what (not a data-path collective)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank[0])
+        per_rank = gathered
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -730,6 +825,9 @@ def main():
                                for k in kt},
           "isolated_us": {k: round(v, 2) for k, v in iso.items()},
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2),
+          "tracker_live_us_per_launch": dict(tracker_live, note="live HIP events in the timed region, per "
+                                             "launch of all streams' frames; stage 2 = ReID-only rows (none "
+                                             "matchable in this workload: the launch exits at once)"),
           "embed_stream_idle_us_per_step": None if side_gap is None else round(side_gap, 2)}
     # end-to-end ROIs/s against min(HBM / B_roi, MFMA / F_roi), with
     # B_roi = 12,800 (map share) + 2 x 102,400 (bf16 ROI tensor written + read) + 512
@@ -783,6 +881,10 @@ def main():
                    "streams_per_gpu": Fs, "N": N, "roi": S, "map_layout": MAP_LAYOUT,
                    "parallelism": f"replicas{world}"},
         "roofline": rf, "identity_rate": round(ident, 5),
+        "ranks": {"launcher": ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else
+                               "bench.py --gpus" if world > 1 else "single process"),
+                  "backend": (os.environ.get("TRK_DIST_BACKEND", "nccl") if world > 1 else None),
+                  "per_rank": per_rank},
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(sc, sd, args.cpu_budget)

@@ -188,3 +188,45 @@ def test_scene_shapes_and_bounds():
     for f in range(5):
         for s in range(3):
             assert sorted(sc["obj"][f, s]) == list(range(16))
+
+
+# ------------------------------------------------- bench.py --gpus N launcher ----
+def _bench_cmd(*extra):
+    import subprocess
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *extra], capture_output=True,
+                          text=True, timeout=600, cwd=REPO,
+                          env=dict(os.environ, TRK_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1"))
+
+
+def test_bench_gpus_disagrees_with_world_size():
+    """--gpus that disagrees with a torchrun WORLD_SIZE fails loudly, before the GPU is touched"""
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, cwd=REPO,
+                       env=dict(os.environ, WORLD_SIZE="3", RANK="0"))
+    assert r.returncode != 0
+    assert "disagrees with WORLD_SIZE=3" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_gpus_2_spawns_ranks_running_the_pipeline():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts two rank processes itself (gloo on
+    the one leased GPU here; RCCL, one GPU per rank, on a node), each running the real
+    Pipeline on its own 8 streams; rank 0 prints one JSON line for the whole job"""
+    import json
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    r = _bench_cmd("--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "replicas2"
+    assert line["ranks"]["launcher"] == "bench.py --gpus" and line["ranks"]["backend"] == "gloo"
+    pr = line["ranks"]["per_rank"]
+    assert [p["rank"] for p in pr] == [0, 1]
+    assert all(p["rois"] == 3 * 8 * 256 and p["identity_rate"] == 1.0 for p in pr), pr
+    # value = all ranks' ROIs / the slowest rank's time
+    assert abs(line["value"] - 2 * 3 * 8 * 256 / max(p["elapsed_s"] for p in pr)) <= 0.01 * line["value"]

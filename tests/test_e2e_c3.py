@@ -1,0 +1,100 @@
+"""End-to-end assignment parity of the BENCHED configuration (BASELINE c3).
+
+bench.Pipeline with its default knobs -- NCHW f32 maps -> ROI Align (bf16 NHWC out,
+fused sample arithmetic) -> the bf16 encoder (rmb_front, SE, transition, head) ->
+the device-resident MultiStreamTracker, frames software-pipelined across three HIP
+streams -- against the reference's CPU chain on the same maps and boxes:
+
+  oracle.roi_align      torchvision 0.20.1's CPU roi_align restated (C)
+  oracle.encoder_forward the reference's encoder eval graph in plain fp32 torch
+                        (encoderAndHead.py:21-26, card.py); run here on the GPU's
+                        fp32 torch ops for time, and cross-checked against the
+                        same function on the CPU (<= 1e-5)
+  tracker_ref.TrackerRef the reference's Tracking.update (mainTracking.py:450-610)
+                        restated on the oracle, pinned on the four reference-run
+                        goldens (tests/test_oracle.py)
+
+The per-frame body is the reference's tracking.py:304-326.  Every frame's matches,
+unmatched track ids and unmatched detections must be identical for every stream.
+The bf16 embedding error against the fp32 chain is measured on the same frames and
+bounded here (the bound is ~2x the maximum measured on MI355X).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import gen_common as G
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# measured on MI355X (profiles/r04_e2e_c3.txt): max |bf16 - fp32| over 8 x 2,048 unit
+# embeddings and the smallest per-row cosine; the assertions use about 2x the error
+EMB_MAX_ABS = 0.02
+EMB_MIN_COS = 0.999
+
+
+def _model(trk, gpu):
+    sd = {k: torch.from_numpy(v) for k, v in G.seeded_state_dict_np(0).items()}
+    m = trk.Model(512, 512, 10, 128).eval()
+    m.load_state_dict(sd, strict=True)
+    return m.to(gpu), sd
+
+
+@pytest.mark.timeout(600)
+def test_bench_pipeline_matches_reference_chain_c3(trk, oracle, gpu):
+    sys.path.insert(0, REPO)
+    import bench
+    import tracker_ref as TR
+    S, N, PRE, K = 8, 256, 30, 8
+    frames = PRE + K
+    sc = bench.make_scenes(gpu, S, N, frames + 2, seed=1000)
+    model, sd = _model(trk, gpu)
+    pipe = bench.Pipeline(sc, model)
+    handles = [pipe.step(f) for f in range(frames)]
+    pipe.tracker.drain()
+    got = [h.result() for h in handles]
+
+    # the product's embeddings of the checked frames, recomputed through the same path
+    emb_dev = {}
+    for f in range(PRE, frames):
+        emb_dev[f] = pipe.stage_embed(pipe.stage_roi(f)).reshape(S * N, 128).float().cpu().numpy()
+    torch.cuda.synchronize()
+
+    prev = (torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    sd_gpu = {k: v.to(gpu) for k, v in sd.items()}
+    refs = [TR.TrackerRef() for _ in range(S)]
+    max_abs, min_cos = 0.0, 1.0
+    nmatch = 0
+    try:
+        for f in range(frames):
+            fmap = bench.frame_map(sc, f).cpu().numpy()
+            rois = sc["np"]["rois"][f]  # [S*N, 5], batch index = stream
+            roi = oracle.roi_align(fmap, rois, (10, 10), 40 / 1280.0, 2, True)
+            with torch.no_grad():
+                emb = oracle.encoder_forward(sd_gpu, torch.from_numpy(roi).to(gpu)).cpu().numpy()
+                if f == PRE:  # the GPU's fp32 torch ops vs the same restatement on the CPU
+                    cpu = oracle.encoder_forward(sd, torch.from_numpy(roi[:64])).numpy()
+                    assert float(np.abs(cpu - emb[:64]).max()) <= 1e-5
+            if f in emb_dev:
+                d = emb_dev[f]
+                max_abs = max(max_abs, float(np.abs(d - emb).max()))
+                min_cos = min(min_cos, float((d * emb).sum(1).min()))
+            for s in range(S):
+                exp = refs[s].update(list(emb[s * N:(s + 1) * N]), sc["np"]["dbox"][f, s].tolist(),
+                                     sc["np"]["dconf"][f, s].tolist())
+                assert got[f][s].as_tuple() == exp, (f, s)
+                nmatch += len(exp[0])
+    finally:
+        torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = prev
+    print(f"\nc3 e2e: {frames} frames x {S} streams identical, {nmatch} matches; bf16 embeddings vs fp32 "
+          f"chain: max |d| {max_abs:.3e}, min cosine {min_cos:.7f}")
+    assert nmatch >= (frames - 1) * S * N  # every detection after the first frame matched
+    assert max_abs <= EMB_MAX_ABS, max_abs
+    assert min_cos >= EMB_MIN_COS, min_cos

@@ -168,6 +168,71 @@ def test_roi_align_sweep_variants(trk, oracle, gpu, knobs):
             L.trk_set_tuning(k.encode(), 1)  # the defaults
 
 
+@pytest.mark.parametrize("C,sweep,ph", [(256, 1, 10), (128, 1, 7), (512, 2, 10), (1024, 2, 7), (512, 1, 1),
+                                        (128, 1, 1), (260, 1, 10)])
+def test_roi_align_sweep_one_chunk_and_one_row(trk, oracle, gpu, C, sweep, ph):
+    """The row sweep's work-item decomposition divides by the chunk count and by PH with
+    magic multipliers; a divisor of 1 (C <= 256 channels per wave, 512 with roi_sweep=2,
+    or a single bin row) has no 32-bit multiplier and takes its own branch.  Every
+    output written and bit-exact vs the oracle (f32; bf16 with the exact arithmetic)."""
+    L = trk.lib()
+    rng = np.random.default_rng(C + ph)
+    B, N = 2, 40
+    feat = _feat(rng, B, C=C)
+    boxes = _boxes(rng, B * N)
+    rois = np.concatenate([np.repeat(np.arange(B), N).astype(np.float32)[:, None], boxes], 1)
+    x = torch.from_numpy(feat).to(gpu)
+    r = torch.from_numpy(rois).to(gpu)
+    try:
+        assert L.trk_set_tuning(b"roi_sweep", sweep) == 0
+        assert L.trk_set_tuning(b"roi_fma", 0) == 0
+        for pw in (10, 7):
+            exp = oracle.roi_align(feat, rois, (ph, pw), 1 / 32, 2, True)
+            got = trk.roi_align(x, r, (ph, pw), 1 / 32, 2, True, channels_last=True)
+            assert np.array_equal(got.cpu().numpy(), exp), (C, sweep, ph, pw)
+            bf = trk.roi_align(x, r, (ph, pw), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+            assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16()), (C, sweep, ph, pw)
+    finally:
+        L.trk_set_tuning(b"roi_sweep", 1)
+        L.trk_set_tuning(b"roi_fma", 1)
+
+
+@pytest.mark.parametrize("fma", [0, 1])
+def test_roi_align_nan_at_origin(trk, oracle, gpu, fma):
+    """torchvision's CPU kernel reads pixel (0,0) with weight 0 for a sample outside the
+    map, so a NaN there reaches exactly the bins that have such a sample.  Both the
+    exact and the fused (bf16 default) arithmetic keep that read: the NaN positions equal
+    the oracle's, and every other output is within the test_roi_align_sweep_variants
+    tolerance (bit-exact with the exact arithmetic)."""
+    L = trk.lib()
+    rng = np.random.default_rng(21)
+    B, N = 2, 64
+    feat = _feat(rng, B)
+    feat[:, :, 0, 0] = np.nan
+    boxes = _boxes(rng, B * N)
+    rois = np.concatenate([np.repeat(np.arange(B), N).astype(np.float32)[:, None], boxes], 1)
+    rois[0, 1:] = [2000, 2000, 2100, 2100]  # all samples outside
+    rois[1, 1:] = [-300, -300, 100, 100]    # some outside
+    rois[N, 1:] = [1200, 1200, 1400, 1500]
+    x = torch.from_numpy(feat).to(gpu)
+    r = torch.from_numpy(rois).to(gpu)
+    try:
+        assert L.trk_set_tuning(b"roi_fma", fma) == 0
+        exp = oracle.roi_align(feat, rois, (10, 10), 1 / 32, 2, True)
+        assert np.isnan(exp).any() and not np.isnan(exp).all()
+        bf = trk.roi_align(x, r, (10, 10), 1 / 32, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+        got = bf.cpu().float().numpy()
+        assert np.array_equal(np.isnan(got), np.isnan(exp))
+        ok = ~np.isnan(exp)
+        if fma:
+            tol = np.abs(exp[ok]) * 2.0 ** -8 + 2.0 ** -19 * float(np.nanmax(np.abs(feat)))
+            assert np.all(np.abs(got[ok] - exp[ok]) <= tol)
+        else:
+            assert np.array_equal(got[ok], torch.from_numpy(exp).bfloat16().float().numpy()[ok])
+    finally:
+        L.trk_set_tuning(b"roi_fma", 1)
+
+
 def test_roi_align_odd_channels_and_empty(trk, oracle, gpu):
     rng = np.random.default_rng(4)
     feat = rng.standard_normal((2, 37, 13, 11)).astype(np.float32)
@@ -652,6 +717,11 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R):
     assert (f1 - f2).abs().max().item() <= 1e-5 * f2.abs().max().item()
     XRN1b, s1b = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)  # deterministic
     assert torch.equal(XRN1, XRN1b) and torch.equal(ops.enc_sums_reduce(s1b, P), f1)
+    # unpacked weights (same numel) are refused, not read in the wrong order
+    with pytest.raises(ValueError, match="enc_pack_fragments"):
+        ops.enc_rmb_front(X, W1, wdw, W2p, b2)
+    with pytest.raises(ValueError, match="enc_pack_fragments"):
+        ops.enc_rmb_front(X, W1p, wdw, W2.reshape(1024, 512), b2)
 
 
 def _partials(total, P, parts=3):

@@ -392,6 +392,55 @@ def test_error_frame_then_stream_continues(trk, gpu):
         assert _same(h.result()[0], rh[0]), f
 
 
+def test_stage2_solver_error_then_stream_continues(trk, gpu):
+    """A frame whose only rows are long-lost (M1 == 0: stage 1 never runs) and whose
+    stage-2 ReID cost holds a NaN raises the reference's ValueError from stage 2's
+    hungarian_assign (mainTracking.py:561).  The reference leaves that frame as the
+    exception found it: every track predicted, no stage-2 misses, no births, no purge.
+    The device's results and every following frame (ReID match, birth, misses) equal
+    tracker_ref (the reference's update restated), whose state after the raise is the
+    reference's."""
+    import tracker_ref as TR
+    rng = np.random.default_rng(31)
+    unit = lambda v: (v / np.linalg.norm(v)).astype(np.float32)
+    app = [unit(rng.standard_normal(128)) for _ in range(3)]
+    boxes = [[100.0, 400.0, 180.0, 520.0], [600.0, 500.0, 700.0, 640.0], [900.0, 300.0, 960.0, 380.0]]
+    near = lambda k: unit(app[k] + 0.02 * rng.standard_normal(128))
+    nan_emb = near(0).copy()
+    nan_emb[7] = np.nan
+    frames = [([near(0), near(1)], [boxes[0], boxes[1]], [0.9, 0.8])]
+    frames += [([], [], [])] * 51                                   # miss 51 > lost_reid_after (50)
+    frames += [([nan_emb], [boxes[0]], [0.9])]                      # stage 2 only -> NaN -> raise
+    frames += [([near(0), near(2)], [boxes[0], boxes[2]], [0.9, 0.7]),  # ReID of track 0, birth
+               ([near(2)], [boxes[2]], [0.7]), ([near(2), near(1)], [boxes[2], boxes[1]], [0.7, 0.8])]
+    bad = 52
+    ref = TR.TrackerRef()
+    dev = trk.MultiStreamTracker(1, capacity=64, device=gpu, max_inflight=3)
+    handles, expect = [], []
+    for f, (e, b, c) in enumerate(frames):
+        n = len(c)
+        if f == bad:
+            with pytest.raises(ValueError, match="invalid numeric entries"):
+                ref.update(e, b, c)
+            expect.append(None)
+        else:
+            expect.append(ref.update(e, b, c))
+        E = torch.from_numpy(np.asarray(e, np.float32).reshape(1, n, 128)).to(gpu)
+        B = torch.from_numpy(np.asarray(b, np.float32).reshape(1, n, 4)).to(gpu)
+        C = torch.from_numpy(np.asarray(c, np.float32).reshape(1, n)).to(gpu)
+        C64 = torch.from_numpy(np.asarray(c, np.float64).reshape(1, n)).to(gpu)
+        handles.append(dev.step_async(E, B, C, [n], [f], dconf64=C64))
+    for f, (h, exp) in enumerate(zip(handles, expect)):
+        if exp is None:
+            with pytest.raises(ValueError, match="invalid numeric entries"):
+                h.result()
+            continue
+        assert h.result()[0].as_tuple() == exp, f
+    # the ReID frame matched track 0 in stage 2 and the new object was born as id 2
+    assert expect[bad + 1][0] == [(0, 0)] and expect[bad + 1][2] == [1]
+    assert (2, 0) in expect[bad + 2][0]
+
+
 def _n256():
     """the N = 256 scene regenerated from its seed (the fixture holds the reference's
     outputs and a digest of the inputs it ran on)"""
