@@ -41,6 +41,7 @@ int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column s
                      // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
 int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + rf_pf, 0: none (GEMM1
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
+int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
@@ -1514,6 +1515,351 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
   }
 }
 
+// ---- rmb_front with decoupled halves (round 4, rf_v = 2, the default).  The same
+// phases, math and per-wave tiles as rf_body, but the 8 waves no longer pass full
+// workgroup barriers between phases.  Half A (waves 0..3, one per SIMD) produces Y1 / Y2
+// channels 0..255 and half B (waves 4..7) channels 256..511; the depthwise of a half only
+// reads its own half's Y1, so the only cross-half dependencies left are GEMM2's K steps
+// 8..15 (Y2(B)) and the LDS regions the halves reuse.  Those are tracked by LDS counters
+// (a wave adds 1 after its LDS writes or DMA have landed; a waiter polls with s_sleep).
+// A runs ahead (older waves, and MFMA phases at s_setprio 1), so on every SIMD one
+// wave's depthwise / activation VALU runs beside its partner's MFMAs instead of after
+// them (rf_body: 68K cycles per workgroup, of which 27K MFMA).
+// LDS (blocks of RF_KBS dwords, the rf_body image): blocks 0..15 = X for GEMM1 (both
+// halves), blocks 16..23 = Y(A); once both halves finished GEMM1, blocks 8..15 = Y(B)
+// and blocks 0..7 = A's output staging; B stages over Y(A) after both halves' GEMM2.
+constexpr int RF2_NB = 24;
+constexpr size_t RF2_CTR = (size_t)(RF2_NB - 1) * RF_KBS * 4 + 112 * 64;  // past block 23's row-111 reads
+enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16, RF2_NCTR = 20 };
+constexpr size_t RF2_LDS = RF2_CTR + RF2_NCTR * 4;
+constexpr int RF2_SROW = 128;  // output staging row (dwords): 256 channels, 16-B chunks XOR-swizzled by row
+static_assert(RF2_LDS <= 160 * 1024, "one rmb_front workgroup per CU");
+static_assert((size_t)RF_S * RF2_SROW * 4 <= (size_t)8 * RF_KBS * 4, "a half's staging fits 8 blocks");
+constexpr uint32_t kRf2Spin = 1u << 22;  // poll bound (~0.1 s): a lost signal ends the wait, never hangs
+
+// Y block of K block kb (32 channels): channels 0..255 in blocks 16..23, 256..511 in 8..15
+__device__ __forceinline__ int rf2_yblk(int kb) { return kb < 8 ? kb + 16 : kb; }
+__device__ __forceinline__ int rf2_yaddr(int s, int col) {
+  const int kb = col >> 5, c = (col & 31) >> 3, d = (col & 7) >> 1;
+  return rf2_yblk(kb) * RF_KBS + s * 16 + ((c ^ rf_sw(s)) << 2) + d;
+}
+// this wave's LDS writes (and any LDS-DMA it waited for) have landed: count it (lane 0
+// only).  Both hand-off halves are single asm statements: a C++ loop or lane branch here
+// splits the unrolled K loops' scheduling regions (1.2 KB of spills per lane)
+__device__ __forceinline__ void rf2_signal(uint32_t* ctr, int) {
+  uint64_t saved;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 %[e], exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %[a], %[one]\n\t"
+      "s_mov_b64 exec, %[e]"
+      : [e] "=&s"(saved)
+      : [a] "v"(lds_addr(ctr)), [one] "v"(1u)
+      : "memory");
+}
+// poll the counter until it reaches target (bounded: a lost signal ends the wait)
+__device__ __forceinline__ void rf2_wait(uint32_t* ctr, uint32_t target) {
+  uint32_t v, sv, n;
+  asm volatile(
+      "s_mov_b32 %[n], 0\n"
+      "1:\n\t"
+      "ds_read_b32 %[v], %[a]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %[s], %[v]\n\t"
+      "s_cmp_ge_u32 %[s], %[t]\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_add_u32 %[n], %[n], 1\n\t"
+      "s_cmp_gt_u32 %[n], %[lim]\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_sleep 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : [v] "=&v"(v), [s] "=&s"(sv), [n] "=&s"(n)
+      : [a] "v"(lds_addr(ctr)), [t] "s"(target), [lim] "s"(kRf2Spin)
+      : "memory", "scc");
+}
+
+template <int G>
+__device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned char* smem) {
+  const int64_t roi = lb >> 1;
+  unsigned long long pst[8];
+  const bool prof = a.prof != nullptr;
+  if (prof) pst[0] = eg_stamp();
+  uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2, hw = wave & 3;  // half A = 0, B = 1; wave within the half
+  const int fr = lane & 15, fc = lane >> 4;
+  const int64_t r0 = roi * RF_S;
+  constexpr int NK = 512 / BK;
+  if (tid < RF2_NCTR) ctr[tid] = 0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g4_barrier();  // the only full barrier: counters zeroed
+
+  // X -> blocks 0..15, moved by half A only (2 DMA ops per block per wave: pieces
+  // 100 hw + lane and 100 hw + 64 + lane < 400, piece p = row p >> 2, slot p & 3)
+  const int xp1 = 100 * hw + lane, xp2 = 100 * hw + 64 + lane;
+  const uint16_t* xs1 = a.X + (r0 + (xp1 >> 2)) * 512 + (((xp1 & 3) ^ rf_sw(xp1 >> 2)) * 8);
+  const uint16_t* xs2 = a.X + (r0 + min(xp2 >> 2, RF_S - 1)) * 512 + (((xp2 & 3) ^ rf_sw(xp2 >> 2)) * 8);
+  auto issueX = [&](int grp) {
+    const uint16_t* p1 = xs1;
+    const uint16_t* p2 = xs2;
+    asm volatile("" : "+v"(p1), "+v"(p2));  // per group: the block addresses are not all hoisted
+#pragma unroll
+    for (int kb = 4 * grp; kb < 4 * grp + 4; ++kb) {
+      __builtin_amdgcn_global_load_lds(GPTR(p1 + kb * BK), LPTR(Y + kb * RF_KBS + 400 * hw), 16, 0, 0);
+      if (lane < 36)
+        __builtin_amdgcn_global_load_lds(GPTR(p2 + kb * BK), LPTR(Y + kb * RF_KBS + 400 * hw + 256), 16, 0, 0);
+    }
+  };
+  const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
+  const uint4* b2p = a.W2p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
+  u32x4 bq[3][4];
+  const int lterm = fr * 4 + (fc ^ rf_sw(fr));
+  const uint32_t y_a = lds_addr(Y) + lterm * 16;
+
+  f4v acc[7][4];
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // ---- GEMM1 (K = 512 over X blocks 0..15); A: 8 DMA ops per group, B: none.  One
+  // loop per half (HALF a template constant): a half test inside the unrolled loop costs
+  // spills
+  auto gemm1 = [&](auto half_c) {
+    constexpr int HALF = decltype(half_c)::value;
+    if (HALF == 0) issueX(0);
+    rf_loadB(b1p, 0, bq[0]);
+    rf_loadB(b1p, 1, bq[1]);
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+      u32x4(&b)[4] = bq[kt % 3];
+      if (HALF == 0) {
+        // group boundary: vmcnt(0) (an LDS-DMA may retire after younger VGPR loads), count
+        // this wave's share of the group, wait for the other three
+        if (kt % 4 == 0) {
+          rf_vmwait(0, b);
+          rf2_signal(ctr + RF2_CX + kt / 4, lane);
+          rf2_wait(ctr + RF2_CX + kt / 4, 4);
+          if (kt / 4 + 1 < 4) issueX(kt / 4 + 1);
+        } else {
+          rf_vmwait(((kt - 1) % 4 == 0 && (kt - 1) / 4 + 1 < 4 ? 8 : 0) + (kt + 1 < NK ? 4 : 0), b);
+        }
+      } else {
+        rf_vmwait(kt + 1 < NK ? 4 : 0, b);
+        if (kt % 4 == 0) rf2_wait(ctr + RF2_CX + kt / 4, 4);
+      }
+      if (kt + 2 < NK) rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
+      rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
+    }
+  };
+  __builtin_amdgcn_s_setprio(1);
+  if (half == 0) gemm1(std::integral_constant<int, 0>{});
+  else gemm1(std::integral_constant<int, 1>{});
+  __builtin_amdgcn_s_setprio(0);
+  rf2_signal(ctr + RF2_CG1 + half, lane);  // this wave's reads of X are done
+  if (prof) {
+    asm volatile("" ::"v"(acc[6][3][3]));
+    pst[1] = eg_stamp();
+  }
+  // B's Y1 goes over X blocks 8..15: every wave of both halves must be past GEMM1
+  if (half == 1) {
+    rf2_wait(ctr + RF2_CG1 + 0, 4);
+    rf2_wait(ctr + RF2_CG1 + 1, 4);
+  }
+  // ---- Y1 -> LDS (the wave's 64 channels of its half's region)
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int px = i * 16 + fr;
+    if (px < RF_S) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4v v = acc[i][t];
+        *reinterpret_cast<uint2*>(Y + rf2_yaddr(px, wave * 64 + t * 16 + fc * 4)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+  const int cg = wave >> 1;  // the wave's 128 depthwise channels (in its own half)
+  dw_pair_t wreg[25];
+  {
+    const float* wp = a.wdw + G * 512 + cg * 128 + 2 * lane;
+#pragma unroll
+    for (int k = 0; k < 25; ++k)
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(wreg[k]) : "v"(wp + k * 1024) : "memory");
+  }
+  rf_loadB(b2p, 0, bq[0]);
+  rf_loadB(b2p, 1, bq[1]);
+  rf2_signal(ctr + RF2_CY1 + half, lane);
+  rf2_wait(ctr + RF2_CY1 + half, 4);  // the half's Y1 is in
+  if (prof) pst[2] = eg_stamp();
+  asm volatile("s_waitcnt vmcnt(8)" : "+v"(wreg[0]), "+v"(wreg[1]), "+v"(wreg[2]), "+v"(wreg[3]), "+v"(wreg[4]),
+               "+v"(wreg[5]), "+v"(wreg[6]), "+v"(wreg[7]), "+v"(wreg[8]), "+v"(wreg[9]), "+v"(wreg[10]),
+               "+v"(wreg[11]), "+v"(wreg[12])::"memory");
+  asm volatile("" : "+v"(wreg[13]), "+v"(wreg[14]), "+v"(wreg[15]), "+v"(wreg[16]), "+v"(wreg[17]), "+v"(wreg[18]),
+               "+v"(wreg[19]), "+v"(wreg[20]), "+v"(wreg[21]), "+v"(wreg[22]), "+v"(wreg[23]), "+v"(wreg[24]));
+
+  // ---- depthwise 5x5 in place: waves 2 cg and 2 cg + 1 own the two output halves of the
+  // same 128 channels, so the read-before-overwrite hand-off is between those two only
+  const int NPF = (G == 0 && a.pf) ? 2 : 0;
+  uint32_t pf0 = 0, pf1 = 0;
+  {
+    const int kb0 = rf2_yblk(cg * 4 + (lane >> 4)), c0 = (lane & 15) >> 2, d0 = lane & 3;
+    const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
+                       kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
+    uint32_t o0[25], o1[25];
+    auto prefetch = [&]() {  // rf_body's L2 prefetch of ROI + a.pf's X rows (reinforce workgroups)
+      if (G == 0 && a.pf) {
+        const int64_t rn = min(roi + a.pf, a.R - 1);
+        const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
+        const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
+        asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
+        asm volatile("global_load_dword %0, %1, off" : "+v"(pf1) : "v"(pb) : "memory");
+      }
+    };
+    if ((wave & 1) == 0) {
+      rf_dw5q<0, 0>(Y, yb, wreg, o0);
+      rf_dw5q<0, 1>(Y, yb, wreg, o1);
+      prefetch();
+      rf2_signal(ctr + RF2_CDW + cg, lane);
+      rf2_wait(ctr + RF2_CDW + cg, 2);
+      rf_dw5q_store<0, 0>(Y, yb, o0);
+      rf_dw5q_store<0, 1>(Y, yb, o1);
+    } else {
+      rf_dw5q<1, 0>(Y, yb, wreg, o0);
+      rf_dw5q<1, 1>(Y, yb, wreg, o1);
+      prefetch();
+      rf2_signal(ctr + RF2_CDW + cg, lane);
+      rf2_wait(ctr + RF2_CDW + cg, 2);
+      rf_dw5q_store<1, 0>(Y, yb, o0);
+      rf_dw5q_store<1, 1>(Y, yb, o1);
+    }
+  }
+  rf2_signal(ctr + RF2_CY2 + half, lane);
+  if (prof) pst[3] = eg_stamp();
+
+  // ---- GEMM2: K steps 0..7 read Y2(A), 8..15 Y2(B)
+  float4 bias4[4];
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    u32x4(&b)[4] = bq[kt % 3];
+    rf_vmwait(kt + 1 < NK ? 4 + (kt < 2 ? NPF : 0) : 0, b);
+    if (kt == 2 && G == 0) asm volatile("" : "+v"(pf0), "+v"(pf1));  // retired by the wait above
+    if (kt == 0) rf2_wait(ctr + RF2_CY2 + 0, 4);
+    if (kt == 8) rf2_wait(ctr + RF2_CY2 + 1, 4);
+    if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
+    if (kt == NK - 3) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
+    }
+    rf_mfma_step(y_a + rf2_yblk(kt) * RF_KBS * 4, b, acc);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  rf2_signal(ctr + RF2_CG2 + half, lane);  // this wave's reads of the Y image are done
+  if (prof) {
+    asm volatile("" ::"v"(acc[6][3][3]));
+    pst[4] = eg_stamp();
+  }
+  // ---- epilogue: BN-folded bias + activation, ROI column sums (rf_body's)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
+        v = G == 1 ? hswish2(v) : silu2(v);
+        acc[i][t][2 * h] = v.x;
+        acc[i][t][2 * h + 1] = v.y;
+      }
+  }
+  {
+    const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float sv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) x += acc[i][t][e];
+        if (fr < 4) x += acc[6][t][e];
+        sv[e] = x;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sv[e] += lane_xor1(sv[e]);
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
+      }
+      if (fr == 0) {
+        long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[e] * kFix);
+        for (int j = 1; j < cnt; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[j * 1024 + e] = 0;
+      }
+    }
+  }
+  if (prof) pst[5] = eg_stamp();
+  // ---- output staging: A over blocks 0..7 (X, dead once B is past GEMM1), B over Y(A)
+  // (dead once both halves are past GEMM2); 16-B chunk c of row r at slot c ^ (r & 15)
+  if (half == 0) {
+    rf2_wait(ctr + RF2_CG1 + 1, 4);
+  } else {
+    rf2_wait(ctr + RF2_CG2 + 0, 4);
+    rf2_wait(ctr + RF2_CG2 + 1, 4);
+  }
+  uint32_t* stg = Y + (half ? 16 * RF_KBS : 0);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int px = i * 16 + fr;
+    if (px < RF_S) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4v v = acc[i][t];
+        const int ch = hw * 64 + t * 16 + fc * 4;  // channel within the half
+        *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((ch >> 3) ^ (px & 15)) << 2) + ((ch & 7) >> 1)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+  rf2_signal(ctr + RF2_CST + half, lane);
+  rf2_wait(ctr + RF2_CST + half, 4);
+  if (prof) pst[6] = eg_stamp();
+  {
+    uint16_t* dst = a.XRN + r0 * 1024 + G * 512 + half * 256;
+    const int ht = tid & 255;
+#pragma unroll 4
+    for (int q = ht; q < RF_S * 32; q += 256) {
+      const int row = q >> 5, c = q & 31;
+      *reinterpret_cast<uint4*>(dst + (int64_t)row * 1024 + c * 8) =
+          *reinterpret_cast<const uint4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2));
+    }
+  }
+  if (prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pst[7] = eg_stamp();
+    if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
+      unsigned long long* o = a.prof + (lb * 8 + wave) * 8;
+      for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
+      o[7] = pst[7] - pst[0];
+    }
+  }
+}
+
 // workgroup (roi, g) = logical id 2 roi + g, XCD-remapped: a ROI's two groups run on one
 // XCD, so the second reads the ROI's X rows from L2
 __global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
@@ -1521,6 +1867,12 @@ __global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
   if (lb & 1) rf_body<1>(a, lb, smem);
   else rf_body<0>(a, lb, smem);
+}
+__global__ void __launch_bounds__(512, 1) rmb_front2_kernel(RfArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  if (lb & 1) rf2_body<1>(a, lb, smem);
+  else rf2_body<0>(a, lb, smem);
 }
 
 template <int EPI>
@@ -1675,6 +2027,8 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front2_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
     attr = true;
   }
   RfArgs a;
@@ -1688,6 +2042,11 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.R = M / RF_S;
   a.pf = g_rf_pf;
   a.prof = g_enc_prof;
+  if (g_rf_v == 2) {
+    hipLaunchKernelGGL(rmb_front2_kernel, dim3((unsigned)nwg), dim3(512), RF2_LDS,
+                       reinterpret_cast<hipStream_t>(stream), a);
+    return trk::check_launch("rmb_front2_kernel");
+  }
   hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
                      a);
   return trk::check_launch("rmb_front_kernel");

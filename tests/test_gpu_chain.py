@@ -74,6 +74,7 @@ def test_c3_bf16_encoder_full_size_vs_fp32(trk, gpu):
     assert zb.shape == (F * N, 128) and zb.dtype == torch.float32
     assert torch.isfinite(zb).all()
     cos = (zb * z32).sum(1)
+    print(f"\nc3 bf16 vs fp32 encoder: max |d| {(zb - z32).abs().max().item():.3e}, min cosine {cos.min().item():.7f}")
     assert cos.min().item() >= 0.999, cos.min().item()
     # deterministic at full size (fixed-point ROI sums, no atomics on values)
     with torch.no_grad():
@@ -173,9 +174,13 @@ def test_reference_half_configuration(trk, gpu):
         z16 = torch.nn.functional.normalize(m16(x16).float(), dim=1)
         z32 = m32(x16.float())
     cos = (z16 * z32).sum(1)
+    print(f"\nfp16 model vs fp32 on fp16 inputs: max |d| {(z16 - z32).abs().max().item():.3e}, "
+          f"min cosine {float(cos.min()):.7f}")
     assert float(cos.min()) >= 0.999, float(cos.min())
     d = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
     x = torch.from_numpy(G.encoder_input(int(d["seed_s10"]), 16, 10)).to(gpu)
     with torch.no_grad():
         z = torch.nn.functional.normalize(m16(x.half()).float(), dim=1).cpu().numpy()
+    print(f"fp16 model vs golden: max |d| {np.abs(z - d['z_s10']).max():.3e}, "
+          f"min cosine {float((z * d['z_s10']).sum(1).min()):.7f}")
     assert float((z * d["z_s10"]).sum(1).min()) >= 0.999

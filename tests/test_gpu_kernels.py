@@ -593,6 +593,8 @@ def test_encoder_gpu_vs_reference_golden(trk, gpu, s):
         zb = m(x.bfloat16().contiguous(memory_format=torch.channels_last)).float().cpu().numpy()
     exp = d[f"z_s{s}"]
     assert np.max(np.abs(z - exp)) <= 1e-4
+    print(f"\nbf16 encoder vs golden s={s}: max |d| {np.max(np.abs(zb - exp)):.3e}, "
+          f"min cosine {(zb * exp).sum(1).min():.7f}")
     assert (zb * exp).sum(1).min() >= 0.999
     # bf16: fused trk GEMMs vs the hipBLASLt + separate-pass graph (same bf16 rounding points
     # except the means, which the fused epilogues take in f32 before rounding)
@@ -691,12 +693,23 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         assert (d == 0).float().mean().item() >= 0.9
 
 
+@pytest.mark.parametrize("rf_v", [2, 1])
 @pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R):
+def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v):
     """trk_enc_rmb_front (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
     LDS) vs enc_g1_dwconv -> enc_dsc_gemm: the same MFMA shape, K order and bf16
     roundings, so XRN must be bit-identical; the ROI sums add the same f32 activations in
-    another order (tol 1e-5 of the largest sum).  R = 2048 is the bench's c3 launch."""
+    another order (tol 1e-5 of the largest sum).  R = 2048 is the bench's c3 launch.
+    rf_v 2 (default): the two wave halves hand off through LDS counters; 1: lockstep."""
+    L = trk.lib()
+    assert L.trk_set_tuning(b"rf_v", rf_v) == 0
+    try:
+        _rmb_front_vs_two_kernel(gpu, R)
+    finally:
+        L.trk_set_tuning(b"rf_v", 2)
+
+
+def _rmb_front_vs_two_kernel(gpu, R):
     from importlib import import_module
     ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
     g = torch.Generator().manual_seed(R)
