@@ -41,6 +41,7 @@ int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column s
                      // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
 int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + rf_pf, 0: none (GEMM1
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
+int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
 int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
@@ -1147,6 +1148,7 @@ struct RfArgs {
   int64_t R;            // ROIs
   int pf;               // trk_set_tuning("rf_pf"): L2 prefetch distance in ROIs (X rows of ROI + pf), 0 = none
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
+  int lag;              // trk_set_tuning("rf_lag"), rf2_body: half B starts GEMM1 once A is past K step lag
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
@@ -1657,8 +1659,15 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     }
   };
   __builtin_amdgcn_s_setprio(1);
-  if (half == 0) gemm1(std::integral_constant<int, 0>{});
-  else gemm1(std::integral_constant<int, 1>{});
+  if (half == 0) {
+    gemm1(std::integral_constant<int, 0>{});
+  } else {
+    // B starts behind A (rf_lag K steps; 16 = after A's whole GEMM1): run together, the
+    // two halves share every SIMD's matrix pipe and reach their VALU phases together
+    if (a.lag >= 16) rf2_wait(ctr + RF2_CG1 + 0, 4);
+    else if (a.lag > 0) rf2_wait(ctr + RF2_CX + a.lag / 4, 4);
+    gemm1(std::integral_constant<int, 1>{});
+  }
   __builtin_amdgcn_s_setprio(0);
   rf2_signal(ctr + RF2_CG1 + half, lane);  // this wave's reads of X are done
   if (prof) {
@@ -2042,6 +2051,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.R = M / RF_S;
   a.pf = g_rf_pf;
   a.prof = g_enc_prof;
+  a.lag = g_rf_lag;
   if (g_rf_v == 2) {
     hipLaunchKernelGGL(rmb_front2_kernel, dim3((unsigned)nwg), dim3(512), RF2_LDS,
                        reinterpret_cast<hipStream_t>(stream), a);

@@ -37,6 +37,17 @@ __device__ __forceinline__ unsigned long long hd_stamp() {
 constexpr int RB = 16;        // ROIs per workgroup
 constexpr int MAXC = 1024;    // channel bound (LDS sizing)
 
+// LDS rows of the 16-ROI tiles: ld = C rounded up to 64 floats (a row is a whole number
+// of 256-B bank rows) and 16-B chunk q of row r at chunk q ^ (r & 15) (within its aligned
+// group of 16 chunks).  The MFMA A reads (lane (r, g) takes chunk kb / 4 + g of row r,
+// served in the lane groups of MI355X_MICROARCH.md §LDS) and the callbacks' row writes
+// then hit 16 distinct chunks per group: the padded rows (ld = C + 4) were 2-way
+// (SQ_LDS_BANK_CONFLICT 3.4 cycles per LDS instruction in enc_se, 2.0 in enc_head)
+__host__ __device__ inline int ld_rows(int c) { return (c + 63) & ~63; }
+__device__ __forceinline__ int swz_at(int row, int col, int ld) {
+  return row * ld + (((col >> 2) ^ (row & 15)) << 2) + (col & 3);
+}
+
 // acc[t] (t < NT) += X[16][K] . W[n0 + 16 t .. + 15][K]^T.  K is walked in
 // chunks of U blocks of 16; chunk c + 1's weight and activation loads (NT x U + U
 // 16-B loads per lane, into the other register buffer) are issued before chunk c's
@@ -48,13 +59,19 @@ struct RbBuf {
 };
 
 template <int NT, int U>
-__device__ __forceinline__ void rb_load(const float* xp, const float* const (&wp)[NT], int kb0, RbBuf<NT, U>& d) {
+__device__ __forceinline__ void rb_load(const float* xp, int xq, const float* const (&wp)[NT], int kb0,
+                                        RbBuf<NT, U>& d) {
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int t = 0; t < NT; ++t) d.b[u][t] = *reinterpret_cast<const float4*>(wp[t] + kb0 + 16 * u);
+  // A: chunk (kb / 4 + g) ^ (r & 15) of row r = the chunk group kb / 64 plus ((kb / 4) & 15) ^ xq
+  // (kb / 4 is a multiple of 4 and g < 4, so kb / 4 + g = kb / 4 ^ g; xq = g ^ (r & 15))
 #pragma unroll
-  for (int u = 0; u < U; ++u) d.a[u] = *reinterpret_cast<const float4*>(xp + kb0 + 16 * u);
+  for (int u = 0; u < U; ++u) {
+    const int q = (kb0 + 16 * u) >> 2;
+    d.a[u] = *reinterpret_cast<const float4*>(xp + (((q & ~15) | ((q & 15) ^ xq)) << 2));
+  }
 }
 
 template <int NT, int U>
@@ -78,18 +95,19 @@ __device__ __forceinline__ void rb_gemm(const float* __restrict__ Xs, int ldx, c
   const float* wp[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) wp[t] = W + (int64_t)(n0 + 16 * t + r) * ldw + 4 * g;
-  const float* xp = Xs + r * ldx + 4 * g;
+  const float* xp = Xs + r * ldx;  // swizzled row (swz_at)
+  const int xq = g ^ (r & 15);
   const int nch = K / KC;
   if (nch > 0) {
     RbBuf<NT, U> b0, b1;
-    rb_load<NT, U>(xp, wp, 0, b0);
+    rb_load<NT, U>(xp, xq, wp, 0, b0);
     int c = 0;
     for (;;) {
-      if (c + 1 < nch) rb_load<NT, U>(xp, wp, (c + 1) * KC, b1);
+      if (c + 1 < nch) rb_load<NT, U>(xp, xq, wp, (c + 1) * KC, b1);
       __builtin_amdgcn_sched_barrier(0);
       rb_mfma<NT, U>(b0, acc);
       if (++c == nch) break;
-      if (c + 1 < nch) rb_load<NT, U>(xp, wp, (c + 1) * KC, b0);
+      if (c + 1 < nch) rb_load<NT, U>(xp, xq, wp, (c + 1) * KC, b0);
       __builtin_amdgcn_sched_barrier(0);
       rb_mfma<NT, U>(b1, acc);
       if (++c == nch) break;
@@ -97,7 +115,7 @@ __device__ __forceinline__ void rb_gemm(const float* __restrict__ Xs, int ldx, c
   }
   for (int kb = nch * KC; kb < K; kb += 16) {
     RbBuf<NT, 1> t1;
-    rb_load<NT, 1>(xp, wp, kb, t1);
+    rb_load<NT, 1>(xp, xq, wp, kb, t1);
     rb_mfma<NT, 1>(t1, acc);
   }
 }
@@ -162,9 +180,9 @@ struct SeArgs {
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) enc_se_kernel(const SeArgs a) {
   extern __shared__ __align__(16) float lds[];
-  const int C = a.C, H = a.H, ldx = C + 4, ldh = H + 4;
-  float* Xs = lds;                 // [16][C + 4] m_r
-  float* Hs = lds + RB * ldx;      // [16][H + 4] relu(W1 m_r + b1)
+  const int C = a.C, H = a.H, ldx = ld_rows(C), ldh = ld_rows(H);
+  float* Xs = lds;                 // [16][ldx] m_r (swz_at rows)
+  float* Hs = lds + RB * ldx;      // [16][ldh] relu(W1 m_r + b1)
   const int64_t r0 = (int64_t)blockIdx.x * RB;
   const int nrow = (int)min<int64_t>(RB, a.R - r0);
   // 4 channels per item, all of a thread's loads in flight together
@@ -192,10 +210,10 @@ __global__ void __launch_bounds__(64 * NW) enc_se_kernel(const SeArgs a) {
       *reinterpret_cast<float4*>(a.m_n + (r0 + rr) * C + c) =
           make_float4(fix_mean(n01.x, a.P), fix_mean(n01.y, a.P), fix_mean(n23.x, a.P), fix_mean(n23.y, a.P));
     }
-    *reinterpret_cast<float4*>(Xs + rr * ldx + c) = mr;
+    *reinterpret_cast<float4*>(Xs + swz_at(rr, c, ldx)) = mr;
   }
   __syncthreads();
-  rb_linear<NW>(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[row * ldh + col] = fmaxf(v, 0.f); });
+  rb_linear<NW>(Xs, ldx, a.w1, a.b1, H, C, [&](int row, int col, float v) { Hs[swz_at(row, col, ldh)] = fmaxf(v, 0.f); });
   __syncthreads();
   // hardsigmoid (torch: min(max(x + 3, 0), 6) / 6), straight to global
   float* __restrict__ sout = a.s;
@@ -220,13 +238,12 @@ __device__ __forceinline__ void ln_silu_rows(const float* Zs, float* Gs, int ldx
     lb[q] = c < C ? ln_b[c] : 0.f;
   }
   for (int rr = wave; rr < RB; rr += NW) {
-    const float* z = Zs + rr * ldx;
     float zv[QL];
     float sum = 0.f;
 #pragma unroll
     for (int q = 0; q < QL; ++q) {
       const int c = lane + 64 * q;
-      zv[q] = c < C ? z[c] : 0.f;
+      zv[q] = c < C ? Zs[swz_at(rr, c, ldx)] : 0.f;
       if (c < C) sum += zv[q];
     }
 #pragma unroll
@@ -246,7 +263,7 @@ __device__ __forceinline__ void ln_silu_rows(const float* Zs, float* Gs, int ldx
       const int c = lane + 64 * q;
       if (c < C) {
         const float y = (zv[q] - mean) * rstd * lw[q] + lb[q];
-        Gs[rr * ldx + c] = y / (1.0f + expf(-y));
+        Gs[swz_at(rr, c, ldx)] = y / (1.0f + expf(-y));
       }
     }
   }
@@ -266,10 +283,10 @@ struct HeadArgs {
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) enc_head_kernel(const HeadArgs a) {
   extern __shared__ __align__(16) float lds[];
-  const int C = a.C, D = a.D, ldx = C + 4, ldd = D + 4;
-  float* Gs = lds;                  // [16][C + 4] g, then silu(LN(z))
-  float* Zs = lds + RB * ldx;       // [16][C + 4] z = W0 g
-  float* Ys = Zs + RB * ldx;        // [16][D + 4] W4 . + b4
+  const int C = a.C, D = a.D, ldx = ld_rows(C), ldd = ld_rows(D);
+  float* Gs = lds;                  // [16][ldx] g, then silu(LN(z)) (swz_at rows)
+  float* Zs = lds + RB * ldx;       // [16][ldx] z = W0 g
+  float* Ys = Zs + RB * ldx;        // [16][ldd] W4 . + b4
   const int64_t r0 = (int64_t)blockIdx.x * RB;
   const int nrow = (int)min<int64_t>(RB, a.R - r0);
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -304,11 +321,11 @@ __global__ void __launch_bounds__(64 * NW) enc_head_kernel(const HeadArgs a) {
         gv[e] = 0.5f * mcat + 0.5f * x2;
       }
     }
-    *reinterpret_cast<float4*>(Gs + rr * ldx + c) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+    *reinterpret_cast<float4*>(Gs + swz_at(rr, c, ldx)) = make_float4(gv[0], gv[1], gv[2], gv[3]);
   }
   __syncthreads();
   if (a.prof) pt[1] = hd_stamp();
-  rb_linear<NW>(Gs, ldx, a.w0, nullptr, C, C, [&](int row, int col, float v) { Zs[row * ldx + col] = v; });
+  rb_linear<NW>(Gs, ldx, a.w0, nullptr, C, C, [&](int row, int col, float v) { Zs[swz_at(row, col, ldx)] = v; });
   __syncthreads();
   if (a.prof) pt[2] = hd_stamp();
   // LayerNorm over C (biased variance, eps inside the sqrt) + SiLU: wave w owns rows w, w + NW, ...
@@ -320,19 +337,21 @@ __global__ void __launch_bounds__(64 * NW) enc_head_kernel(const HeadArgs a) {
   }
   __syncthreads();
   if (a.prof) pt[3] = hd_stamp();
-  rb_linear<NW>(Gs, ldx, a.w4, a.b4, D, C, [&](int row, int col, float v) { Ys[row * ldd + col] = v; });
+  rb_linear<NW>(Gs, ldx, a.w4, a.b4, D, C, [&](int row, int col, float v) { Ys[swz_at(row, col, ldd)] = v; });
   __syncthreads();
   if (a.prof) pt[4] = hd_stamp();
   // F.normalize(dim=1): y / max(||y||, 1e-12)
   for (int rr = wave; rr < RB; rr += NW) {
-    const float* y = Ys + rr * ldd;
     float sq = 0.f;
-    for (int c = lane; c < D; c += 64) sq += y[c] * y[c];
+    for (int c = lane; c < D; c += 64) {
+      const float yc = Ys[swz_at(rr, c, ldd)];
+      sq += yc * yc;
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
     const float nrm = fmaxf(sqrtf(sq), 1e-12f);
     if (rr < nrow)
-      for (int c = lane; c < D; c += 64) a.out[(r0 + rr) * D + c] = y[c] / nrm;
+      for (int c = lane; c < D; c += 64) a.out[(r0 + rr) * D + c] = Ys[swz_at(rr, c, ldd)] / nrm;
   }
   if (a.prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -360,7 +379,7 @@ extern "C" int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int
   TRK_REQUIRE(al16(sums) && al16(w1) && al16(w2) && al16(m_r) && al16(m_n) && al16(s),
               "enc_se: operands must be 16-byte aligned");
   SeArgs a{sums, ld_sums, w1, b1, w2, b2, m_r, m_n, s, (int)R, (int)C, (int)H, (int)P, (float)P};
-  const size_t lds = (size_t)RB * ((C + 4) + (H + 4)) * 4;
+  const size_t lds = (size_t)RB * (ld_rows((int)C) + ld_rows((int)H)) * 4;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<8>),
@@ -391,7 +410,7 @@ extern "C" int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_
               "enc_head: operands must be 16-byte aligned");
   HeadArgs a{tsums, s, m_r, m_n, w0, ln_w, ln_b, w4, b4, out, (int)R, (int)C, (int)D, (int)P, (float)P, ln_eps, alpha,
              g_head_prof};
-  const size_t lds = (size_t)RB * (2 * (C + 4) + (D + 4)) * 4;
+  const size_t lds = (size_t)RB * (2 * ld_rows((int)C) + ld_rows((int)D)) * 4;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_head_kernel<8>),

@@ -693,20 +693,22 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         assert (d == 0).float().mean().item() >= 0.9
 
 
-@pytest.mark.parametrize("rf_v", [2, 1])
+@pytest.mark.parametrize("rf_v,rf_lag", [(2, 16), (2, 8), (2, 0), (1, 16)])
 @pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v):
+def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag):
     """trk_enc_rmb_front (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
     LDS) vs enc_g1_dwconv -> enc_dsc_gemm: the same MFMA shape, K order and bf16
     roundings, so XRN must be bit-identical; the ROI sums add the same f32 activations in
     another order (tol 1e-5 of the largest sum).  R = 2048 is the bench's c3 launch.
-    rf_v 2 (default): the two wave halves hand off through LDS counters; 1: lockstep."""
+    rf_v 2 (default): the two wave halves hand off through LDS counters, half B starting
+    GEMM1 rf_lag K steps behind half A; 1: lockstep phases."""
     L = trk.lib()
-    assert L.trk_set_tuning(b"rf_v", rf_v) == 0
+    assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf_lag", rf_lag) == 0
     try:
         _rmb_front_vs_two_kernel(gpu, R)
     finally:
         L.trk_set_tuning(b"rf_v", 2)
+        L.trk_set_tuning(b"rf_lag", 16)
 
 
 def _rmb_front_vs_two_kernel(gpu, R):

@@ -1,4 +1,4 @@
-"""Copy the judged summaries of one gpu_check.sh run from gpurun_out/ into
+"""Copy the judged summaries of one tools/gpu_round.sh run from gpurun_out/ into
 profiles/ (tracked): rocprofv3 kernel stats, the PMC traffic table and the
 bench JSON line."""
 import csv, json, os, shutil, sys

@@ -26,5 +26,5 @@ cd /tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv \
   -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline || exit $?
 cd "$ROOT"
-bash tools/gpu_pmc.sh "$TAG" > "$OUT/pmc_$TAG.txt" 2>&1 || exit $?
+bash tools/exp/gpu_pmc.sh "$TAG" > "$OUT/pmc_$TAG.txt" 2>&1 || exit $?
 echo "== done"
