@@ -1149,6 +1149,15 @@ struct RfArgs {
   int pf;               // trk_set_tuning("rf_pf"): L2 prefetch distance in ROIs (X rows of ROI + pf), 0 = none
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
   int lag;              // trk_set_tuning("rf_lag"), rf2_body: half B starts GEMM1 once A is past K step lag
+  // fused mode (trk_enc_rmb_fused: SE and the transition inside the kernel)
+  const uint4* Wtp;     // [32 k steps][32 col tiles][64 lanes] 16-B fragments of Wt [512][1024]
+  const float* bt;      // [512] transition bias
+  const float *se_w1, *se_b1, *se_w2, *se_b2;  // [128][512], [128], [512][128], [512] (f32)
+  uint16_t* XN;         // [R * 100][512] hand-off: the normal group's bf16 Hardswish(x_n)
+  int* flags;           // [R] the epoch the normal group's XN rows were published with
+  int epoch;
+  float *m_r, *m_n, *s; // [R][512] squeeze means and SE scales (trk_enc_se's outputs)
+  long long* tsums;     // [R][kPart][512] sums of SiLU(T) (partial 0; the others 0)
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
@@ -1532,8 +1541,13 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
 // and blocks 0..7 = A's output staging; B stages over Y(A) after both halves' GEMM2.
 constexpr int RF2_NB = 24;
 constexpr size_t RF2_CTR = (size_t)(RF2_NB - 1) * RF_KBS * 4 + 112 * 64;  // past block 23's row-111 reads
-enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16, RF2_NCTR = 20 };
+enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16,
+       RF3_CPUB = 18, RF3_CYF = 19, RF3_CH = 20, RF3_CS = 21, RF3_CYS = 22, RF2_NCTR = 32 };
 constexpr size_t RF2_LDS = RF2_CTR + RF2_NCTR * 4;
+// fused mode: the SE vectors after the counters (m_r, relu(W1 m_r + b1), s)
+constexpr size_t RF3_M = RF2_LDS, RF3_H = RF3_M + 512 * 4, RF3_S = RF3_H + 128 * 4;
+constexpr size_t RF3_LDS = RF3_S + 512 * 4;
+static_assert(RF3_LDS <= 160 * 1024, "one fused rmb workgroup per CU");
 constexpr int RF2_SROW = 128;  // output staging row (dwords): 256 channels, 16-B chunks XOR-swizzled by row
 static_assert(RF2_LDS <= 160 * 1024, "one rmb_front workgroup per CU");
 static_assert((size_t)RF_S * RF2_SROW * 4 <= (size_t)8 * RF_KBS * 4, "a half's staging fits 8 blocks");
@@ -1582,7 +1596,327 @@ __device__ __forceinline__ void rf2_wait(uint32_t* ctr, uint32_t target) {
       : "memory", "scc");
 }
 
+// ---- fused tail (trk_enc_rmb_fused): what trk_enc_se and trk_enc_transition_gemm did for
+// the ROI, inside the ROI's two workgroups.  acc holds the group's activated 64 x 112 tile.
+//   normal group (G = 1): m_n, then its bf16 Hardswish(x_n) rows -> XN with sc1 stores,
+//     each wave's stores retired, then the ROI's flag = epoch (one sc1 store).
+//   reinforce group (G = 0): m_r; bf16 SiLU(x_r) -> the LDS K-block image (blocks 0..15);
+//     SE (FC1: 4 threads per hidden unit, FC2: one thread per channel, f32 FMA chains);
+//     the image scaled in place, y = bf16(x_f * s) as gemm4<TRANS> stages it; then
+//     GEMM3 T = Wt . [y ; x_n] (K = 1024: the image, then the partner's XN rows polled
+//     for and loaded with sc1 loads into an 8-block LDS ring, blocks 16..23), + bias,
+//     SiLU, per-channel sums -> tsums.  The pair runs on one XCD (the grid is padded to a
+//     multiple of 16 workgroups), so the hand-off is an L2 round trip.
+// sc1 (agent-coherent) global access: stores drop their line from the writer's L2 and
+// loads bypass the reader's L1 (MI355X_MICROARCH.md, inter-workgroup hand-off table)
+__device__ __forceinline__ void rf3_store_sc1(uint16_t* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void rf3_load_sc1(const uint16_t* p, u32x4& v) {
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+}
+// poll the ROI's flag (sc1 loads) until it holds epoch; bounded like rf2_wait
+__device__ __forceinline__ void rf3_wait_flag(const int* flag, int epoch) {
+  uint32_t v, sv, n;
+  asm volatile(
+      "s_mov_b32 %[n], 0\n"
+      "1:\n\t"
+      "global_load_dword %[v], %[p], off sc1\n\t"
+      "s_waitcnt vmcnt(0)\n\t"
+      "v_readfirstlane_b32 %[s], %[v]\n\t"
+      "s_cmp_eq_u32 %[s], %[t]\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_add_u32 %[n], %[n], 1\n\t"
+      "s_cmp_gt_u32 %[n], %[lim]\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_sleep 2\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : [v] "=&v"(v), [s] "=&s"(sv), [n] "=&s"(n)
+      : [p] "v"(flag), [t] "s"(epoch), [lim] "s"(kRf2Spin)
+      : "memory", "scc");
+}
+
+// per-channel sums of the wave's activated tile (rf_body's lane / DPP order); lanes fr == 0
+// end up with the sums of channels 16 t + 4 fc + e
+__device__ __forceinline__ void rf3_colsums(const f4v (&acc)[7][4], int fr, float (&sv)[4][4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = 0.f;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) x += acc[i][t][e];
+      if (fr < 4) x += acc[6][t][e];
+      x += lane_xor1(x);
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // ^2
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));  // row_ror 4
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, true));  // row_ror 8
+      sv[t][e] = x;
+    }
+  }
+}
+// the squeeze mean of a sum as trk_enc_se takes it: (float)(llrint(sum * 2^24) * 2^-24) / 100
+__device__ __forceinline__ float rf3_mean(float sum) {
+  return (float)((double)llrintf(sum * kFix) * (1.0 / 16777216.0)) / (float)RF_S;
+}
+
 template <int G>
+__device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned char* smem, f4v (&acc)[7][4]) {
+  uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2, hw = wave & 3;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int64_t r0 = roi * RF_S;
+  float sv[4][4];
+  rf3_colsums(acc, fr, sv);
+  if constexpr (G == 1) {
+    // ---- normal group: m_n, bf16 x_n rows -> XN (sc1), flag
+    if (fr == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        *reinterpret_cast<float4*>(a.m_n + roi * 512 + wave * 64 + t * 16 + fc * 4) =
+            make_float4(rf3_mean(sv[t][0]), rf3_mean(sv[t][1]), rf3_mean(sv[t][2]), rf3_mean(sv[t][3]));
+    }
+    if (half == 0) {
+      rf2_wait(ctr + RF2_CG1 + 1, 4);
+    } else {
+      rf2_wait(ctr + RF2_CG2 + 0, 4);
+      rf2_wait(ctr + RF2_CG2 + 1, 4);
+    }
+    uint32_t* stg = Y + (half ? 16 * RF_KBS : 0);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int px = i * 16 + fr;
+      if (px < RF_S) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f4v v = acc[i][t];
+          const int ch = hw * 64 + t * 16 + fc * 4;
+          *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((ch >> 3) ^ (px & 15)) << 2) + ((ch & 7) >> 1)) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+      }
+    }
+    rf2_signal(ctr + RF2_CST + half, lane);
+    rf2_wait(ctr + RF2_CST + half, 4);
+    uint16_t* dst = a.XN + r0 * 512 + half * 256;
+    const int ht = tid & 255;
+    for (int q = ht; q < RF_S * 32; q += 256) {
+      const int row = q >> 5, c = q & 31;
+      rf3_store_sc1(dst + (int64_t)row * 512 + c * 8,
+                    *reinterpret_cast<const u32x4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2)));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's XN stores retired
+    rf2_signal(ctr + RF3_CPUB, lane);
+    if (wave == 0) {
+      rf2_wait(ctr + RF3_CPUB, 8);  // every wave's stores retired: publish
+      if (lane == 0) __hip_atomic_store(a.flags + roi, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  } else {
+    float* Ms = reinterpret_cast<float*>(smem + RF3_M);
+    float* Hs = reinterpret_cast<float*>(smem + RF3_H);
+    float* Ss = reinterpret_cast<float*>(smem + RF3_S);
+    // ---- reinforce group: m_r (global + LDS), bf16 x_f -> the K-block image
+    if (fr == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 m = make_float4(rf3_mean(sv[t][0]), rf3_mean(sv[t][1]), rf3_mean(sv[t][2]), rf3_mean(sv[t][3]));
+        *reinterpret_cast<float4*>(a.m_r + roi * 512 + wave * 64 + t * 16 + fc * 4) = m;
+        *reinterpret_cast<float4*>(Ms + wave * 64 + t * 16 + fc * 4) = m;
+      }
+    }
+    // A's channels go to blocks 0..7 (X: dead once B is past GEMM1), B's to 8..15 (Y(B): dead
+    // once both halves are past GEMM2; the ring, blocks 16..23 = Y(A), likewise)
+    if (half == 0) {
+      rf2_wait(ctr + RF2_CG1 + 1, 4);
+    } else {
+      rf2_wait(ctr + RF2_CG2 + 0, 4);
+      rf2_wait(ctr + RF2_CG2 + 1, 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int px = i * 16 + fr;
+      if (px < RF_S) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f4v v = acc[i][t];
+          *reinterpret_cast<uint2*>(Y + rf_yaddr(px, wave * 64 + t * 16 + fc * 4)) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+      }
+    }
+    rf2_signal(ctr + RF3_CYF, lane);
+    // the partner's x_n: its flag, then (once every wave is past GEMM2: the ring is Y(A))
+    // LDS-DMA with sc1 of x_n K blocks into the ring, 4 blocks per group, one op per block
+    // per wave: lanes < 50 move pieces 50 wave + lane (row p >> 2, slot p & 3), as rf_body's X
+    rf3_wait_flag(a.flags + roi, a.epoch);
+    const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
+    const uint16_t* xsrc = a.XN + (r0 + xr) * 512 + (((xp & 3) ^ rf_sw(xr)) * 8);
+    auto ring_dma = [&](int grp) {  // x_n blocks 4 grp .. 4 grp + 3 -> slots (4 grp) & 7 ..
+      if (lane < 50) {
+        const uint16_t* xs = xsrc;
+        asm volatile("" : "+v"(xs));
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          __builtin_amdgcn_global_load_lds(GPTR(xs + (4 * grp + q) * BK),
+                                           LPTR(Y + (16 + ((4 * grp + q) & 7)) * RF_KBS + 200 * wave), 16, 0,
+                                           16 /* sc1 */);
+      }
+    };
+    rf2_wait(ctr + RF3_CYF, 8);  // m_r and the x_f image complete, every wave past GEMM2
+    ring_dma(0);
+    ring_dma(1);
+    // FC1 / FC2 as 8-lane row groups: lane l of a group takes k = 32 kk + 4 l .. + 3, so one
+    // load instruction covers 8 rows x 128 contiguous bytes; the 8 partials are added by
+    // two DPP steps and one xor-4 shuffle (f32, another order than trk_enc_se's MFMA: ulps)
+    const int l8 = lane & 7, g8 = lane >> 3;
+    auto sum8 = [&](float x) {
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));  // quad [1,0,3,2]
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));  // quad [2,3,0,1]
+      return x + __shfl_xor(x, 4);
+    };
+    // FC1: h[j] = relu(b1[j] + W1[j] . m_r), rows j = 16 wave + 8 p + g8
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int j = 16 * wave + 8 * p + g8;
+      const float* w = a.se_w1 + j * 512 + 4 * l8;
+      float h = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
+        const float4 mv = *reinterpret_cast<const float4*>(Ms + 32 * kk + 4 * l8);
+        h = __builtin_fmaf(wv.x, mv.x, h);
+        h = __builtin_fmaf(wv.y, mv.y, h);
+        h = __builtin_fmaf(wv.z, mv.z, h);
+        h = __builtin_fmaf(wv.w, mv.w, h);
+      }
+      h = sum8(h);
+      if (l8 == 0) Hs[j] = fmaxf(h + a.se_b1[j], 0.f);
+    }
+    rf2_signal(ctr + RF3_CH, lane);
+    rf2_wait(ctr + RF3_CH, 8);
+    // FC2: s[c] = hardsigmoid(b2[c] + W2[c] . h), rows c = 64 wave + 8 p + g8
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int c = 64 * wave + 8 * p + g8;
+      const float* w = a.se_w2 + c * 128 + 4 * l8;
+      float x = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
+        const float4 hv = *reinterpret_cast<const float4*>(Hs + 32 * kk + 4 * l8);
+        x = __builtin_fmaf(wv.x, hv.x, x);
+        x = __builtin_fmaf(wv.y, hv.y, x);
+        x = __builtin_fmaf(wv.z, hv.z, x);
+        x = __builtin_fmaf(wv.w, hv.w, x);
+      }
+      x = sum8(x);
+      if (l8 == 0) {
+        const float sc = fminf(fmaxf(x + a.se_b2[c] + 3.0f, 0.f), 6.0f) / 6.0f;
+        Ss[c] = sc;
+        a.s[roi * 512 + c] = sc;
+      }
+    }
+    rf2_signal(ctr + RF3_CS, lane);
+    rf2_wait(ctr + RF3_CS, 8);
+    // y = bf16(float(bf16 x_f) * s) in place: thread t takes channel chunk t & 63 (8 channels,
+    // block (t & 63) >> 2, chunk t & 3) of rows (t >> 6) + 8 i
+    {
+      const int cc = tid & 63, kb = cc >> 2, c4 = cc & 3;
+      float sc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sc[e] = Ss[cc * 8 + e];
+#pragma unroll
+      for (int i = 0; i < 13; ++i) {
+        const int px = (tid >> 6) + 8 * i;
+        if (px < RF_S) {
+          u32x4* pp = reinterpret_cast<u32x4*>(Y + kb * RF_KBS + px * 16 + ((c4 ^ rf_sw(px)) << 2));
+          const u32x4 v = *pp;
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * sc[2 * e], __uint_as_float(v[e] & 0xffff0000u) * sc[2 * e + 1]);
+          *pp = o;
+        }
+      }
+    }
+    rf2_signal(ctr + RF3_CYS, lane);
+    rf2_wait(ctr + RF3_CYS, 8);
+    // ---- GEMM3: K steps 0..15 over the image, 16..31 over the ring.  Ring groups 0 and 1
+    // (slots 0..7) were issued before the SE, 2 (slots 0..3) at step 20, 3 (4..7) at step 24,
+    // each behind the barrier that ends the reads of the slots' previous group; barriers at
+    // 16, 24, 28 publish the groups
+    constexpr int NK3 = 32;
+    const uint4* b3p = a.Wtp + (size_t)(wave * 4) * 64 + lane;
+    u32x4 bq[3][4];
+    const int lterm = fr * 4 + (fc ^ rf_sw(fr));
+    const uint32_t y_a = lds_addr(Y) + lterm * 16;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+    float4 bias4[4];
+    rf_loadB(b3p, 0, bq[0]);
+    rf_loadB(b3p, 1, bq[1]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kt = 0; kt < NK3; ++kt) {
+      u32x4(&b)[4] = bq[kt % 3];
+      // vmcnt(0) retires this wave's ring DMA before the barrier that publishes it (groups 0-1
+      // at step 0 for 16, 2 at 24, 3 at 28); steps 21 / 25 count the group issued one step before
+      const bool rs = kt == 0 || kt == 24 || kt == 28;
+      rf_vmwait(rs ? 0 : (kt + 1 < NK3 ? 4 + ((kt == 21 || kt == 25) ? 4 : 0) : 0), b);
+      if (kt == 16 || kt == 20 || kt == 24 || kt == 28) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        g4_barrier();
+      }
+      if (kt == 20) ring_dma(2);  // slots 0..3: their group 0 was read in steps 16..19
+      if (kt == 24) ring_dma(3);  // slots 4..7: group 1, steps 20..23
+      if (kt + 2 < NK3) rf_loadB(b3p, kt + 2, bq[(kt + 2) % 3]);
+      if (kt == NK3 - 3) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          bias4[t] = *reinterpret_cast<const float4*>(a.bt + wave * 64 + t * 16 + fc * 4);
+      }
+      const int blk = kt < 16 ? kt : 16 + ((kt - 16) & 7);
+      rf_mfma_step(y_a + blk * RF_KBS * 4, b, acc);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    // ---- SiLU(T + bias) and its per-channel sums over the ROI -> tsums
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
+          v = silu2(v);
+          acc[i][t][2 * h] = v.x;
+          acc[i][t][2 * h + 1] = v.y;
+        }
+    }
+    rf3_colsums(acc, fr, sv);
+    if (fr == 0) {
+      const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        long long* o = a.tsums + roi * kPart * 512 + wave * 64 + t * 16 + fc * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[t][e] * kFix);
+        for (int j = 1; j < cnt; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[j * 512 + e] = 0;
+      }
+    }
+  }
+}
+
+template <int G, int MODE>
 __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned char* smem) {
   const int64_t roi = lb >> 1;
   unsigned long long pst[8];
@@ -1792,6 +2126,10 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
         acc[i][t][2 * h + 1] = v.y;
       }
   }
+  if constexpr (MODE == 1) {
+    rf3_tail<G>(a, roi, smem, acc);
+    return;
+  }
   {
     const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
 #pragma unroll
@@ -1880,8 +2218,17 @@ __global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
 __global__ void __launch_bounds__(512, 1) rmb_front2_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  if (lb & 1) rf2_body<1>(a, lb, smem);
-  else rf2_body<0>(a, lb, smem);
+  if (lb & 1) rf2_body<1, 0>(a, lb, smem);
+  else rf2_body<0, 0>(a, lb, smem);
+}
+// fused: rmb_front + SE + transition; the grid is padded to a multiple of 16 workgroups so
+// xcd_remap never splits a ROI's pair across XCDs (the pair hands x_n over through L2)
+__global__ void __launch_bounds__(512, 1) rmb_fused_kernel(RfArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  if ((lb >> 1) >= a.R) return;
+  if (lb & 1) rf2_body<1, 1>(a, lb, smem);
+  else rf2_body<0, 1>(a, lb, smem);
 }
 
 template <int EPI>
@@ -2060,6 +2407,55 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
                      a);
   return trk::check_launch("rmb_front_kernel");
+}
+
+extern "C" int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                                 const float* bias, const void* Wtp, const float* bt, const float* se_w1,
+                                 const float* se_b1, const float* se_w2, const float* se_b2, void* xn_work,
+                                 int* flags, int epoch, float* m_r, float* m_n, float* s, long long* tsums,
+                                 void* stream) {
+  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_fused: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
+  if (M == 0) return TRK_OK;
+  TRK_REQUIRE(X && W1p && wdw && W2p && bias && Wtp && bt && se_w1 && se_b1 && se_w2 && se_b2 && xn_work && flags &&
+                  m_r && m_n && s && tsums,
+              "enc_rmb_fused: null pointer");
+  TRK_REQUIRE(aligned16(X) && aligned16(W1p) && aligned16(W2p) && aligned16(Wtp) && aligned16(wdw) &&
+                  aligned16(bt) && aligned16(se_w1) && aligned16(se_w2) && aligned16(xn_work) && aligned16(m_r) &&
+                  aligned16(m_n) && aligned16(s) && aligned16(tsums),
+              "enc_rmb_fused: operands must be 16-byte aligned");
+  TRK_REQUIRE(epoch != 0, "enc_rmb_fused: epoch must differ from the flags' initial 0");
+  const int64_t R = M / RF_S;
+  // pairs (2 roi, 2 roi + 1) stay on one XCD under xcd_remap when every XCD's range starts
+  // at an even id: a grid that is a multiple of 16 (the padding workgroups exit at once)
+  const int64_t nwg = (2 * R + 15) / 16 * 16;
+  TRK_REQUIRE(nwg < 0x7fffffff, "enc_rmb_fused: too many workgroups");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_fused_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF3_LDS);
+    attr = true;
+  }
+  RfArgs a;
+  memset(&a, 0, sizeof a);
+  a.X = (const uint16_t*)X;
+  a.W1p = (const uint4*)W1p;
+  a.wdw = wdw;
+  a.W2p = (const uint4*)W2p;
+  a.bias = bias;
+  a.R = R;
+  a.pf = g_rf_pf;
+  a.lag = g_rf_lag;
+  a.Wtp = (const uint4*)Wtp;
+  a.bt = bt;
+  a.se_w1 = se_w1; a.se_b1 = se_b1; a.se_w2 = se_w2; a.se_b2 = se_b2;
+  a.XN = (uint16_t*)xn_work;
+  a.flags = flags;
+  a.epoch = epoch;
+  a.m_r = m_r; a.m_n = m_n; a.s = s;
+  a.tsums = tsums;
+  hipLaunchKernelGGL(rmb_fused_kernel, dim3((unsigned)nwg), dim3(512), RF3_LDS, reinterpret_cast<hipStream_t>(stream),
+                     a);
+  return trk::check_launch("rmb_fused_kernel");
 }
 
 // diagnostics: gemm4 per-workgroup phase stamps (8 u64 per workgroup); nullptr

@@ -79,13 +79,29 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
   return base + bid / nx;
 }
 
+// (frame, channel tile, pixel tile) of a transpose block: the 1-D grid is XCD-remapped
+// like roi_sweep_kernel's, so with B = 8 frames each frame's NHWC copy is written by (and
+// stays in the L2 of) the XCD whose roi_sweep blocks read it next
+struct TBlk { int64_t b; int cy, px; };
+__device__ __forceinline__ TBlk tblk(int gx, int gy) {
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t per = (int64_t)gx * gy;
+  TBlk t;
+  t.b = lb / per;
+  const int rem = (int)(lb - t.b * per);
+  t.cy = rem / gx;
+  t.px = rem - t.cy * gx;
+  return t;
+}
+
 __global__ void __launch_bounds__(256)
 nchw_to_nhwc_kernel(const float* __restrict__ in, float* __restrict__ out,
-                    int64_t C, int64_t HW) {
-  // tile: 64 channels x 64 pixels through LDS; blockIdx.z = batch
+                    int64_t C, int64_t HW, int gx, int gy) {
+  // tile: 64 channels x 64 pixels through LDS
   __shared__ float tile[64][65];
-  const int64_t b = blockIdx.z;
-  const int64_t c0 = (int64_t)blockIdx.y * 64, p0 = (int64_t)blockIdx.x * 64;
+  const TBlk tb = tblk(gx, gy);
+  const int64_t b = tb.b;
+  const int64_t c0 = (int64_t)tb.cy * 64, p0 = (int64_t)tb.px * 64;
   const float* src = in + b * C * HW;
   float* dst = out + b * C * HW;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 4 rows per pass
@@ -105,10 +121,11 @@ nchw_to_nhwc_kernel(const float* __restrict__ in, float* __restrict__ out,
 // consecutive channels of one pixel (256 B each); the 4 x 4 element turn goes
 // through the LDS tile.  HBM-bound: 2 x 4 B per element.
 __global__ void __launch_bounds__(256)
-nchw_to_nhwc4_kernel(const float* __restrict__ in, float* __restrict__ out, int C, int HW) {
+nchw_to_nhwc4_kernel(const float* __restrict__ in, float* __restrict__ out, int C, int HW, int gx, int gy) {
   __shared__ float tile[64][65];
-  const int64_t b = blockIdx.z;
-  const int c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+  const TBlk tb = tblk(gx, gy);
+  const int64_t b = tb.b;
+  const int c0 = tb.cy * 64, p0 = tb.px * 64;
   const float* src = in + b * (int64_t)C * HW;
   float* dst = out + b * (int64_t)C * HW;
   const int q = threadIdx.x & 15, r0 = threadIdx.x >> 4;
@@ -940,12 +957,14 @@ extern "C" int trk_nchw_to_nhwc(const float* in, int64_t B, int64_t C, int64_t H
   TRK_REQUIRE(in && out, "nchw_to_nhwc: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t HW = H * W;
-  dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)B);
+  const int gx = (int)((HW + 63) / 64), gy = (int)((C + 63) / 64);
+  TRK_REQUIRE((int64_t)gx * gy * B < ((int64_t)1 << 31), "nchw_to_nhwc: too many blocks");
+  const dim3 grid((unsigned)((int64_t)gx * gy * B));
   if (HW % 4 == 0 && C % 4 == 0 && trk::aligned16_ptr(in) && trk::aligned16_ptr(out)) {
-    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, grid, dim3(256), 0, st, in, out, (int)C, (int)HW);
+    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, grid, dim3(256), 0, st, in, out, (int)C, (int)HW, gx, gy);
     return trk::check_launch("nchw_to_nhwc4_kernel");
   }
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, st, in, out, C, HW);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, st, in, out, C, HW, gx, gy);
   return trk::check_launch("nchw_to_nhwc_kernel");
 }
 

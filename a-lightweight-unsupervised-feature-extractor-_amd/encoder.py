@@ -171,6 +171,9 @@ class Model(nn.Module):
                 w["w2_pk"] = enc_pack_fragments(w["w2_nk"])
             w["b2"] = torch.cat([w["br"].float(), w["bn"].float()]).to(device, torch.float32)
             w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
+            if tuple(w["wt_nk"].shape) == (512, 1024):
+                from .ops import enc_pack_fragments_k                                # rmb_fused's GEMM3
+                w["wt_pk"] = enc_pack_fragments_k(w["wt_nk"])
             w["bt_f"] = r.transition[0].bias.float().to(device)
             w["bt"] = r.transition[0].bias.to(device, dtype)
             # f32 operands of the per-ROI tail kernels (enc_se / enc_head)
@@ -220,6 +223,8 @@ class Model(nn.Module):
     fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel
                          # (enc_rmb_front; Y2 never reaches HBM); False: enc_g1_dwconv + enc_dsc_gemm
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
+    fused_full = False   # with fused_front and fused_tail: the SE and the transition GEMM inside the
+                         # front kernel too (enc_rmb_fused; the [M, 1024] XRN never reaches HBM)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
     stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
                          # enqueued (a caller can record an event there to place other streams' work)
@@ -227,7 +232,7 @@ class Model(nn.Module):
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_rmb_front, enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
+                          enc_rmb_front, enc_rmb_fused, enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -240,6 +245,15 @@ class Model(nn.Module):
                  h2 % 32 == 0 and Co % 256 == 0)
         front = (fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_front and
                  "w1_pk" in W and Co == 512)
+        if front and self.fused_tail and self.fused_full and "wt_pk" in W:
+            m_r, m_n, s, tsums = enc_rmb_fused(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"], W["wt_pk"], W["bt_f"],
+                                               W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+            if self.stage_hook is not None:
+                self.stage_hook("g1")
+                self.stage_hook("dsc")
+            head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
+                                    self.head.net[1].eps, W["h4"], W["h4b"])
+            return DeferredHead(head, (tsums, s, m_r, m_n)) if self.defer_head else head()
         if front:
             XRN, sums = enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
             if self.stage_hook is not None:

@@ -185,6 +185,15 @@ def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor,
     return XRN, f[:, :Ng], f[:, Ng:]
 
 
+def enc_pack_fragments_k(W: torch.Tensor) -> torch.Tensor:
+    """[N, K] bf16 weights -> the 16x16x32 MFMA A-fragment order of trk_enc_rmb_fused's
+    transition: [K/32 k steps][N/16 col tiles][64 lanes][8], element (s, n, l, j) =
+    W[16n + l%16][32s + 8(l//16) + j]."""
+    N, K = W.shape
+    W = W.reshape(N // 16, 16, K // 32, 4, 8)                 # n, fr, s, fc, j
+    return W.permute(2, 0, 3, 1, 4).contiguous()               # s, n, fc, fr, j  (lane = 16 fc + fr)
+
+
 def enc_pack_fragments(W: torch.Tensor) -> torch.Tensor:
     """[2*512, 512] (or [2, 512, 512]) bf16 weights [N][K] -> the 16x16x32 MFMA
     fragment order trk_enc_rmb_front reads: [2][16 k steps][32 col tiles][64 lanes][8],
@@ -215,6 +224,44 @@ def enc_rmb_front(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: to
                                   _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(sums),
                                   _stream(X.device)), "enc_rmb_front")
     return XRN, sums
+
+
+def enc_rmb_fused(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor, bias: torch.Tensor,
+                  Wtp: torch.Tensor, bt: torch.Tensor, se_w1: torch.Tensor, se_b1: torch.Tensor,
+                  se_w2: torch.Tensor, se_b2: torch.Tensor):
+    """enc_rmb_front + enc_se + enc_transition_gemm in one kernel (bf16, 10x10 ROIs of 512
+    channels): X [R*100, 512]; W1p / W2p from enc_pack_fragments, Wtp = enc_pack_fragments_k(Wt
+    [512, 1024]); wdw [25, 1024], bias [1024], bt [512], SE weights f32 -> (m_r, m_n, s [R, 512]
+    f32, tsums [R, TRK_ENC_PARTS, 512] int64): enc_se's and enc_transition_gemm(raw=True)'s
+    outputs, for enc_head."""
+    _need_gpu(X, "enc_rmb_fused")
+    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16 or \
+            Wtp.dtype != torch.bfloat16:
+        raise TypeError("enc_rmb_fused: bf16 operands required")
+    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
+        raise ValueError("enc_rmb_fused: X must be contiguous [R*100, 512]")
+    pk = (2, 16, 32, 4, 16, 8)
+    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or tuple(Wtp.shape) != (32, 32, 4, 16, 8):
+        raise ValueError("enc_rmb_fused: W1p / W2p [2, 16, 32, 4, 16, 8] (enc_pack_fragments), "
+                         "Wtp [32, 32, 4, 16, 8] (enc_pack_fragments_k)")
+    if wdw.shape != (25, 1024) or bias.numel() != 1024 or bt.numel() != 512 or tuple(se_w1.shape) != (128, 512) \
+            or tuple(se_w2.shape) != (512, 128) or se_b1.numel() != 128 or se_b2.numel() != 512:
+        raise ValueError("enc_rmb_fused: shape mismatch")
+    M = X.shape[0]
+    R = M // 100
+    dev = X.device
+    # per call: the hand-off workspace and flags (zeroed: epoch 1 is then fresh), so launches
+    # on different streams never share them
+    xn = torch.empty((M, 512), device=dev, dtype=torch.bfloat16)
+    flags = torch.zeros(max(R, 1), device=dev, dtype=torch.int32)
+    out = torch.empty((3, R, 512), device=dev, dtype=torch.float32)
+    tsums = torch.empty((R, _lib.TRK_ENC_PARTS, 512), device=dev, dtype=torch.int64)
+    c = lambda t: _f32c(t)
+    check(lib().trk_enc_rmb_fused(_ptr(X), M, _ptr(W1p), _ptr(c(wdw)), _ptr(W2p), _ptr(c(bias)), _ptr(Wtp),
+                                  _ptr(c(bt)), _ptr(c(se_w1)), _ptr(c(se_b1)), _ptr(c(se_w2)), _ptr(c(se_b2)),
+                                  _ptr(xn), _ptr(flags), 1, _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _ptr(tsums),
+                                  _stream(dev)), "enc_rmb_fused")
+    return out[0], out[1], out[2], tsums
 
 
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,

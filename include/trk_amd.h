@@ -60,6 +60,10 @@ const char* trk_last_error(void);
  *                    prefetched into L2; 4: without the prefetch
  *   "rf_pf"          8 (default): trk_enc_rmb_front prefetches the X rows of ROI + rf_pf into
  *                    L2 (0..64; 0: no prefetch)
+ *   "rf_v"           2 (default): trk_enc_rmb_front's wave halves hand off through LDS counters
+ *                    (decoupled phases); 1: lockstep phases (both bit-identical)
+ *   "rf_lag"         16 (default): with rf_v 2 (and in trk_enc_rmb_fused), half B starts its
+ *                    first GEMM once half A is past that K step (0, 4, 8, 12, 16)
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
  *                    given (the device tracker), else the detection-tile kernel; 1: the
@@ -250,6 +254,22 @@ int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const voi
  *   ROI's whole sum in partial 0 and 0 in its other partials. */
 int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                       const float* bias, void* XRN, long long* sums, void* stream);
+/* trk_enc_rmb_fused: trk_enc_rmb_front + trk_enc_se + trk_enc_transition_gemm in ONE kernel
+ *   (10x10 ROIs, C = 512; card.py:28-78, :138-146).  A ROI's two workgroups: the normal
+ *   group hands its bf16 Hardswish(x_n) rows to the reinforce group through xn_work
+ *   ([M][512] bf16) and flags[roi] (= epoch once published); the reinforce group computes
+ *   the SE (m_r, FC1, ReLU, FC2, hardsigmoid: f32) and T = Wt . [x_f * s | x_n] + bt with its
+ *   SiLU summed per channel.  Outputs are trk_enc_se's and trk_enc_transition_gemm's:
+ *   m_r, m_n, s [R][512] f32 and tsums [R][TRK_ENC_PARTS][512] (partial 0 = the ROI's sum,
+ *   the others 0) for trk_enc_head; XRN never reaches HBM.  Wtp = Wt [512][1024] in the
+ *   fragment order of trk_enc_rmb_front with 32 k steps ([32][32][64][8] bf16); se_w1
+ *   [128][512], se_b1 [128], se_w2 [512][128], se_b2 [512], bt [512] f32.  flags [R] int32
+ *   must not hold epoch when the launch starts (zero them per launch and pass epoch 1), and
+ *   xn_work / flags must not be shared with a concurrent launch. */
+int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                      const float* bias, const void* Wtp, const float* bt, const float* se_w1, const float* se_b1,
+                      const float* se_w2, const float* se_b2, void* xn_work, int* flags, int epoch, float* m_r,
+                      float* m_n, float* s, long long* tsums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
 /* Per-ROI tail of the encoder (f32, 16 ROIs per workgroup, f32-input MFMA).

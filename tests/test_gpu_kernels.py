@@ -739,6 +739,44 @@ def _rmb_front_vs_two_kernel(gpu, R):
         ops.enc_rmb_front(X, W1p, wdw, W2.reshape(1024, 512), b2)
 
 
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_fused_vs_separate_kernels(trk, gpu, R):
+    """trk_enc_rmb_fused (front + SE + transition in one kernel; the normal group hands its
+    x_n rows to the reinforce group through L2) vs enc_rmb_front -> enc_se ->
+    enc_transition_gemm on the same operands.  m_r / m_n: the same lane sums and fixed-point
+    means, bit-identical.  s: the SE's f32 dot products in another order, |ds| <= 1e-6.
+    tsums: the transition with the reference path fed the fused s (identical y = bf16(x_f
+    s)), the per-channel SiLU sums in another order: within 1e-5 of the largest sum.
+    R = 1 and 37 leave padding workgroups (the grid is a multiple of 16)."""
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(100 + R)
+    M, P = R * 100, 100
+    X = torch.randn(M, 512, generator=g).to(gpu).bfloat16()
+    W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
+    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
+    W2 = (torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16()
+    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
+    Wt = (torch.randn(512, 1024, generator=g) / 32).to(gpu).bfloat16()
+    bt = (torch.randn(512, generator=g) / 10).to(gpu)
+    sw1 = (torch.randn(128, 512, generator=g) / 22).to(gpu)
+    sb1 = (torch.randn(128, generator=g) / 10).to(gpu)
+    sw2 = (torch.randn(512, 128, generator=g) / 11).to(gpu)
+    sb2 = (torch.randn(512, generator=g) / 10).to(gpu)
+    W1p, W2p, Wtp = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2), ops.enc_pack_fragments_k(Wt)
+    assert Wtp[3, 5, 2, 7, 4].item() == Wt[16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
+    m_r, m_n, s, tsums = ops.enc_rmb_fused(X, W1p, wdw, W2p, b2, Wtp, bt, sw1, sb1, sw2, sb2)
+    XRN, sums = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    e_r, e_n, e_s = ops.enc_se(sums, P, sw1, sb1, sw2, sb2)
+    assert torch.equal(m_r, e_r) and torch.equal(m_n, e_n)
+    assert (s - e_s).abs().max().item() <= 1e-6
+    e_t = ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True)
+    ft, et = ops.enc_sums_reduce(tsums, P), ops.enc_sums_reduce(e_t, P)
+    assert (ft - et).abs().max().item() <= 1e-5 * et.abs().max().item()
+    m_r2, m_n2, s2, tsums2 = ops.enc_rmb_fused(X, W1p, wdw, W2p, b2, Wtp, bt, sw1, sb1, sw2, sb2)  # deterministic
+    assert torch.equal(m_r, m_r2) and torch.equal(s, s2) and torch.equal(tsums, tsums2)
+
+
 def _partials(total, P, parts=3):
     """split int64 per-ROI totals [R, ld] into the GEMMs' partial layout
     [R, parts, ld] (one entry per 128-row tile covering the ROI; the rest junk)"""
