@@ -164,12 +164,10 @@ def test_c3_fused_full_encoder_vs_front_path(trk, gpu):
     with torch.no_grad():
         roib = trk.roi_align(feat, torch.from_numpy(rois).to(gpu), (10, 10), 40 / 1280.0, 2, True,
                              out_dtype=torch.bfloat16, channels_last=True)
+        model.fused_full = True
         z_full = model(roib)
         model.fused_full = False
-        try:
-            z_front = model(roib)
-        finally:
-            model.fused_full = True
+        z_front = model(roib)
     d = (z_full - z_front).abs().max().item()
     print(f"\nc3 fused-full vs front path: max |d| {d:.3e}")
     assert d <= 2e-5, d
