@@ -404,7 +404,7 @@ class LiveProbe:
 
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_nchw_to_nhwc": "map_nhwc", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
-             "trk_enc_rmb_front": "enc_rmb_front",
+             "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_rmb_fused": "enc_rmb_fused",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
              "trk_step_begin": "step_begin", "trk_step_mid": "step_mid", "trk_step_end": "step_end",
@@ -478,10 +478,12 @@ class LiveProbe:
         on purpose)"""
         if n_side != 1:
             return None
-        ends = self.ev["enc_gemm_trans" if head_deferred else "enc_head"]
+        fused = bool(self.ev.get("enc_rmb_fused"))
+        ends = self.ev[("enc_rmb_fused" if fused else "enc_gemm_trans") if head_deferred else "enc_head"]
         first = "roi_stage"
         if roi_own_stream:
-            first = "enc_rmb_front" if self.ev.get("enc_rmb_front") else "enc_g1_dwconv"
+            first = ("enc_rmb_fused" if fused else
+                     "enc_rmb_front" if self.ev.get("enc_rmb_front") else "enc_g1_dwconv")
         starts = self.ev[first]
         gaps = [e1.elapsed_time(s0) * 1e3 for (_, e1), (s0, _) in zip(ends, starts[1:])]
         return float(np.mean(gaps)) if gaps else None
@@ -516,6 +518,9 @@ def kernel_pass(pipe, f, reps=10):
     X = roi.permute(0, 2, 3, 1).reshape(K * 100, 512)
     if "w1_pk" in W:
         timed("enc_rmb_front", lambda: ops.enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"]))
+    if "wt_pk" in W:
+        timed("enc_rmb_fused", lambda: ops.enc_rmb_fused(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"], W["wt_pk"],
+                                                         W["bt_f"], W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"]))
     timed("enc_g1_dwconv", lambda: ops.enc_g1_dwconv(X, W["w1_nk"], W["dw_t"]))
     Y2 = ops.enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])
     timed("enc_gemm_dsc", lambda: ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"]))
@@ -714,6 +719,10 @@ def main():
     # TRK_FRONT=0: the two-kernel encoder front (g1dw4 -> Y2 in HBM -> gemm4<DSC>) instead of
     # rmb_front (one kernel, Y2 in LDS)
     model.fused_front = os.environ.get("TRK_FRONT", "1") == "1"
+    # TRK_FULL=1/0: the SE and transition inside the front kernel (enc_rmb_fused) or not; unset:
+    # encoder.Model's default
+    if "TRK_FULL" in os.environ:
+        model.fused_full = os.environ["TRK_FULL"] == "1"
 
     # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
     # the syncs around the timed region make it do exactly `steps` embeddings (those of
@@ -777,14 +786,17 @@ def main():
         # first 1x1 convs + depthwise + both DSC GEMMs in one kernel: X in, XRN + sums out
         "enc_rmb_front": (R * 512 * 2 + R * 1024 * 2 + 2 * 1024 * 512 * 2 + 25 * 1024 * 4 + K * 1024 * 8,
                           2.0 * R * 1024 * 512 * 2 + 2.0 * R * 1024 * 25, BF16_PEAK_TFLOPS),
+        # front + SE + transition in one kernel: X in, the x_n hand-off written and read once
+        # (bf16), the three weight sets, the means / scales / transition sums out
+        "enc_rmb_fused": (R * 512 * 2 + 2 * R * 512 * 2 + 3 * 1024 * 512 * 2 + 2 * 128 * 512 * 4 + K * 512 * (3 * 4 + 24),
+                          2.0 * R * 1024 * 512 * 3 + 2.0 * R * 1024 * 25 + 4.0 * K * 128 * 512, BF16_PEAK_TFLOPS),
         "cost": (Fs * (M * 30 * 128 * 4 + N * 128 * 4 + M * N * 4), 2.0 * Fs * M * 30 * N * 128,
                  F32_MFMA_PEAK_TFLOPS),
     }
-    # the encoder path not taken in the timed region is still timed isolated (kernel_pass);
-    # the dominant kernel is chosen among the ones the timed region ran
-    front = pipe.model.fused_front and "enc_rmb_front" in kt
-    ran = {k for k in algo if k in kt and (k not in ("enc_g1_dwconv", "enc_gemm_dsc") or not front)
-           and (k != "enc_rmb_front" or front)}
+    # the encoder paths not taken in the timed region are still timed isolated (kernel_pass);
+    # the dominant kernel is chosen among the ones the timed region ran (live-probed, plus the
+    # ROI Align sweep and the cost build, which every step runs)
+    ran = {k for k in algo if k in live} | {"roi_align", "cost"}
     per = {}
     for k, (byt, fl, mpeak) in algo.items():
         if k not in kt:
