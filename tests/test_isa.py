@@ -1,0 +1,58 @@
+"""ISA check of the hand-counted vmcnt waits in the rmb kernels (csrc/enc_gemm.hip).
+
+rmb_front / rmb_fused issue their K-loop loads (weight fragments, depthwise taps,
+prefetches, LDS-DMA) as asm statements and retire them with counted s_waitcnt vmcnt(N).
+The compiler does not know those loads are in flight: if it moved or reused a
+destination register before the covering wait, the kernel would read (or clobber) a
+value still being loaded, and only some code generations would show it.  This test
+compiles the file for gfx950 and scans each rmb kernel's straight-line regions
+(tools/isa_vmem_check.py): no instruction may name a pending load's destination VGPRs.
+CPU only (hipcc cross-compiles); skipped without hipcc.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import isa_vmem_check as IC  # noqa: E402
+
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def test_scanner_flags_an_early_use():
+    body = ["\tglobal_load_dwordx4 v[4:7], v[0:1], off",
+            "\tglobal_load_dwordx4 v[8:11], v[0:1], off offset:1024",
+            "\ts_waitcnt vmcnt(1)",
+            "\tv_add_f32_e32 v12, v4, v5",      # v[4:7] retired by vmcnt(1): fine
+            "\tv_add_f32_e32 v13, v8, v9",      # v[8:11] still in flight: reported
+            "\ts_waitcnt vmcnt(0)",
+            "\tv_add_f32_e32 v14, v8, v9"]
+    bad = IC.scan(body)
+    assert [b[0] for b in bad] == [4]
+    # a later load into a pending destination (write-after-write) is reported too
+    assert IC.scan(["\tglobal_load_dword v3, v[0:1], off", "\tglobal_load_dword v3, v[0:1], off offset:4"])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
+    src = os.path.join(REPO, "a-lightweight-unsupervised-feature-extractor-_amd", "csrc")
+    # the sources include ../../include/trk_amd.h: mirror that layout
+    c = tmp_path / "p" / "c"
+    shutil.copytree(src, c, ignore=shutil.ignore_patterns("build", "*.o"))
+    shutil.copytree(os.path.join(REPO, "include"), tmp_path / "include")
+    asm = tmp_path / "enc_gemm.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+                    "-fhip-fp32-correctly-rounded-divide-sqrt", "--offload-device-only", "-S", "-o", str(asm),
+                    "enc_gemm.hip"], cwd=c, check=True, capture_output=True)
+    lines = asm.read_text().splitlines()
+    found = 0
+    for name, body in IC.kernels(lines, ["rmb_front_kernel", "rmb_front2_kernel", "rmb_fused_kernel"]):
+        found += 1
+        bad = IC.scan(body)
+        assert not bad, (name, bad[:5])
+    assert found == 3
