@@ -1662,7 +1662,22 @@ __device__ __forceinline__ float rf3_mean(float sum) {
 }
 
 template <int G>
-__device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned char* smem, f4v (&acc)[7][4]) {
+__device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned char* smem, f4v (&acc)[7][4],
+                                         int64_t lb, unsigned long long t_start) {
+  // diagnostics (trk_enc_set_prof): per wave [start -> tail, then the tail's phases] (8 x u64)
+  const bool prof = a.prof != nullptr;
+  unsigned long long ps[9];
+  if (prof) ps[0] = eg_stamp();
+  auto stamp = [&](int k) {
+    if (prof) ps[k] = eg_stamp();
+  };
+  auto flush = [&](int last) {
+    if (prof && (threadIdx.x & 63) == 0) {
+      unsigned long long* o = a.prof + (lb * 8 + (threadIdx.x >> 6)) * 8;
+      o[0] = ps[0] - t_start;
+      for (int q = 1; q < 8; ++q) o[q] = q <= last ? ps[q] - ps[q - 1] : 0;
+    }
+  };
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1702,6 +1717,7 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     }
     rf2_signal(ctr + RF2_CST + half, lane);
     rf2_wait(ctr + RF2_CST + half, 4);
+    stamp(1);
     uint16_t* dst = a.XN + r0 * 512 + half * 256;
     const int ht = tid & 255;
     for (int q = ht; q < RF_S * 32; q += 256) {
@@ -1710,11 +1726,14 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
                     *reinterpret_cast<const u32x4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2)));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's XN stores retired
+    stamp(2);
     rf2_signal(ctr + RF3_CPUB, lane);
     if (wave == 0) {
       rf2_wait(ctr + RF3_CPUB, 8);  // every wave's stores retired: publish
       if (lane == 0) __hip_atomic_store(a.flags + roi, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    stamp(3);
+    flush(3);
     return;
   } else {
     float* Ms = reinterpret_cast<float*>(smem + RF3_M);
@@ -1750,10 +1769,12 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
       }
     }
     rf2_signal(ctr + RF3_CYF, lane);
+    stamp(1);
     // the partner's x_n: its flag, then (once every wave is past GEMM2: the ring is Y(A))
     // LDS-DMA with sc1 of x_n K blocks into the ring, 4 blocks per group, one op per block
     // per wave: lanes < 50 move pieces 50 wave + lane (row p >> 2, slot p & 3), as rf_body's X
     rf3_wait_flag(a.flags + roi, a.epoch);
+    stamp(2);
     const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
     const uint16_t* xsrc = a.XN + (r0 + xr) * 512 + (((xp & 3) ^ rf_sw(xr)) * 8);
     auto ring_dma = [&](int grp) {  // x_n blocks 4 grp .. 4 grp + 3 -> slots (4 grp) & 7 ..
@@ -1770,6 +1791,7 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     rf2_wait(ctr + RF3_CYF, 8);  // m_r and the x_f image complete, every wave past GEMM2
     ring_dma(0);
     ring_dma(1);
+    stamp(3);
     // FC1 / FC2 as 8-lane row groups: lane l of a group takes k = 32 kk + 4 l .. + 3, so one
     // load instruction covers 8 rows x 128 contiguous bytes; the 8 partials are added by
     // two DPP steps and one xor-4 shuffle (f32, another order than trk_enc_se's MFMA: ulps)
@@ -1799,6 +1821,7 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     }
     rf2_signal(ctr + RF3_CH, lane);
     rf2_wait(ctr + RF3_CH, 8);
+    stamp(4);
     // FC2: s[c] = hardsigmoid(b2[c] + W2[c] . h), rows c = 64 wave + 8 p + g8
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
@@ -1823,6 +1846,7 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     }
     rf2_signal(ctr + RF3_CS, lane);
     rf2_wait(ctr + RF3_CS, 8);
+    stamp(5);
     // y = bf16(float(bf16 x_f) * s) in place: thread t takes channel chunk t & 63 (8 channels,
     // block (t & 63) >> 2, chunk t & 3) of rows (t >> 6) + 8 i
     {
@@ -1846,6 +1870,7 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     }
     rf2_signal(ctr + RF3_CYS, lane);
     rf2_wait(ctr + RF3_CYS, 8);
+    stamp(6);
     // ---- GEMM3: K steps 0..15 over the image, 16..31 over the ring.  Ring groups 0 and 1
     // (slots 0..7) were issued before the SE, 2 (slots 0..3) at step 20, 3 (4..7) at step 24,
     // each behind the barrier that ends the reads of the slots' previous group; barriers at
@@ -1913,6 +1938,9 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
           for (int e = 0; e < 4; ++e) o[j * 512 + e] = 0;
       }
     }
+    if (prof) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(7);
+    flush(7);
   }
 }
 
@@ -2127,7 +2155,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
       }
   }
   if constexpr (MODE == 1) {
-    rf3_tail<G>(a, roi, smem, acc);
+    rf3_tail<G>(a, roi, smem, acc, lb, prof ? pst[0] : 0ull);
     return;
   }
   {

@@ -774,7 +774,8 @@ def test_enc_rmb_fused_vs_separate_kernels(trk, gpu, R):
     ft, et = ops.enc_sums_reduce(tsums, P), ops.enc_sums_reduce(e_t, P)
     assert (ft - et).abs().max().item() <= 1e-5 * et.abs().max().item()
     m_r2, m_n2, s2, tsums2 = ops.enc_rmb_fused(X, W1p, wdw, W2p, b2, Wtp, bt, sw1, sb1, sw2, sb2)  # deterministic
-    assert torch.equal(m_r, m_r2) and torch.equal(s, s2) and torch.equal(tsums, tsums2)
+    # (partials past a ROI's count are never read: compare the reduced sums)
+    assert torch.equal(m_r, m_r2) and torch.equal(s, s2) and torch.equal(ops.enc_sums_reduce(tsums2, P), ft)
 
 
 def _partials(total, P, parts=3):
