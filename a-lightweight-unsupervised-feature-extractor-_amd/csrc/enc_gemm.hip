@@ -1637,9 +1637,15 @@ __device__ __forceinline__ void rf3_wait_flag(const int* flag, int epoch) {
       : "memory", "scc");
 }
 
-// per-channel sums of the wave's activated tile (rf_body's lane / DPP order); lanes fr == 0
-// end up with the sums of channels 16 t + 4 fc + e
-__device__ __forceinline__ void rf3_colsums(const f4v (&acc)[7][4], int fr, float (&sv)[4][4]) {
+// per-channel sums of the wave's activated tile (rf_body's lane / DPP order): after the
+// row_ror steps every lane of a 16-lane row holds all 16 sums of its channel group fc;
+// lane fr returns the one of channel 16 (fr >> 2) + 4 fc + (fr & 3) (rf3_lane_ch), so the
+// fixed-point conversions run once per channel instead of 16 times on lanes fr == 0
+__device__ __forceinline__ int rf3_lane_ch(int wave, int fr, int fc) {
+  return wave * 64 + (fr >> 2) * 16 + fc * 4 + (fr & 3);
+}
+__device__ __forceinline__ float rf3_colsum(const f4v (&acc)[7][4], int fr) {
+  float mine = 0.f;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
 #pragma unroll
@@ -1652,14 +1658,41 @@ __device__ __forceinline__ void rf3_colsums(const f4v (&acc)[7][4], int fr, floa
       x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // ^2
       x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));  // row_ror 4
       x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, true));  // row_ror 8
-      sv[t][e] = x;
+      mine = (fr == t * 4 + e) ? x : mine;
     }
   }
+  return mine;
 }
 // the squeeze mean of a sum as trk_enc_se takes it: (float)(llrint(sum * 2^24) * 2^-24) / 100
 __device__ __forceinline__ float rf3_mean(float sum) {
   return (float)((double)llrintf(sum * kFix) * (1.0 / 16777216.0)) / (float)RF_S;
 }
+__device__ __forceinline__ void rf3_store_f32_sc1(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+// 8 consecutive floats (32-B aligned) with two sc1 loads and one wait
+__device__ __forceinline__ void rf3_load8_sc1(const float* p, float (&v)[8]) {
+  u32x4 x, y;
+  asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
+               "global_load_dwordx4 %1, %2, off offset:16 sc1\n\t"
+               "s_waitcnt vmcnt(0)"
+               : "=&v"(x), "=&v"(y)
+               : "v"(p)
+               : "memory");
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = __uint_as_float(x[e]);
+    v[4 + e] = __uint_as_float(y[e]);
+  }
+}
+__device__ __forceinline__ float rf3_load_f32_sc1(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// the fused tail's hand-off flags per ROI (RF3_NFL ints): x_n rows, m_r, s published
+enum { RF3_FXN = 0, RF3_FMR = 1, RF3_FS = 2, RF3_NFL = 4 };
 
 template <int G>
 __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned char* smem, f4v (&acc)[7][4],
@@ -1680,21 +1713,29 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
   };
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
+  float* Ms = reinterpret_cast<float*>(smem + RF3_M);
+  float* Hs = reinterpret_cast<float*>(smem + RF3_H);
+  int* fl = a.flags + roi * RF3_NFL;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = wave >> 2, hw = wave & 3;
   const int fr = lane & 15, fc = lane >> 4;
   const int64_t r0 = roi * RF_S;
-  float sv[4][4];
-  rf3_colsums(acc, fr, sv);
-  if constexpr (G == 1) {
-    // ---- normal group: m_n, bf16 x_n rows -> XN (sc1), flag
-    if (fr == 0) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        *reinterpret_cast<float4*>(a.m_n + roi * 512 + wave * 64 + t * 16 + fc * 4) =
-            make_float4(rf3_mean(sv[t][0]), rf3_mean(sv[t][1]), rf3_mean(sv[t][2]), rf3_mean(sv[t][3]));
+  const int ch = rf3_lane_ch(wave, fr, fc);
+  const float mean = rf3_mean(rf3_colsum(acc, fr));
+  // one lane of wave 0 publishes flag k once every wave has counted its retired stores
+  auto publish = [&](int cnt, int k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    rf2_signal(ctr + cnt, lane);
+    if (wave == 0) {
+      rf2_wait(ctr + cnt, 8);
+      if (lane == 0) __hip_atomic_store(fl + k, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  };
+  if constexpr (G == 1) {
+    // ---- normal group: m_n; bf16 x_n rows -> XN (sc1), flag; then the ROI's SE (the
+    // reinforce group's m_r, published early, in; s out), off the reinforce group's path
+    a.m_n[roi * 512 + ch] = mean;
     if (half == 0) {
       rf2_wait(ctr + RF2_CG1 + 1, 4);
     } else {
@@ -1709,8 +1750,8 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const f4v v = acc[i][t];
-          const int ch = hw * 64 + t * 16 + fc * 4;
-          *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((ch >> 3) ^ (px & 15)) << 2) + ((ch & 7) >> 1)) =
+          const int c = hw * 64 + t * 16 + fc * 4;
+          *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((c >> 3) ^ (px & 15)) << 2) + ((c & 7) >> 1)) =
               make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
       }
@@ -1718,36 +1759,77 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     rf2_signal(ctr + RF2_CST + half, lane);
     rf2_wait(ctr + RF2_CST + half, 4);
     stamp(1);
-    uint16_t* dst = a.XN + r0 * 512 + half * 256;
-    const int ht = tid & 255;
-    for (int q = ht; q < RF_S * 32; q += 256) {
-      const int row = q >> 5, c = q & 31;
-      rf3_store_sc1(dst + (int64_t)row * 512 + c * 8,
-                    *reinterpret_cast<const u32x4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2)));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's XN stores retired
-    stamp(2);
-    rf2_signal(ctr + RF3_CPUB, lane);
-    if (wave == 0) {
-      rf2_wait(ctr + RF3_CPUB, 8);  // every wave's stores retired: publish
-      if (lane == 0) __hip_atomic_store(a.flags + roi, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    stamp(3);
-    flush(3);
-    return;
-  } else {
-    float* Ms = reinterpret_cast<float*>(smem + RF3_M);
-    float* Hs = reinterpret_cast<float*>(smem + RF3_H);
-    float* Ss = reinterpret_cast<float*>(smem + RF3_S);
-    // ---- reinforce group: m_r (global + LDS), bf16 x_f -> the K-block image
-    if (fr == 0) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float4 m = make_float4(rf3_mean(sv[t][0]), rf3_mean(sv[t][1]), rf3_mean(sv[t][2]), rf3_mean(sv[t][3]));
-        *reinterpret_cast<float4*>(a.m_r + roi * 512 + wave * 64 + t * 16 + fc * 4) = m;
-        *reinterpret_cast<float4*>(Ms + wave * 64 + t * 16 + fc * 4) = m;
+    {
+      uint16_t* dst = a.XN + r0 * 512 + half * 256;
+      const int ht = tid & 255;
+      for (int q = ht; q < RF_S * 32; q += 256) {
+        const int row = q >> 5, c = q & 31;
+        rf3_store_sc1(dst + (int64_t)row * 512 + c * 8,
+                      *reinterpret_cast<const u32x4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2)));
       }
     }
+    publish(RF3_CPUB, RF3_FXN);
+    stamp(2);
+    // SE: m_r -> LDS, FC1, FC2 (one row group of 8 lanes per output, as trk_enc_se's sums in
+    // another order), s -> global (sc1) + flag
+    rf3_wait_flag(fl + RF3_FMR, a.epoch);
+    Ms[tid] = rf3_load_f32_sc1(a.m_r + roi * 512 + tid);
+    rf2_signal(ctr + RF3_CYF, lane);
+    rf2_wait(ctr + RF3_CYF, 8);
+    stamp(3);
+    const int l8 = lane & 7, g8 = lane >> 3;
+    auto sum8 = [&](float x) {
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));  // quad [1,0,3,2]
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));  // quad [2,3,0,1]
+      return x + __shfl_xor(x, 4);
+    };
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {  // FC1: h[j] = relu(b1[j] + W1[j] . m_r), j = 16 wave + 8 p + g8
+      const int j = 16 * wave + 8 * p + g8;
+      const float* w = a.se_w1 + j * 512 + 4 * l8;
+      float h = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
+        const float4 mv = *reinterpret_cast<const float4*>(Ms + 32 * kk + 4 * l8);
+        h = __builtin_fmaf(wv.x, mv.x, h);
+        h = __builtin_fmaf(wv.y, mv.y, h);
+        h = __builtin_fmaf(wv.z, mv.z, h);
+        h = __builtin_fmaf(wv.w, mv.w, h);
+      }
+      h = sum8(h);
+      if (l8 == 0) Hs[j] = fmaxf(h + a.se_b1[j], 0.f);
+    }
+    rf2_signal(ctr + RF3_CH, lane);
+    rf2_wait(ctr + RF3_CH, 8);
+    stamp(4);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {  // FC2: s[c] = hardsigmoid(b2[c] + W2[c] . h), c = 64 wave + 8 p + g8
+      const int c = 64 * wave + 8 * p + g8;
+      const float* w = a.se_w2 + c * 128 + 4 * l8;
+      float x = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
+        const float4 hv = *reinterpret_cast<const float4*>(Hs + 32 * kk + 4 * l8);
+        x = __builtin_fmaf(wv.x, hv.x, x);
+        x = __builtin_fmaf(wv.y, hv.y, x);
+        x = __builtin_fmaf(wv.z, hv.z, x);
+        x = __builtin_fmaf(wv.w, hv.w, x);
+      }
+      x = sum8(x);
+      if (l8 == 0) rf3_store_f32_sc1(a.s + roi * 512 + c, fminf(fmaxf(x + a.se_b2[c] + 3.0f, 0.f), 6.0f) / 6.0f);
+    }
+    publish(RF3_CS, RF3_FS);
+    stamp(5);
+    flush(5);
+    return;
+  } else {
+    // ---- reinforce group: m_r out first (the normal group's SE waits for it), bf16 x_f ->
+    // the K-block image (unscaled); GEMM3's x_n half over the ring, then -- once s has
+    // arrived -- the image scaled in place and GEMM3's x_f half
+    rf3_store_f32_sc1(a.m_r + roi * 512 + ch, mean);
+    publish(RF3_CYS, RF3_FMR);
     // A's channels go to blocks 0..7 (X: dead once B is past GEMM1), B's to 8..15 (Y(B): dead
     // once both halves are past GEMM2; the ring, blocks 16..23 = Y(A), likewise)
     if (half == 0) {
@@ -1770,11 +1852,10 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
     }
     rf2_signal(ctr + RF3_CYF, lane);
     stamp(1);
-    // the partner's x_n: its flag, then (once every wave is past GEMM2: the ring is Y(A))
-    // LDS-DMA with sc1 of x_n K blocks into the ring, 4 blocks per group, one op per block
-    // per wave: lanes < 50 move pieces 50 wave + lane (row p >> 2, slot p & 3), as rf_body's X
-    rf3_wait_flag(a.flags + roi, a.epoch);
-    stamp(2);
+    // the partner's x_n (flag, then LDS-DMA with sc1 into the ring once every wave is past
+    // GEMM2): 4 K blocks per group, one op per block per wave, lanes < 50 moving pieces
+    // 50 wave + lane (row p >> 2, slot p & 3), as rf_body's X
+    rf3_wait_flag(fl + RF3_FXN, a.epoch);
     const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
     const uint16_t* xsrc = a.XN + (r0 + xr) * 512 + (((xp & 3) ^ rf_sw(xr)) * 8);
     auto ring_dma = [&](int grp) {  // x_n blocks 4 grp .. 4 grp + 3 -> slots (4 grp) & 7 ..
@@ -1788,95 +1869,18 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
                                            16 /* sc1 */);
       }
     };
-    rf2_wait(ctr + RF3_CYF, 8);  // m_r and the x_f image complete, every wave past GEMM2
+    rf2_wait(ctr + RF3_CYF, 8);  // the x_f image complete, every wave past GEMM2
     ring_dma(0);
     ring_dma(1);
-    stamp(3);
-    // FC1 / FC2 as 8-lane row groups: lane l of a group takes k = 32 kk + 4 l .. + 3, so one
-    // load instruction covers 8 rows x 128 contiguous bytes; the 8 partials are added by
-    // two DPP steps and one xor-4 shuffle (f32, another order than trk_enc_se's MFMA: ulps)
-    const int l8 = lane & 7, g8 = lane >> 3;
-    auto sum8 = [&](float x) {
-      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));  // quad [1,0,3,2]
-      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));  // quad [2,3,0,1]
-      return x + __shfl_xor(x, 4);
-    };
-    // FC1: h[j] = relu(b1[j] + W1[j] . m_r), rows j = 16 wave + 8 p + g8
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int j = 16 * wave + 8 * p + g8;
-      const float* w = a.se_w1 + j * 512 + 4 * l8;
-      float h = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
-        const float4 mv = *reinterpret_cast<const float4*>(Ms + 32 * kk + 4 * l8);
-        h = __builtin_fmaf(wv.x, mv.x, h);
-        h = __builtin_fmaf(wv.y, mv.y, h);
-        h = __builtin_fmaf(wv.z, mv.z, h);
-        h = __builtin_fmaf(wv.w, mv.w, h);
-      }
-      h = sum8(h);
-      if (l8 == 0) Hs[j] = fmaxf(h + a.se_b1[j], 0.f);
-    }
-    rf2_signal(ctr + RF3_CH, lane);
-    rf2_wait(ctr + RF3_CH, 8);
-    stamp(4);
-    // FC2: s[c] = hardsigmoid(b2[c] + W2[c] . h), rows c = 64 wave + 8 p + g8
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int c = 64 * wave + 8 * p + g8;
-      const float* w = a.se_w2 + c * 128 + 4 * l8;
-      float x = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
-        const float4 hv = *reinterpret_cast<const float4*>(Hs + 32 * kk + 4 * l8);
-        x = __builtin_fmaf(wv.x, hv.x, x);
-        x = __builtin_fmaf(wv.y, hv.y, x);
-        x = __builtin_fmaf(wv.z, hv.z, x);
-        x = __builtin_fmaf(wv.w, hv.w, x);
-      }
-      x = sum8(x);
-      if (l8 == 0) {
-        const float sc = fminf(fmaxf(x + a.se_b2[c] + 3.0f, 0.f), 6.0f) / 6.0f;
-        Ss[c] = sc;
-        a.s[roi * 512 + c] = sc;
-      }
-    }
-    rf2_signal(ctr + RF3_CS, lane);
-    rf2_wait(ctr + RF3_CS, 8);
-    stamp(5);
-    // y = bf16(float(bf16 x_f) * s) in place: thread t takes channel chunk t & 63 (8 channels,
-    // block (t & 63) >> 2, chunk t & 3) of rows (t >> 6) + 8 i
-    {
-      const int cc = tid & 63, kb = cc >> 2, c4 = cc & 3;
-      float sc[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sc[e] = Ss[cc * 8 + e];
-#pragma unroll
-      for (int i = 0; i < 13; ++i) {
-        const int px = (tid >> 6) + 8 * i;
-        if (px < RF_S) {
-          u32x4* pp = reinterpret_cast<u32x4*>(Y + kb * RF_KBS + px * 16 + ((c4 ^ rf_sw(px)) << 2));
-          const u32x4 v = *pp;
-          u32x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            o[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * sc[2 * e], __uint_as_float(v[e] & 0xffff0000u) * sc[2 * e + 1]);
-          *pp = o;
-        }
-      }
-    }
-    rf2_signal(ctr + RF3_CYS, lane);
-    rf2_wait(ctr + RF3_CYS, 8);
-    stamp(6);
-    // ---- GEMM3: K steps 0..15 over the image, 16..31 over the ring.  Ring groups 0 and 1
-    // (slots 0..7) were issued before the SE, 2 (slots 0..3) at step 20, 3 (4..7) at step 24,
-    // each behind the barrier that ends the reads of the slots' previous group; barriers at
-    // 16, 24, 28 publish the groups
+    stamp(2);
+    // ---- GEMM3 (K = 1024): steps 0..15 = x_n (ring; Wt k steps 16..31), 16..31 = x_f * s
+    // (image; Wt k steps 0..15).  Ring: groups 0, 1 (slots 0..7) issued above, 2 (slots 0..3)
+    // at step 4 and 3 (4..7) at step 8, each behind the barrier that ends the reads of the
+    // slots' previous group; barriers at 4, 8, 12 publish groups 1 (at 0: vmcnt(0) before the
+    // first barrier), 2, 3.  Before step 16: s from the normal group, the image scaled in place
     constexpr int NK3 = 32;
     const uint4* b3p = a.Wtp + (size_t)(wave * 4) * 64 + lane;
+    auto wstep = [](int kt) { return (kt + 16) & 31; };
     u32x4 bq[3][4];
     const int lterm = fr * 4 + (fc ^ rf_sw(fr));
     const uint32_t y_a = lds_addr(Y) + lterm * 16;
@@ -1885,32 +1889,64 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
     float4 bias4[4];
-    rf_loadB(b3p, 0, bq[0]);
-    rf_loadB(b3p, 1, bq[1]);
+    rf_loadB(b3p, wstep(0), bq[0]);
+    rf_loadB(b3p, wstep(1), bq[1]);
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kt = 0; kt < NK3; ++kt) {
+    auto step = [&](int kt) {
       u32x4(&b)[4] = bq[kt % 3];
-      // vmcnt(0) retires this wave's ring DMA before the barrier that publishes it (groups 0-1
-      // at step 0 for 16, 2 at 24, 3 at 28); steps 21 / 25 count the group issued one step before
-      const bool rs = kt == 0 || kt == 24 || kt == 28;
-      rf_vmwait(rs ? 0 : (kt + 1 < NK3 ? 4 + ((kt == 21 || kt == 25) ? 4 : 0) : 0), b);
-      if (kt == 16 || kt == 20 || kt == 24 || kt == 28) {
+      // vmcnt(0): this wave's ring DMA retired before the barrier that publishes it (groups
+      // 0-1 at step 0, 2 at 8, 3 at 12); steps 5 / 9 count the group issued one step before;
+      // step 16 follows the scaling, whose sc1 loads waited for everything
+      const bool rs = kt == 0 || kt == 8 || kt == 12;
+      rf_vmwait(rs ? 0 : (kt + 1 < NK3 ? 4 + ((kt == 5 || kt == 9) ? 4 : 0) : 0), b);
+      if (kt == 0 || kt == 4 || kt == 8 || kt == 12) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         g4_barrier();
       }
-      if (kt == 20) ring_dma(2);  // slots 0..3: their group 0 was read in steps 16..19
-      if (kt == 24) ring_dma(3);  // slots 4..7: group 1, steps 20..23
-      if (kt + 2 < NK3) rf_loadB(b3p, kt + 2, bq[(kt + 2) % 3]);
+      if (kt == 4) ring_dma(2);  // slots 0..3: group 0 was read in steps 0..3
+      if (kt == 8) ring_dma(3);  // slots 4..7: group 1, steps 4..7
+      if (kt + 2 < NK3) rf_loadB(b3p, wstep(kt + 2), bq[(kt + 2) % 3]);
       if (kt == NK3 - 3) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           bias4[t] = *reinterpret_cast<const float4*>(a.bt + wave * 64 + t * 16 + fc * 4);
       }
-      const int blk = kt < 16 ? kt : 16 + ((kt - 16) & 7);
+      const int blk = kt < 16 ? 16 + (kt & 7) : kt - 16;
       rf_mfma_step(y_a + blk * RF_KBS * 4, b, acc);
-    }
+    };
+#pragma unroll
+    for (int kt = 0; kt < 16; ++kt) step(kt);
     __builtin_amdgcn_s_setprio(0);
+    if (prof) ps[3] = eg_stamp();
+    rf3_wait_flag(fl + RF3_FS, a.epoch);
+    if (prof) ps[4] = eg_stamp();
+    {
+      // y = bf16(float(bf16 x_f) * s) in place: thread t takes channel chunk t & 63 (8
+      // channels, block (t & 63) >> 2, chunk t & 3) of rows wave + 8 i
+      const int cc = tid & 63, kb = cc >> 2, c4 = cc & 3;
+      float sc[8];
+      rf3_load8_sc1(a.s + roi * 512 + cc * 8, sc);
+      auto scale_row = [&](int px) {
+        u32x4* pp = reinterpret_cast<u32x4*>(Y + kb * RF_KBS + px * 16 + ((c4 ^ rf_sw(px)) << 2));
+        const u32x4 v = *pp;
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * sc[2 * e], __uint_as_float(v[e] & 0xffff0000u) * sc[2 * e + 1]);
+        *pp = o;
+      };
+#pragma unroll
+      for (int i = 0; i < 12; ++i) scale_row(wave + 8 * i);  // rows 0..95
+      if (wave < 4) scale_row(96 + wave);                      // rows 96..99 (wave-uniform)
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    g4_barrier();  // the whole image scaled
+    if (prof) ps[5] = eg_stamp();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kt = 16; kt < NK3; ++kt) step(kt);
+    __builtin_amdgcn_s_setprio(0);
+    if (prof) ps[6] = eg_stamp();
     // ---- SiLU(T + bias) and its per-channel sums over the ROI -> tsums
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1925,18 +1961,12 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
           acc[i][t][2 * h + 1] = v.y;
         }
     }
-    rf3_colsums(acc, fr, sv);
-    if (fr == 0) {
+    const float ts = rf3_colsum(acc, fr);
+    {
       const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        long long* o = a.tsums + roi * kPart * 512 + wave * 64 + t * 16 + fc * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[t][e] * kFix);
-        for (int j = 1; j < cnt; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[j * 512 + e] = 0;
-      }
+      long long* o = a.tsums + roi * kPart * 512 + ch;
+      o[0] = llrintf(ts * kFix);
+      for (int j = 1; j < cnt; ++j) o[j * 512] = 0;
     }
     if (prof) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(7);
@@ -2481,6 +2511,7 @@ extern "C" int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, cons
   a.epoch = epoch;
   a.m_r = m_r; a.m_n = m_n; a.s = s;
   a.tsums = tsums;
+  a.prof = g_enc_prof;
   hipLaunchKernelGGL(rmb_fused_kernel, dim3((unsigned)nwg), dim3(512), RF3_LDS, reinterpret_cast<hipStream_t>(stream),
                      a);
   return trk::check_launch("rmb_fused_kernel");

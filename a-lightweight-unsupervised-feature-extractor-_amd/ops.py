@@ -253,7 +253,7 @@ def enc_rmb_fused(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: to
     # per call: the hand-off workspace and flags (zeroed: epoch 1 is then fresh), so launches
     # on different streams never share them
     xn = torch.empty((M, 512), device=dev, dtype=torch.bfloat16)
-    flags = torch.zeros(max(R, 1), device=dev, dtype=torch.int32)
+    flags = torch.zeros(max(R, 1) * 4, device=dev, dtype=torch.int32)  # [R][4]: x_n, m_r, s published
     out = torch.empty((3, R, 512), device=dev, dtype=torch.float32)
     tsums = torch.empty((R, _lib.TRK_ENC_PARTS, 512), device=dev, dtype=torch.int64)
     c = lambda t: _f32c(t)

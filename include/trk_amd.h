@@ -255,15 +255,15 @@ int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const voi
 int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                       const float* bias, void* XRN, long long* sums, void* stream);
 /* trk_enc_rmb_fused: trk_enc_rmb_front + trk_enc_se + trk_enc_transition_gemm in ONE kernel
- *   (10x10 ROIs, C = 512; card.py:28-78, :138-146).  A ROI's two workgroups: the normal
- *   group hands its bf16 Hardswish(x_n) rows to the reinforce group through xn_work
- *   ([M][512] bf16) and flags[roi] (= epoch once published); the reinforce group computes
- *   the SE (m_r, FC1, ReLU, FC2, hardsigmoid: f32) and T = Wt . [x_f * s | x_n] + bt with its
- *   SiLU summed per channel.  Outputs are trk_enc_se's and trk_enc_transition_gemm's:
+ *   (10x10 ROIs, C = 512; card.py:28-78, :138-146).  A ROI's two workgroups hand data over
+ *   through global memory and flags[roi][4] (= epoch once published): the normal group its
+ *   bf16 Hardswish(x_n) rows (xn_work, [M][512] bf16) and, from the reinforce group's m_r,
+ *   the SE scales s (FC1, ReLU, FC2, hardsigmoid: f32); the reinforce group computes
+ *   T = Wt . [x_f * s | x_n] + bt with its SiLU summed per channel.  Outputs are trk_enc_se's and trk_enc_transition_gemm's:
  *   m_r, m_n, s [R][512] f32 and tsums [R][TRK_ENC_PARTS][512] (partial 0 = the ROI's sum,
  *   the others 0) for trk_enc_head; XRN never reaches HBM.  Wtp = Wt [512][1024] in the
  *   fragment order of trk_enc_rmb_front with 32 k steps ([32][32][64][8] bf16); se_w1
- *   [128][512], se_b1 [128], se_w2 [512][128], se_b2 [512], bt [512] f32.  flags [R] int32
+ *   [128][512], se_b1 [128], se_w2 [512][128], se_b2 [512], bt [512] f32.  flags [R][4] int32
  *   must not hold epoch when the launch starts (zero them per launch and pass epoch 1), and
  *   xn_work / flags must not be shared with a concurrent launch. */
 int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,

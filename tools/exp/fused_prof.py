@@ -43,8 +43,8 @@ fused()
 torch.cuda.synchronize()
 L.trk_enc_set_prof(None)
 p = buf.view(nwg // 2, 2, 8, 8)[:R].double().cpu()  # [roi][group][wave][slot]
-names_r = ["to_tail", "y_image", "flag_wait", "cyf_ring", "fc1", "fc2", "scale", "gemm3_epi"]
-names_n = ["to_tail", "staging", "xn_copy", "publish", "-", "-", "-", "-"]
+names_r = ["to_tail", "mr_pub_y_image", "xn_flag_ring", "gemm3_xn", "s_flag_wait", "scale", "gemm3_xf", "epilogue"]
+names_n = ["to_tail", "staging", "xn_copy_publish", "mr_wait_load", "fc1", "fc2_publish", "-", "-"]
 for gi, names in ((0, names_r), (1, names_n)):
     med = p[:, gi].median(0).values  # [wave][slot]
     print(json.dumps({"group": "reinforce" if gi == 0 else "normal",
