@@ -1476,8 +1476,8 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
       for (int e = 0; e < 4; ++e) {
         sv[e] += lane_xor1(sv[e]);
         sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
         sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
       }
       if (fr == 0) {
         long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
@@ -1637,8 +1637,9 @@ __device__ __forceinline__ void rf3_wait_flag(const int* flag, int epoch) {
       : "memory", "scc");
 }
 
-// per-channel sums of the wave's activated tile (rf_body's lane / DPP order): after the
-// row_ror steps every lane of a 16-lane row holds all 16 sums of its channel group fc;
+// per-channel sums of the wave's activated tile (rf_body's lane / DPP order): xor 1, xor 2,
+// row_ror 8, row_ror 4 is a butterfly (row_ror 4 before 8 is not: lanes 0 and 4 would add
+// the quads in different orders), so every lane of a 16-lane row holds the same 16 sums;
 // lane fr returns the one of channel 16 (fr >> 2) + 4 fc + (fr & 3) (rf3_lane_ch), so the
 // fixed-point conversions run once per channel instead of 16 times on lanes fr == 0
 __device__ __forceinline__ int rf3_lane_ch(int wave, int fr, int fc) {
@@ -1656,8 +1657,8 @@ __device__ __forceinline__ float rf3_colsum(const f4v (&acc)[7][4], int fr) {
       if (fr < 4) x += acc[6][t][e];
       x += lane_xor1(x);
       x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // ^2
-      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));  // row_ror 4
       x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, true));  // row_ror 8
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));  // row_ror 4
       mine = (fr == t * 4 + e) ? x : mine;
     }
   }
@@ -2205,8 +2206,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
       for (int e = 0; e < 4; ++e) {
         sv[e] += lane_xor1(sv[e]);
         sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
         sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
+        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
       }
       if (fr == 0) {
         long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;

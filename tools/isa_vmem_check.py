@@ -3,7 +3,8 @@ s_waitcnt vmcnt that retires the load (the hazard hand-counted vmcnt waits can h
 the compiler moves or reuses an asm load's destination).  Linear scan of each kernel:
 every global_/buffer_/flat_ memory op counts in vmcnt in issue order; a load's destination
 stays pending until a vmcnt(N) leaves at most N younger ops outstanding; any other
-instruction naming a pending VGPR is reported.  Pending state is dropped at compiler
+instruction naming a pending VGPR is reported (a younger load into the same destination is
+not: loads return in issue order).  Pending state is dropped at compiler
 basic-block labels (paths are interleaved in the layout).  usage: isa_vmem_check.py file.s [kernel-substring ...]"""
 import re
 import sys
@@ -60,13 +61,15 @@ def scan(body):
             continue
         pending = set().union(*[d for d, _ in out]) if out else set()
         used = regs(s)
+        dest = set()
+        if VMEM.match(op) and "load" in op and "_lds" not in op:
+            dest = regs(s[len(op):].split(",")[0])
+            # a younger load into a pending destination is ordered behind it (vector memory
+            # loads return in issue order on gfx9), so only its address operands count
+            used -= dest
         if pending & used:
             bad.append((i, s, sorted(pending & used)[:4]))
         if VMEM.match(op):
-            dest = set()
-            if "load" in op and "_lds" not in op:
-                first = s[len(op):].split(",")[0]
-                dest = regs(first)
             out.append((dest, s))
     return bad
 
