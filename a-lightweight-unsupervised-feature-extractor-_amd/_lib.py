@@ -96,6 +96,8 @@ def _declare(L):
     L.trk_enc_rmb_fused.restype = i32
     L.trk_enc_transition_gemm.argtypes = [P, i64, i64, i64, P, i64, P, P, i64, P, P]
     L.trk_enc_transition_gemm.restype = i32
+    L.trk_enc_transition_gemm2.argtypes = [P, i64, i64, i64, P, i64, P, P, P, i64, P, P]
+    L.trk_enc_transition_gemm2.restype = i32
     L.trk_enc_sums_reduce.argtypes = [P, i64, i64, i64, P, P]
     L.trk_enc_sums_reduce.restype = i32
     L.trk_enc_se.argtypes = [P, i64, i64, i64, i64, P, P, i64, P, P, P, P, P, P]

@@ -43,6 +43,12 @@ int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X r
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
 int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
+int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
+                      // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
+                      // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
+int g_enc_trans_wide = 0;  // trk_set_tuning("enc_trans_wide"): 1 = gemm4's transition on 256 x 256 tiles (8
+                           // waves, one workgroup per CU; P >= 86; 301 vs 282 us isolated, pipeline 2 of 3 pairs
+                           // lost: kept as a tested variant), 0 = 128 x 256 tiles, two workgroups per CU
 int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
@@ -471,9 +477,18 @@ constexpr size_t G4_LDS = (G4_RING + G4_STILE) > (G4_STAGE + G4_RED) ? (G4_RING 
 static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
 
 // WIDE (P >= 64): a wave's 64 rows span at most 2 ROIs and a tile's 128 at most 3, so
-// the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions)
-template <int EPI, bool WIDE, int HSWM, int SMF>
+// the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions).
+// WMV: waves along M.  2 = the 128 x 256 tile above (4 waves, two workgroups per CU); 4 =
+// a 256 x 256 tile on 8 waves, one workgroup per CU (transition only, P >= 86 so the tile
+// spans <= 4 ROIs): the same wave tiles and MFMAs, the B tile streamed once per 256 rows
+// instead of per 128 -- 32 instead of 48 KB of L2 -> LDS per K step for the same work
+template <int EPI, bool WIDE, int HSWM, int SMF, int WMV = 2>
 __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, unsigned char* smem) {
+  static_assert(WMV == 2 || (WMV == 4 && EPI == EPI_TRANS && SMF == 1), "wide-M gemm4: transition, MFMA sums");
+  constexpr int NT = 128 * WMV, BM = 64 * WMV;   // threads, tile rows
+  constexpr int ABUF = BM * 4, BUF = ABUF + 1024;  // uint4: A | B (256 rows) per ring stage
+  constexpr int NB = 1024 / NT;                    // B DMA ops per thread per stage (A: 2)
+  constexpr size_t RING = (size_t)3 * BUF * 16;
   uint4* ring = reinterpret_cast<uint4*>(smem);
   // opaque per tile: keeps the compiler from hoisting lane-dependent addresses
   // out of the persistent tile loop (they would stay live across the MFMA loop)
@@ -486,52 +501,57 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   const int ntl = (int)(lb % (ntile_n * a.groups));
   const int64_t mt = lb / (ntile_n * a.groups);
   const int g = ntl / ntile_n, n0 = (ntl % ntile_n) * 256;
-  const int64_t m0 = mt * 128;
+  const int64_t m0 = mt * BM;
   const uint16_t* Ag = a.A + (int64_t)g * a.K;
   const uint16_t* Bg = a.B + (int64_t)g * a.N * a.K;
   const int nk = a.K / BK;
   const int64_t roi_base = m0 / a.P;
 
   const uint16_t* asrc[2];
-  const uint16_t* bsrc[4];
+  const uint16_t* bsrc[NB];
   int arow[2], achk[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x16(r);
+    const int p = q * NT + tid, r = p >> 2, c = (p & 3) ^ x16(r);
     arow[q] = r;
     achk[q] = c;
     asrc[q] = Ag + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x16(r);
+  for (int q = 0; q < NB; ++q) {
+    const int p = q * NT + tid, r = p >> 2, c = (p & 3) ^ x16(r);
     bsrc[q] = Bg + (int64_t)(n0 + r) * a.K + c * 8;
   }
   auto issue = [&](int kt) {
-    uint4* d = ring + (kt % 3) * G4_BUF + wave * 64;
+    uint4* d = ring + (kt % 3) * BUF + wave * 64;
 #pragma unroll
     for (int q = 0; q < 2; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * NT), 16, 0, 0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + kt * BK), LPTR(d + 512 + q * 256), 16, 0, 0);
+    for (int q = 0; q < NB; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + kt * BK), LPTR(d + ABUF + q * NT), 16, 0, 0);
+  };
+  // retire the oldest of two issued stages: the other stage's 2 + NB ops may stay in flight
+  auto wait_older_stage = []() {
+    if constexpr (NB == 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   };
 
-  const float* stile = reinterpret_cast<const float*>(smem + G4_RING);
+  const float* stile = reinterpret_cast<const float*>(smem + RING);
   const float* srow[2] = {stile, stile};
   if constexpr (EPI == EPI_TRANS) {
     const int per = a.kscale / 4;
     const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
     // only the slots a tile can span (ceil(127 / P) + 1): the launch sizes LDS for them
-    const int tslots = min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
+    const int tslots = min(G4_SLOTS, (BM - 1 + a.P - 1) / a.P + 1);
 #pragma unroll
-    for (int q = 0; q < G4_SQ; ++q) {
-      const int p = q * 256 + tid;
+    for (int q = 0; q < G4_SQ * 256 / NT; ++q) {
+      const int p = q * NT + tid;
       if (p >= tslots * per) continue;
       const int slot = min(p / per, G4_SLOTS - 1);
       const int64_t roi = min(roi_base + slot, nroi - 1);
       const float* src = a.scale + roi * a.kscale + (p % per) * 4;
-      __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(reinterpret_cast<uint4*>(smem + G4_RING) + q * 256 + wave * 64),
+      __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(reinterpret_cast<uint4*>(smem + RING) + q * NT + wave * 64),
                                        16, 0, 0);
     }
 #pragma unroll
@@ -543,11 +563,11 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   auto transform = [&](int kt) {
     if constexpr (EPI == EPI_TRANS) {
       if (kt * BK < a.kscale) {
-        const uint32_t d = lds_addr(ring + (kt % 3) * G4_BUF + tid);
+        const uint32_t d = lds_addr(ring + (kt % 3) * BUF + tid);
         u32x4 v[2], s4[2][2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          v[q] = lds_read128(d + q * 256 * 16);
+          v[q] = lds_read128(d + q * NT * 16);
           const uint32_t sa = lds_addr(srow[q] + kt * BK);
           s4[q][0] = lds_read128(sa);
           s4[q][1] = lds_read128(sa + 16);
@@ -563,7 +583,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
             const float s_hi = __uint_as_float(s4[q][e >> 1][(2 * e + 1) & 3]);
             o[e] = pack_bf16x2(__uint_as_float(v[q][e] << 16) * s_lo, __uint_as_float(v[q][e] & 0xffff0000u) * s_hi);
           }
-          lds_write128(d + q * 256 * 16, o);
+          lds_write128(d + q * NT * 16, o);
         }
       }
     }
@@ -572,7 +592,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   const int fr = lane & 15, fc = lane >> 4;
   const int lterm = fr * 4 + (fc ^ x16(fr));
   const int aoff = (wr * 64) * 4 + lterm;            // + mt * 64
-  const int boff = 512 + (wc * 128) * 4 + lterm;     // + nt * 64
+  const int boff = ABUF + (wc * 128) * 4 + lterm;    // + nt * 64
 
   f4v acc[4][8];
 #pragma unroll
@@ -588,10 +608,13 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   issue(0);
   if (nk > 1) {
     issue(1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    wait_older_stage();
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  // the transition's s tile was landed by every wave's DMA, and transform reads any slot of
+  // it: one barrier after each wave's own wait (the A elements it scales are its own DMA's)
+  if constexpr (EPI == EPI_TRANS) g4_barrier();
   transform(0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   g4_barrier();
@@ -600,7 +623,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   // step kt - 1): the MFMAs start as soon as the fragments are read, and the DMA
   // issue -- which stalls while the memory pipeline is full -- runs beside them
   for (int kt = 0; kt < nk; ++kt) {
-    const uint4* buf = ring + (kt % 3) * G4_BUF;
+    const uint4* buf = ring + (kt % 3) * BUF;
     bf8v bfr[8], afr[4];
 #pragma unroll
     for (int t = 0; t < 8; ++t) bfr[t] = *reinterpret_cast<const bf8v*>(buf + boff + t * 64);
@@ -616,7 +639,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       issue(kt + 2);
     }
     if (kt + 1 < nk) {
-      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if (kt + 2 < nk) wait_older_stage();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       transform(kt + 1);
     }
@@ -652,7 +675,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   // per-ROI column sums: each row-half wave (wr) writes its f32 partials for every tile
   // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
   // consumer adds llrintf(p0 * 2^24) + llrintf(p1 * 2^24) (the former int64 atomics' sum)
-  float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [2][SLOTS][256]
+  float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [WMV][SLOTS][256]
   if constexpr (SMF != 0) {
     // the same partials on the MFMA: S[slot][col] = sum_rows mask[slot][row] * act[row][col]
     // as 16x16x32 bf16 MFMAs whose B operand is the accumulator fragments themselves --
@@ -777,14 +800,21 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   __syncthreads();
   if (prof) pst[4] = eg_stamp();
   {
-    const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
+    const int64_t last_row = min(m0 + BM, (int64_t)a.M) - 1;
     const int nslot = (int)(last_row / a.P - roi_base) + 1;
-    for (int q = tid; q < nslot * 256; q += 256) {
+    for (int q = tid; q < nslot * 256; q += NT) {
       const int slot = q >> 8, c = q & 255;
       const int64_t roi = roi_base + slot;
-      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
-      a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] =
-          llrintf(part[slot * 256 + c] * kFix) + llrintf(part[(G4_SLOTS + slot) * 256 + c] * kFix);
+      long long v = 0;
+#pragma unroll
+      for (int w = 0; w < WMV; ++w) v += llrintf(part[(w * G4_SLOTS + slot) * 256 + c] * kFix);
+      // partial j = the ROI's 128-row block index; a 256-row tile covers two blocks: the sum
+      // goes to the first one inside the ROI, 0 to the second (every partial written once)
+      const int64_t rb0 = roi * a.P / kPartRows, rb1 = (roi * a.P + a.P - 1) / kPartRows;
+      const int64_t tb0 = max(m0 / kPartRows, rb0);
+      long long* o = a.sums + (roi * kPart + (tb0 - rb0)) * a.ld_sums + g * a.N + n0 + c;
+      o[0] = v;
+      if (WMV == 4 && tb0 + 1 <= rb1 && tb0 + 1 <= (m0 + BM - 1) / kPartRows) o[a.ld_sums] = 0;
     }
   }
   if (prof) pst[5] = eg_stamp();
@@ -793,7 +823,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
     const int64_t cbase = (int64_t)g * a.N + n0;
 #pragma unroll 4
     for (int q = 0; q < 16; ++q) {
-      const int p = q * 256 + tid, rl = p >> 5, c8 = (p & 31) * 8;
+      const int p = q * NT + tid, rl = p >> 5, c8 = (p & 31) * 8;
       const int64_t row = m0 + rl;
       if (row < a.M)
         *reinterpret_cast<uint4*>(a.C + row * a.ldc + cbase + c8) =
@@ -822,6 +852,12 @@ __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t nt
   if (EPI == EPI_DSC && (lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1, SMF>(a, lb, smem);
   else gemm4_tile<EPI, WIDE, 0, SMF>(a, lb, smem);
 }
+// the 256 x 256 transition tile (gemm4_tile WMV = 4): 8 waves, one workgroup per CU
+__global__ void __launch_bounds__(512, 1) gemm4w_trans_kernel(EncGemmArgs a, int64_t ntiles) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  gemm4_tile<EPI_TRANS, true, 0, 1, 4>(a, xcd_remap(blockIdx.x, ntiles), smem);
+}
+constexpr size_t G4W_RING = (size_t)3 * (256 * 4 + 1024) * 16;  // 96 KiB
 
 // ---------------------------------------------------------------------------
 // g1dw4 (g1dw_mode 7): g1dw_kernel's first 1x1 convs + depthwise 5x5 on 4-wave
@@ -2290,6 +2326,227 @@ __global__ void __launch_bounds__(512, 1) rmb_fused_kernel(RfArgs a) {
   else rf2_body<0, 1>(a, lb, smem);
 }
 
+// ---------------------------------------------------------------------------
+// trans4 (trk_set_tuning("enc_trans", 1)): the transition (K = 1024, x_f = the first 512
+// columns scaled by s) on gemm4's 128 x 256 tiles, with the weights read straight into
+// VGPRs instead of through LDS.  4 waves as 1 (M) x 4 (N): wave w owns 64 output
+// columns for all 128 rows (8 x 4 MFMA 16x16x32 tiles), so no weight element is used by
+// two waves of the workgroup and the pre-packed fragments (ops.enc_pack_fragments_k: [k
+// step][16-col tile][lane] x 16 B) arrive as one contiguous 4 KiB per wave and K step,
+// two steps ahead (asm loads, counted vmcnt, rmb_front's rf_loadB).  LDS carries only the
+// activation rows: an 8 KiB stage per K step (3-stage LDS-DMA ring, swizzle and SE scaling
+// as gemm4) + the s tile, 32 KiB per workgroup; per K step and CU that is 16 KB of DMA and
+// 64 KB of fragment reads against gemm4's 48 + 96.  MFMA operands, K order and the per-
+// 64-row-block sums are gemm4's, so T and the ROI sums are bit-identical to it.
+constexpr int T4_NK = 32;                       // K = 1024
+constexpr int T4_BUF = 512;                     // uint4 per stage: 128 rows x 64 B
+constexpr size_t T4_RING = (size_t)3 * T4_BUF * 16;
+
+__global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uint4* Wtp, int64_t ntiles) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t lb = xcd_remap(blockIdx.x, ntiles);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntile_n = a.N / 256;
+  const int n0 = (int)(lb % ntile_n) * 256;
+  const int64_t m0 = lb / ntile_n * 128;
+  const int64_t roi_base = m0 / a.P;
+  const int fr = lane & 15, fc = lane >> 4;
+
+  const uint16_t* asrc[2];
+  int arow[2], achk[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x16(r);
+    arow[q] = r;
+    achk[q] = c;
+    asrc[q] = a.A + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
+  }
+  const uint4* bp = Wtp + (size_t)(n0 / 16 + wave * 4) * 64 + lane;
+  u32x4 bq[3][4];
+  auto issue = [&](int kt) {
+    uint4* d = ring + (kt % 3) * T4_BUF + wave * 64;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
+    rf_loadB(bp, kt, bq[kt % 3]);
+  };
+
+  // the s tile (the slots a 128-row tile spans) behind the ring, as gemm4
+  float* stile = reinterpret_cast<float*>(smem + T4_RING);
+  const float* srow[2];
+  {
+    const int per = 512 / 4;
+    const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
+    const int tslots = min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = q * 256 + tid;
+      if (p >= tslots * per) continue;
+      const int slot = min(p / per, G4_SLOTS - 1);
+      const int64_t roi = min(roi_base + slot, nroi - 1);
+      __builtin_amdgcn_global_load_lds(GPTR(a.scale + roi * 512 + (p % per) * 4),
+                                       LPTR(reinterpret_cast<uint4*>(stile) + q * 256 + wave * 64), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t row = min(m0 + arow[q], (int64_t)a.M - 1);
+      srow[q] = stile + (int)(row / a.P - roi_base) * 512 + achk[q] * 8;
+    }
+  }
+  // bf16(x * s) in place on this thread's own two DMA'd chunks of stage kt (x_f steps)
+  auto transform = [&](int kt) {
+    const uint32_t d = lds_addr(ring + (kt % 3) * T4_BUF + tid);
+    u32x4 v[2], s4[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      v[q] = lds_read128(d + q * 256 * 16);
+      const uint32_t sa = lds_addr(srow[q] + kt * BK);
+      s4[q][0] = lds_read128(sa);
+      s4[q][1] = lds_read128(sa + 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(s4[0][0]), "+v"(s4[0][1]), "+v"(s4[1][0]),
+                 "+v"(s4[1][1])::"memory");
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float s_lo = __uint_as_float(s4[q][e >> 1][(2 * e) & 3]);
+        const float s_hi = __uint_as_float(s4[q][e >> 1][(2 * e + 1) & 3]);
+        o[e] = pack_bf16x2(__uint_as_float(v[q][e] << 16) * s_lo, __uint_as_float(v[q][e] & 0xffff0000u) * s_hi);
+      }
+      lds_write128(d + q * 256 * 16, o);
+    }
+  };
+
+  const int lterm = fr * 4 + (fc ^ x16(fr));
+  f4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  unsigned long long pst[8];
+  const bool prof = a.prof != nullptr;
+  if (prof) pst[0] = eg_stamp();
+  issue(0);
+  issue(1);
+  rf_vmwait(6, bq[0]);  // stage 0 (own A chunks and B(0)); the s tile is older
+  g4_barrier();         // every wave's s-tile DMA landed
+  transform(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g4_barrier();
+#pragma unroll
+  for (int kt = 0; kt < T4_NK; ++kt) {
+    const uint4* buf = ring + (kt % 3) * T4_BUF;
+    bf8v afr[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + lterm + i * 64);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], __builtin_bit_cast(bf8v, bq[kt % 3][t]),
+                                                            acc[i][t], 0, 0, 0);
+    if (kt + 2 < T4_NK) {
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 2);
+    }
+    if (kt + 1 < T4_NK) {
+      rf_vmwait(kt + 2 < T4_NK ? 6 : 0, bq[(kt + 1) % 3]);
+      if ((kt + 1) * BK < 512) transform(kt + 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    g4_barrier();
+  }
+  if (prof) pst[1] = eg_stamp();
+
+  // ---- SiLU(T + bias), then gemm4's MFMA ROI sums per 64-row half (rows 64 h ..)
+  const int colq = wave * 64 + fr;  // + t * 16 (column within the tile)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float bv = a.bias[n0 + colq + t * 16];
+    const f2v b2 = {bv, bv};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        f2v v = f2v{acc[i][t][2 * hh], acc[i][t][2 * hh + 1]} + b2;
+        v = silu2(v);
+        acc[i][t][2 * hh] = v.x;
+        acc[i][t][2 * hh + 1] = v.y;
+      }
+  }
+  if (prof) pst[2] = eg_stamp();
+  float* part = reinterpret_cast<float*>(smem);  // [2 halves][SLOTS][256] (the ring is idle)
+  {
+    const int P = a.P;
+    const int off = (int)(m0 - roi_base * P);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf8v mask[2];
+#pragma unroll
+      for (int p2 = 0; p2 < 2; ++p2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int rl = h * 64 + (2 * p2 + (j >> 2)) * 16 + 4 * fc + (j & 3);
+          const int x = off + rl;
+          const int slot = (x >= P) + (x >= 2 * P) + (x >= 3 * P);
+          mask[p2][j] = (slot == fr && m0 + rl < (int64_t)a.M) ? (__bf16)1.0f : (__bf16)0.0f;
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f4v sacc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p2 = 0; p2 < 2; ++p2) {
+          const f4v u = acc[4 * h + 2 * p2][t], v = acc[4 * h + 2 * p2 + 1][t];
+          bf8v hi, lo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            hi[e] = (__bf16)u[e];
+            hi[4 + e] = (__bf16)v[e];
+            lo[e] = (__bf16)(u[e] - (float)hi[e]);
+            lo[4 + e] = (__bf16)(v[e] - (float)hi[4 + e]);
+          }
+          sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mask[p2], hi, sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mask[p2], lo, sacc, 0, 0, 0);
+        }
+        if (lane < 16) {
+#pragma unroll
+          for (int ts = 0; ts < G4_SLOTS; ++ts) part[(h * G4_SLOTS + ts) * 256 + colq + t * 16] = sacc[ts];
+        }
+      }
+    }
+  }
+  if (prof) pst[3] = eg_stamp();
+  __syncthreads();
+  {
+    const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
+    const int nslot = (int)(last_row / a.P - roi_base) + 1;
+    for (int q = tid; q < nslot * 256; q += 256) {
+      const int slot = q >> 8, c = q & 255;
+      const int64_t roi = roi_base + slot;
+      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
+      a.sums[(roi * kPart + j) * a.ld_sums + n0 + c] =
+          llrintf(part[slot * 256 + c] * kFix) + llrintf(part[(G4_SLOTS + slot) * 256 + c] * kFix);
+    }
+  }
+  if (prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pst[4] = eg_stamp();
+    if (tid == 0) {
+      unsigned long long* o = a.prof + lb * 8;
+      for (int q = 0; q < 4; ++q) o[q] = pst[q + 1] - pst[q];
+      o[4] = pst[4] - pst[0];
+      o[5] = o[6] = o[7] = 0;
+    }
+  }
+}
+
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
@@ -2385,6 +2642,12 @@ extern "C" int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg
 extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
                                        int64_t kscale, const void* Wt, const float* bias, int64_t N,
                                        long long* sums, void* stream) {
+  return trk_enc_transition_gemm2(XRN, M, P, K, s, kscale, Wt, nullptr, bias, N, sums, stream);
+}
+
+extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
+                                        int64_t kscale, const void* Wt, const void* Wtp, const float* bias,
+                                        int64_t N, long long* sums, void* stream) {
   TRK_REQUIRE(M >= 0 && P >= 32 && P <= 256 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 &&
                   kscale % BK == 0 && kscale <= K,
               "enc_transition_gemm: need 32 <= P <= 256, K %% 32 == 0, N %% 256 == 0, kscale %% 32 == 0");
@@ -2398,6 +2661,29 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
+  if (g_enc_gemm >= 1 && g_enc_trans == 1 && P >= 43 && K == 1024 && kscale == 512 && Wtp) {
+    const int64_t nwg = ((int64_t)M + 127) / 128 * (N / 256);
+    TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
+    a.prof = g_enc_prof;
+    hipLaunchKernelGGL(trans4_kernel, dim3((unsigned)nwg), dim3(256), T4_RING + (size_t)G4_SLOTS * 512 * 4, st, a,
+                       reinterpret_cast<const uint4*>(Wtp), nwg);
+    return trk::check_launch("trans4_kernel");
+  }
+  if (g_enc_gemm >= 1 && g_enc_trans_wide && P >= 86 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) {
+    const int64_t nwg = ((int64_t)M + 255) / 256 * (N / 256);
+    TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4w_trans_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    a.prof = g_enc_prof;
+    const int tslots = std::min(G4_SLOTS, (255 + (int)P - 1) / (int)P + 1);
+    const size_t lds = G4W_RING + (size_t)tslots * kscale * 4;
+    hipLaunchKernelGGL(gemm4w_trans_kernel, dim3((unsigned)nwg), dim3(512), lds, st, a, nwg);
+    return trk::check_launch("gemm4w_trans_kernel");
+  }
   if (g_enc_gemm >= 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
   return launch<EPI_TRANS, 128, 256>(a, st);
 }

@@ -279,7 +279,7 @@ class Model(nn.Module):
             if self.fused_tail:
                 # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
                 m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
-                tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True)
+                tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True, Wtp=W.get("wt_pk"))
                 head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                         self.head.net[1].eps, W["h4"], W["h4b"])
                 if not self.defer_head:
@@ -292,7 +292,7 @@ class Model(nn.Module):
             f = enc_sums_reduce(sums, ss)
             m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
             s = self._se(m_r)
-            m_cat = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"]) / ss
+            m_cat = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], Wtp=W.get("wt_pk")) / ss
             a = self._alpha()
             g = 0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n)
             return self._head(g)

@@ -265,10 +265,12 @@ def enc_rmb_fused(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: to
 
 
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
-                        bias: torch.Tensor, raw: bool = False) -> torch.Tensor:
+                        bias: torch.Tensor, raw: bool = False, Wtp: torch.Tensor = None) -> torch.Tensor:
     """sum over each ROI's P rows of SiLU([x_f * s | x_n] . Wt^T + bias):
     XRN [M, K] bf16 (x_f = first kscale = s.shape[1] columns), s [R, kscale]
-    f32, Wt [N, K] bf16 -> [R, N] f32 (raw=True: the int64 x 2^24 sums, for enc_head)."""
+    f32, Wt [N, K] bf16 -> [R, N] f32 (raw=True: the int64 x 2^24 sums, for enc_head).
+    Wtp: optionally Wt as enc_pack_fragments_k(Wt), which the trans4 kernel
+    (set_tuning("enc_trans", 1)) reads straight into registers; same bits either way."""
     _need_gpu(XRN, "enc_transition_gemm")
     if XRN.dtype != torch.bfloat16 or Wt.dtype != torch.bfloat16:
         raise TypeError("enc_transition_gemm: bf16 operands required")
@@ -277,11 +279,14 @@ def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Te
     R = (M + P - 1) // P
     if K2 != K or s.shape[0] != R or bias.numel() != N:
         raise ValueError("enc_transition_gemm: shape mismatch")
+    if Wtp is not None and (Wtp.dtype != torch.bfloat16 or Wtp.numel() != Wt.numel() or not Wtp.is_contiguous()):
+        raise ValueError("enc_transition_gemm: Wtp must be enc_pack_fragments_k(Wt)")
     XRN, Wt = XRN.contiguous(), Wt.contiguous()
     s, bias = s.to(torch.float32).contiguous(), bias.to(torch.float32).contiguous()
     sums = torch.empty((R, _lib.TRK_ENC_PARTS, N), device=XRN.device, dtype=torch.int64)  # partials
-    check(lib().trk_enc_transition_gemm(_ptr(XRN), M, P, K, _ptr(s), s.shape[1], _ptr(Wt), _ptr(bias), N,
-                                        _ptr(sums), _stream(XRN.device)), "enc_transition_gemm")
+    check(lib().trk_enc_transition_gemm2(_ptr(XRN), M, P, K, _ptr(s), s.shape[1], _ptr(Wt),
+                                         _ptr(Wtp) if Wtp is not None else None, _ptr(bias), N,
+                                         _ptr(sums), _stream(XRN.device)), "enc_transition_gemm")
     if raw:
         return sums
     return enc_sums_reduce(sums, P)

@@ -404,6 +404,7 @@ class LiveProbe:
 
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_nchw_to_nhwc": "map_nhwc", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
+             "trk_enc_transition_gemm2": "enc_gemm_trans",
              "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_rmb_fused": "enc_rmb_fused",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
@@ -527,7 +528,8 @@ def kernel_pass(pipe, f, reps=10):
     XRN, sum_r, _ = ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"])
     with torch.no_grad():
         s_se = m._se(sum_r / 100)
-    timed("enc_gemm_trans", lambda: ops.enc_transition_gemm(XRN, 100, s_se, W["wt_nk"], W["bt_f"]))
+    timed("enc_gemm_trans", lambda: ops.enc_transition_gemm(XRN, 100, s_se, W["wt_nk"], W["bt_f"],
+                                                            Wtp=W.get("wt_pk")))
     timed("encoder", lambda: pipe.stage_embed(roi))
     emb = pipe.stage_embed(roi)
     # tracker kernels on the current track table (rows = all live tracks)

@@ -272,6 +272,13 @@ int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wd
                       float* m_n, float* s, long long* tsums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
+/* trk_enc_transition_gemm2: the same, also given Wtp = Wt in the fragment order of trk_enc_rmb_fused
+ *   (may be NULL).  With Wtp, K = 1024, kscale = 512 and trk_set_tuning("enc_trans", 1) the
+ *   weights are read straight into registers (trans4 kernel) instead of through LDS; the sums
+ *   are bit-identical either way. */
+int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
+                             const void* Wt, const void* Wtp, const float* bias, int64_t N, long long* sums,
+                             void* stream);
 /* Per-ROI tail of the encoder (f32, 16 ROIs per workgroup, f32-input MFMA).
  * trk_enc_se: squeeze means and SE excitation (card.py:59-78) from the partial
  *   sums of trk_enc_dsc_gemm ([R][TRK_ENC_PARTS][ld_sums], ld_sums >= 2C: C sums

@@ -693,6 +693,65 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
         assert (d == 0).float().mean().item() >= 0.9
 
 
+@pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (86, 61)])
+def test_enc_transition_wide_tile_vs_default(trk, gpu, P, R):
+    """The transition on 256 x 256 tiles (enc_trans_wide 1: 8 waves, one workgroup per CU)
+    vs the default 128 x 256 tiles: the same wave tiles (64 rows x 128 columns) on the same
+    64-row blocks, MFMA K order and SE-scaled bf16 operands, and the per-ROI sums are int64
+    sums of the same per-wave f32 partials -- so the reduced sums must be bit-identical.
+    A 256-row tile covers two 128-row partial slots: P = 100 / 200 put ROIs across both
+    (the second one must be written as 0), R = 1 and 37 leave the last tile ragged."""
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(1000 + R)
+    M, Ng = R * P, 512
+    XRN = torch.randn(M, 2 * Ng, generator=g).to(gpu).bfloat16()
+    s = torch.rand(R, Ng, generator=g).to(gpu)
+    Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
+    bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
+    ref = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+    L = trk.lib()
+    try:
+        assert L.trk_set_tuning(b"enc_trans_wide", 1) == 0
+        raw = ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True)
+        raw.fill_(0x5A5A5A5A5A5A)  # stale partials must be overwritten, not added to
+        got = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+        got2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+    finally:
+        L.trk_set_tuning(b"enc_trans_wide", 0)
+    assert torch.equal(got, ref) and torch.equal(got2, ref)  # (no fragments given: gemm4 either way)
+
+
+@pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (49, 29)])
+def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R):
+    """trans4 (enc_trans 1: the weights straight into VGPRs from the packed fragments,
+    4 waves x 64 columns x 128 rows) vs gemm4 (weights through LDS, 2 x 2 waves): the same
+    MFMA operands and K order, the same SE-scaled bf16 rows and the same per-64-row-block
+    MFMA sums, so the reduced ROI sums must be bit-identical; deterministic run to run."""
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(2000 + R + P)
+    M, Ng = R * P, 512
+    XRN = torch.randn(M, 2 * Ng, generator=g).to(gpu).bfloat16()
+    s = torch.rand(R, Ng, generator=g).to(gpu)
+    Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
+    bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
+    Wtp = ops.enc_pack_fragments_k(Wt)
+    ref = ops.enc_transition_gemm(XRN, P, s, Wt, bt)  # no fragments: gemm4 whatever the knob
+    L = trk.lib()
+    try:
+        assert L.trk_set_tuning(b"enc_trans", 1) == 0
+        got = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+        got2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+        assert L.trk_set_tuning(b"enc_trans", 0) == 0
+        nopk = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)  # knob 0: gemm4 with the fragments given
+    finally:
+        L.trk_set_tuning(b"enc_trans", 1)
+    assert torch.equal(got, ref) and torch.equal(got2, ref) and torch.equal(nopk, ref)
+    with pytest.raises(ValueError, match="enc_pack_fragments_k"):
+        ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp[:-1])
+
+
 @pytest.mark.parametrize("rf_v,rf_lag", [(2, 16), (2, 8), (2, 0), (1, 16)])
 @pytest.mark.parametrize("R", [1, 37, 2048])
 def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag):
