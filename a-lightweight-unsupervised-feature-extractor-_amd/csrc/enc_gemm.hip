@@ -34,6 +34,8 @@
 //   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
 #include "trk_common.h"
 
+#include <utility>
+
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
 int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
 int g_enc_lds_tight = 1;  // trk_set_tuning("enc_lds_tight"): gemm4 launched with the LDS its tile uses (1) or 80 KiB
@@ -46,6 +48,11 @@ int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halve
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
+int g_t4_mode = 5;  // trk_set_tuning("t4_mode"): trans4 pipeline (K steps per LDS stage, B distance):
+                    // 0 = (1, 2), 1 = (2, 2), 2 = (1, 3), 3 = (2, 3); 4..6 = (1, 2) + setprio / mid-step issue /
+                    // both; 7 = (2, 3) + both.  Isolated medians (tools/exp/trans_ab.py): 244.1, 240.0 (3),
+                    // 248.7 (4), 235.4 (5), 241.3 (6), 245.0 (7) us; pipeline 5 vs 0 in three interleaved pairs
+                    // 1.983/1.990/1.952M vs 1.954/1.954/1.942M ROIs/s: 5 (mid-step issue) is the default
 int g_enc_trans_wide = 0;  // trk_set_tuning("enc_trans_wide"): 1 = gemm4's transition on 256 x 256 tiles (8
                            // waves, one workgroup per CU; P >= 86; 301 vs 282 us isolated, pipeline 2 of 3 pairs
                            // lost: kept as a tested variant), 0 = 128 x 256 tiles, two workgroups per CU
@@ -1167,7 +1174,8 @@ __device__ __forceinline__ void rf_vmwait(int n, u32x4 (&b)[4]) {
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory"); break;
   switch (n) {
     RF_VMW(1) RF_VMW(2) RF_VMW(3) RF_VMW(4) RF_VMW(5) RF_VMW(6) RF_VMW(7) RF_VMW(8) RF_VMW(9) RF_VMW(10)
-    RF_VMW(11) RF_VMW(12) RF_VMW(13) RF_VMW(14) RF_VMW(15)
+    RF_VMW(11) RF_VMW(12) RF_VMW(13) RF_VMW(14) RF_VMW(15) RF_VMW(16) RF_VMW(17) RF_VMW(18) RF_VMW(19)
+    RF_VMW(20) RF_VMW(21) RF_VMW(22) RF_VMW(23) RF_VMW(24)
     default: asm volatile("s_waitcnt vmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
   }
 #undef RF_VMW
@@ -2339,10 +2347,55 @@ __global__ void __launch_bounds__(512, 1) rmb_fused_kernel(RfArgs a) {
 // 64 KB of fragment reads against gemm4's 48 + 96.  MFMA operands, K order and the per-
 // 64-row-block sums are gemm4's, so T and the ROI sums are bit-identical to it.
 constexpr int T4_NK = 32;                       // K = 1024
-constexpr int T4_BUF = 512;                     // uint4 per stage: 128 rows x 64 B
-constexpr size_t T4_RING = (size_t)3 * T4_BUF * 16;
+constexpr int T4_BUF = 512;                     // uint4 per K step: 128 rows x 64 B
+// SPS K steps per LDS stage (one barrier per stage), 3 stages: stage j + 2 is issued at the
+// start of stage j; B fragments BD steps ahead in BD + 1 register sets.  Issue order:
+// A stage 0, B(0), A stage 1, B(1) .. B(BD - 1); step kt: B(kt + BD), then (first step of
+// a stage) the A stage two ahead.  t4_vm(kt) = ops issued after the youngest op the end
+// of step kt needs (B(kt + 1); at a stage end also the next A stage): its vmcnt.
+template <int SPS, int BD>
+constexpr int t4_vm(int kt) {
+  constexpr int NS = T4_NK / SPS;
+  int bend[T4_NK] = {}, aend[T4_NK] = {};
+  int pos = 2 * SPS;
+  aend[0] = pos;
+  pos += 4;
+  bend[0] = pos;
+  pos += 2 * SPS;
+  aend[1] = pos;
+  pos += 4;
+  bend[1] = pos;
+  for (int b = 2; b < BD; ++b) bend[b] = (pos += 4);
+  if (kt < 0) return pos - (aend[0] > bend[0] ? aend[0] : bend[0]);
+  for (int k = 0; k <= kt; ++k) {
+    if (k + BD < T4_NK) bend[k + BD] = (pos += 4);
+    if (k % SPS == 0 && k / SPS + 2 < NS) aend[k / SPS + 2] = (pos += 2 * SPS);
+  }
+  int need = kt + 1 < T4_NK ? bend[kt + 1] : pos;
+  if ((kt + 1) % SPS == 0 && kt + 1 < T4_NK && aend[(kt + 1) / SPS] > need) need = aend[(kt + 1) / SPS];
+  return pos - need;
+}
+template <int SPS, int BD>
+constexpr bool t4_vm_ok() {
+  for (int kt = -1; kt < T4_NK; ++kt)
+    if (t4_vm<SPS, BD>(kt) < 0 || t4_vm<SPS, BD>(kt) > 24) return false;
+  return true;
+}
+static_assert(t4_vm<1, 2>(-1) == 6 && t4_vm<1, 2>(0) == 6 && t4_vm<1, 2>(T4_NK - 2) == 0, "trans4 vmcnt: gemm4 order");
 
+// f(integral_constant<int, k>) for k = 0, 1, ...: a loop whose index is a constant expression
+template <typename F, int... K>
+__device__ __forceinline__ void seq_for(F&& f, std::integer_sequence<int, K...>) {
+  (f(std::integral_constant<int, K>{}), ...);
+}
+
+// OPT bit 0: s_setprio(1) over each step's MFMAs; bit 1: the step's B loads and A DMA issued
+// between its MFMAs (after row tiles 1 and 3) instead of after them
+template <int SPS, int BD, int OPT = 0>
 __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uint4* Wtp, int64_t ntiles) {
+  static_assert(t4_vm_ok<SPS, BD>(), "trans4 vmcnt out of the rf_vmwait range");
+  constexpr int NS = T4_NK / SPS, NSLOT = 3 * SPS;
+  constexpr size_t RING = (size_t)NSLOT * T4_BUF * 16;
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t lb = xcd_remap(blockIdx.x, ntiles);
   uint4* ring = reinterpret_cast<uint4*>(smem);
@@ -2366,17 +2419,21 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
     asrc[q] = a.A + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
   }
   const uint4* bp = Wtp + (size_t)(n0 / 16 + wave * 4) * 64 + lane;
-  u32x4 bq[3][4];
-  auto issue = [&](int kt) {
-    uint4* d = ring + (kt % 3) * T4_BUF + wave * 64;
+  u32x4 bq[BD + 1][4];
+  auto issueA = [&](int st) {  // the SPS K steps of stage st
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
-    rf_loadB(bp, kt, bq[kt % 3]);
+    for (int u = 0; u < SPS; ++u) {
+      const int kt = st * SPS + u;
+      uint4* d = ring + (kt % NSLOT) * T4_BUF + wave * 64;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
+    }
   };
+  auto loadB = [&](int kt) { rf_loadB(bp, kt, bq[kt % (BD + 1)]); };
 
   // the s tile (the slots a 128-row tile spans) behind the ring, as gemm4
-  float* stile = reinterpret_cast<float*>(smem + T4_RING);
+  float* stile = reinterpret_cast<float*>(smem + RING);
   const float* srow[2];
   {
     const int per = 512 / 4;
@@ -2397,9 +2454,9 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
       srow[q] = stile + (int)(row / a.P - roi_base) * 512 + achk[q] * 8;
     }
   }
-  // bf16(x * s) in place on this thread's own two DMA'd chunks of stage kt (x_f steps)
+  // bf16(x * s) in place on this thread's own two DMA'd chunks of K step kt (x_f steps)
   auto transform = [&](int kt) {
-    const uint32_t d = lds_addr(ring + (kt % 3) * T4_BUF + tid);
+    const uint32_t d = lds_addr(ring + (kt % NSLOT) * T4_BUF + tid);
     u32x4 v[2], s4[2][2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -2422,6 +2479,11 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
       lds_write128(d + q * 256 * 16, o);
     }
   };
+  auto transform_stage = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < SPS; ++u)
+      if ((st * SPS + u) * BK < 512) transform(st * SPS + u);
+  };
 
   const int lterm = fr * 4 + (fc ^ x16(fr));
   f4v acc[8][4];
@@ -2433,36 +2495,61 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
   unsigned long long pst[8];
   const bool prof = a.prof != nullptr;
   if (prof) pst[0] = eg_stamp();
-  issue(0);
-  issue(1);
-  rf_vmwait(6, bq[0]);  // stage 0 (own A chunks and B(0)); the s tile is older
-  g4_barrier();         // every wave's s-tile DMA landed
-  transform(0);
+  issueA(0);
+  loadB(0);
+  issueA(1);
+  loadB(1);
+#pragma unroll
+  for (int b = 2; b < BD; ++b) loadB(b);
+  rf_vmwait(t4_vm<SPS, BD>(-1), bq[0]);  // A stage 0 (own chunks) and B(0); the s tile is older
+  g4_barrier();                           // every wave's s-tile DMA landed
+  transform_stage(0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   g4_barrier();
-#pragma unroll
-  for (int kt = 0; kt < T4_NK; ++kt) {
-    const uint4* buf = ring + (kt % 3) * T4_BUF;
+  // the K steps as a compile-time sequence (the counted waits, ring slots and register
+  // sets must be immediates; #pragma unroll gave up on the deeper variants)
+  auto step = [&](auto ktc) {
+    constexpr int kt = decltype(ktc)::value;
+    const uint4* buf = ring + (kt % NSLOT) * T4_BUF;
     bf8v afr[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + lterm + i * 64);
+    if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], __builtin_bit_cast(bf8v, bq[kt % 3][t]),
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], __builtin_bit_cast(bf8v, bq[kt % (BD + 1)][t]),
                                                             acc[i][t], 0, 0, 0);
-    if (kt + 2 < T4_NK) {
-      __builtin_amdgcn_sched_barrier(0);
-      issue(kt + 2);
+      if constexpr (OPT & 2) {
+        if (i == 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (kt + BD < T4_NK) loadB(kt + BD);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (i == 3) {
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
-    if (kt + 1 < T4_NK) {
-      rf_vmwait(kt + 2 < T4_NK ? 6 : 0, bq[(kt + 1) % 3]);
-      if ((kt + 1) * BK < 512) transform(kt + 1);
+    if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!(OPT & 2)) {
+      if constexpr (kt + BD < T4_NK) loadB(kt + BD);
+      if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    g4_barrier();
-  }
+    if constexpr (kt + 1 < T4_NK) {
+      rf_vmwait(t4_vm<SPS, BD>(kt), bq[(kt + 1) % (BD + 1)]);
+      if constexpr ((kt + 1) % SPS == 0) {
+        transform_stage((kt + 1) / SPS);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        g4_barrier();
+      }
+    }
+  };
+  seq_for(step, std::make_integer_sequence<int, T4_NK>{});
   if (prof) pst[1] = eg_stamp();
 
   // ---- SiLU(T + bias), then gemm4's MFMA ROI sums per 64-row half (rows 64 h ..)
@@ -2665,8 +2752,24 @@ extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, i
     const int64_t nwg = ((int64_t)M + 127) / 128 * (N / 256);
     TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
     a.prof = g_enc_prof;
-    hipLaunchKernelGGL(trans4_kernel, dim3((unsigned)nwg), dim3(256), T4_RING + (size_t)G4_SLOTS * 512 * 4, st, a,
-                       reinterpret_cast<const uint4*>(Wtp), nwg);
+    const size_t slds = (size_t)G4_SLOTS * 512 * 4;
+    const uint4* wp = reinterpret_cast<const uint4*>(Wtp);
+    if (g_t4_mode == 1)
+      hipLaunchKernelGGL((trans4_kernel<2, 2>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 2)
+      hipLaunchKernelGGL((trans4_kernel<1, 3>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 3)
+      hipLaunchKernelGGL((trans4_kernel<2, 3>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 4)
+      hipLaunchKernelGGL((trans4_kernel<1, 2, 1>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 5)
+      hipLaunchKernelGGL((trans4_kernel<1, 2, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 6)
+      hipLaunchKernelGGL((trans4_kernel<1, 2, 3>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 7)
+      hipLaunchKernelGGL((trans4_kernel<2, 3, 3>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else
+      hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
     return trk::check_launch("trans4_kernel");
   }
   if (g_enc_gemm >= 1 && g_enc_trans_wide && P >= 86 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) {

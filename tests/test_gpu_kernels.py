@@ -722,12 +722,15 @@ def test_enc_transition_wide_tile_vs_default(trk, gpu, P, R):
     assert torch.equal(got, ref) and torch.equal(got2, ref)  # (no fragments given: gemm4 either way)
 
 
+@pytest.mark.parametrize("t4_mode", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (49, 29)])
-def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R):
+def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R, t4_mode):
     """trans4 (enc_trans 1: the weights straight into VGPRs from the packed fragments,
     4 waves x 64 columns x 128 rows) vs gemm4 (weights through LDS, 2 x 2 waves): the same
     MFMA operands and K order, the same SE-scaled bf16 rows and the same per-64-row-block
-    MFMA sums, so the reduced ROI sums must be bit-identical; deterministic run to run."""
+    MFMA sums, so the reduced ROI sums must be bit-identical; deterministic run to run.
+    t4_mode: K steps per LDS stage x B prefetch distance (0: 1x2, 1: 2x2, 2: 1x3, 3: 2x3) and
+    4-7: setprio / mid-step issue (5, mid-step issue at 1x2, is the default)."""
     from importlib import import_module
     ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
     g = torch.Generator().manual_seed(2000 + R + P)
@@ -740,13 +743,14 @@ def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R):
     ref = ops.enc_transition_gemm(XRN, P, s, Wt, bt)  # no fragments: gemm4 whatever the knob
     L = trk.lib()
     try:
-        assert L.trk_set_tuning(b"enc_trans", 1) == 0
+        assert L.trk_set_tuning(b"enc_trans", 1) == 0 and L.trk_set_tuning(b"t4_mode", t4_mode) == 0
         got = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
         got2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
         assert L.trk_set_tuning(b"enc_trans", 0) == 0
         nopk = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)  # knob 0: gemm4 with the fragments given
     finally:
         L.trk_set_tuning(b"enc_trans", 1)
+        L.trk_set_tuning(b"t4_mode", 5)  # the default
     assert torch.equal(got, ref) and torch.equal(got2, ref) and torch.equal(nopk, ref)
     with pytest.raises(ValueError, match="enc_pack_fragments_k"):
         ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp[:-1])

@@ -16,7 +16,8 @@ bt = torch.randn(512, device=dev, generator=g) / 4
 Wtp = ops.enc_pack_fragments_k(Wt)
 L = ops.lib()
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-VARS = {"gemm4": (0, 0), "gemm4_wide": (1, 0), "trans4": (0, 1)}
+VARS = {"gemm4": (0, 0, 0), "trans4_1x2": (0, 1, 0), "trans4_2x3": (0, 1, 3), "t4_prio": (0, 1, 4),
+        "t4_mid": (0, 1, 5), "t4_prio_mid": (0, 1, 6), "t4_2x3_prio_mid": (0, 1, 7)}
 res = {k: [] for k in VARS}
 outs = {}
 
@@ -24,6 +25,7 @@ outs = {}
 def setv(k):
     L.trk_set_tuning(b"enc_trans_wide", VARS[k][0])
     L.trk_set_tuning(b"enc_trans", VARS[k][1])
+    L.trk_set_tuning(b"t4_mode", VARS[k][2])
 
 
 for k in VARS:
@@ -39,7 +41,7 @@ for rnd in range(8):
         ev[1].record()
         torch.cuda.synchronize()
         res[k].append(ev[0].elapsed_time(ev[1]) * 100)
-setv("gemm4")
+setv("t4_mid")
 print(json.dumps({"us": {k: round(statistics.median(v), 1) for k, v in res.items()},
                   "all": {k: [round(x, 1) for x in v] for k, v in res.items()},
                   "identical": all(torch.equal(outs[k], outs["gemm4"]) for k in VARS)}), flush=True)
