@@ -197,7 +197,10 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   if (threadIdx.x == 0) ctl[3] = nr;
   __syncthreads();
   {
-    constexpr int R = KS >= 16 ? 2 : (KS >= 8 ? 4 : 8);  // rows in flight per wave
+    // rows in flight per wave: every row's loads are issued before the first reduction, so a
+    // 256-column frame takes 4 load round trips (8 at 8 rows; the cost matrix was just written
+    // on another XCD, so each round trip is an L2 miss)
+    constexpr int R = KS >= 16 ? 2 : (KS >= 8 ? 4 : 16);
     int bad = 0;
     for (int i0 = wave * R; i0 < nr; i0 += 4 * R) {
       T x[R][KS];
@@ -459,11 +462,14 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
     return;
   }
   if (!tr) {
+    // a matrix solved whole by the shortcut: no augmenting path moved any row or dual since,
+    // so u[q] still is C[q][col4row[q]] (exactly: the float minimum widened to double)
+    const int kp = ctl[3] >= nr ? nr : 0;
     for (int q = threadIdx.x; q < nr; q += blockDim.x) {
       const int c = col4row[q];
       orows[q] = q;
       ocols[q] = c;
-      if (assign) assign[q] = ((double)C[(int64_t)q * ld + c] <= A.cost_max) ? c : -1;
+      if (assign) assign[q] = ((q < kp ? u[q] : (double)C[(int64_t)q * ld + c]) <= A.cost_max) ? c : -1;
     }
   } else {
     // argsort(col4row): working column j (= original row j) is matched to

@@ -1058,6 +1058,17 @@ def test_lsap_prefix_shortcut_vs_oracle(trk, oracle, gpu):
         n = int(res["count"][k])
         assert np.array_equal(res["rows"][k, :n].cpu().numpy(), er)
         assert np.array_equal(res["cols"][k, :n].cpu().numpy(), ec)
+    # the cost gate (hungarian_assign, hung.py:35-40) on whole-prefix and cut matrices: a matrix
+    # solved whole by the shortcut reads its gate values from the duals (u = the row minimum)
+    for cmax in (0.03, 2.5):
+        res = trk.lsap_batched(torch.from_numpy(buf).to(gpu), [C.shape[0] for C in cases[:5]],
+                               [C.shape[1] for C in cases[:5]], cost_max=cmax)
+        for k, C in enumerate(cases[:5]):
+            er, ec = oracle.lsap(C)
+            exp = np.full(C.shape[0], -1, np.int64)
+            ok = C[er, ec].astype(np.float64) <= cmax
+            exp[er[ok]] = ec[ok]
+            assert np.array_equal(res["assign"][k, :C.shape[0]].cpu().numpy(), exp), (k, cmax)
 
 
 def test_roi_align_a1_boundary_branches_gpu(trk, oracle, gpu):
