@@ -125,6 +125,23 @@ __device__ __forceinline__ double wave_min(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// the same for a float (exact: a float minimum widened to double is the double minimum)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_min_step_f(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(0x7f800000, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
+  return o < v ? o : v;
+}
+__device__ __forceinline__ float wave_min_t(float v) {
+  v = dpp_min_step_f<0x111, 0xF>(v);
+  v = dpp_min_step_f<0x112, 0xF>(v);
+  v = dpp_min_step_f<0x114, 0xF>(v);
+  v = dpp_min_step_f<0x118, 0xF>(v);
+  v = dpp_min_step_f<0x142, 0xA>(v);
+  v = dpp_min_step_f<0x143, 0xC>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ double wave_min_t(double v) { return wave_min(v); }
+
 // lexicographic min over the wave; the result is returned wave-uniform
 // (row_shr 1/2/4/8 inside each row of 16, then row_bcast15 / row_bcast31,
 // total in lane 63).  (value, key) pairs are unique per column, so the order
@@ -175,6 +192,9 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   const size_t ring_off = ((size_t)(12 * nr + 4 * RB + 32) + 15) & ~size_t(15);
   T* ring = reinterpret_cast<T*>(smem + ring_off);
 
+  // diagnostics: workgroup phase stamps [entry, shortcut pass done, solver done, end]
+  unsigned long long ts[4] = {0, 0, 0, 0};
+  if (A.prof) ts[0] = stamp();
   for (int q = threadIdx.x; q < RB; q += blockDim.x) ready[q] = 0;
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 
@@ -211,39 +231,46 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
           const int c = lane + 64 * k;
           x[r][k] = (i0 + r < nr && k < ks && c < nc) ? gload(i0 + r, c) : (T)INFINITY;
         }
+      // the R rows' reductions are independent chains (the compiler interleaves them); each
+      // row's result is parked in lane r, and lanes < R publish the R rows at once
+      T m[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int i = i0 + r;
-        if (i < nr) {
-          double lm = INFINITY;  // this lane's minimum (invalid slots hold +inf)
+        T lm = (T)INFINITY;  // this lane's minimum (invalid slots hold +inf)
 #pragma unroll
-          for (int k = 0; k < KS; ++k) {
-            const T e = x[r][k];
-            if (e != e || e == (T)-INFINITY) bad = 1;
-            const double d = (double)e;
-            lm = d < lm ? d : lm;
-          }
-          const double m = wave_min(lm);
-          // entries equal to the minimum: unique iff one lane holds exactly one
-          int cnt = 0, col = 0;
-#pragma unroll
-          for (int k = 0; k < KS; ++k) {
-            const bool eq = (double)x[r][k] == m;
-            col = (eq && cnt == 0) ? lane + 64 * k : col;
-            cnt += eq ? 1 : 0;
-          }
-          const uint64_t holders = __ballot(cnt > 0);
-          const int hl = (int)__builtin_ctzll(holders | (1ull << 63));
-          const int hcnt = __builtin_amdgcn_readlane(cnt, hl);
-          const int hcol = __builtin_amdgcn_readlane(col, hl);
-          const bool uniq = m < INFINITY && __popcll(holders) == 1 && hcnt == 1;
-          if (lane == 0) {
-            u[i] = m;
-            col4row[i] = uniq ? hcol : -1;
-            if (uniq) atomicMin(&firstrow[hcol], i);
-            else atomicMin(&ctl[3], i);
-          }
+        for (int k = 0; k < KS; ++k) {
+          const T e = x[r][k];
+          if (e != e || e == (T)-INFINITY) bad = 1;
+          lm = e < lm ? e : lm;
         }
+        m[r] = wave_min_t(lm);
+      }
+      double my_m = 0.0;
+      int my_col = -1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        // entries equal to the minimum: unique iff one lane holds exactly one
+        int cnt = 0, col = 0;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const bool eq = x[r][k] == m[r];
+          col = (eq && cnt == 0) ? lane + 64 * k : col;
+          cnt += eq ? 1 : 0;
+        }
+        const uint64_t holders = __ballot(cnt > 0);
+        const int hl = (int)__builtin_ctzll(holders | (1ull << 63));
+        const int hcnt = __builtin_amdgcn_readlane(cnt, hl);
+        const int hcol = __builtin_amdgcn_readlane(col, hl);
+        const bool uniq = m[r] < (T)INFINITY && __popcll(holders) == 1 && hcnt == 1;
+        my_m = lane == r ? (double)m[r] : my_m;
+        my_col = lane == r ? (uniq ? hcol : -1) : my_col;
+      }
+      if (lane < R && i0 + lane < nr) {
+        const int i = i0 + lane;
+        u[i] = my_m;
+        col4row[i] = my_col;
+        if (my_col >= 0) atomicMin(&firstrow[my_col], i);
+        else atomicMin(&ctl[3], i);
       }
     }
     if (__any(bad) && lane == 0) ctl[1] = 1;
@@ -273,6 +300,7 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   }
   if (threadIdx.x == 0) ctl[0] = kpre;
   __syncthreads();  // firstrow read: the ring is the loaders' from here
+  if (A.prof) ts[1] = stamp();
 
   if (wave > 0) {
     // ------------------------------------------------------------ loaders
@@ -435,7 +463,7 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
       if (prof) { const unsigned long long t = stamp(); p_aug += t - p_t; p_t = t; }
     }
     if (prof && lane == 0) {
-      unsigned long long* o = A.prof + (int64_t)f * 8;
+      unsigned long long* o = A.prof + (int64_t)f * 16;
       o[0] = p_wait; o[1] = p_scan; o[2] = p_dual; o[3] = p_aug; o[4] = p_iter;
       o[5] = p_t - p_t0; o[6] = (unsigned long long)nr; o[7] = (unsigned long long)nc;
     }
@@ -452,6 +480,7 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
     }
   }
   __syncthreads();
+  if (A.prof) ts[2] = stamp();
   int status = ctl[2];
   if (ctl[4]) status = -3;  // a loader stalled: not a property of the matrix
   if (ctl[1]) status = -1;  // an invalid entry anywhere -> scipy raises (checked first)
@@ -461,6 +490,16 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
     if (threadIdx.x == 0) { A.count[f] = 0; A.status[f] = status; }
     return;
   }
+  auto prof_end = [&]() {
+    if (A.prof && threadIdx.x == 0) {
+      ts[3] = stamp();
+      unsigned long long* o = A.prof + (int64_t)f * 16 + 8;
+      o[0] = ts[1] - ts[0];  // shortcut pass (incl. set-up)
+      o[1] = ts[2] - ts[1];  // loaders + solver
+      o[2] = ts[3] - ts[2];  // outputs
+      o[3] = ts[3] - ts[0];
+    }
+  };
   if (!tr) {
     // a matrix solved whole by the shortcut: no augmenting path moved any row or dual since,
     // so u[q] still is C[q][col4row[q]] (exactly: the float minimum widened to double)
@@ -499,6 +538,7 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
       }
   }
   if (threadIdx.x == 0) { A.count[f] = nr; A.status[f] = 0; }
+  prof_end();
 }
 
 constexpr int lsap_ks_next(int k) { return k == 1 ? 4 : 2 * k; }
@@ -618,7 +658,7 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
-    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 8 : nullptr;
+    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 16 : nullptr;
     int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                              : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
@@ -673,7 +713,7 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
-    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 8 : nullptr;
+    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 16 : nullptr;
     int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                              : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
@@ -682,7 +722,8 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
 }
 
 /* diagnostics: per-matrix solver cycle breakdown of later trk_lsap / trk_lsap_dev launches
- * into buf [F][8] u64 (wait, scan, dual, augment, iterations, total, nr, nc); NULL = off */
+ * into buf [F][16] u64 (solver: wait, scan, dual, augment, iterations, total, nr, nc; workgroup:
+ * shortcut pass, loaders + solver, outputs, total, 0...); NULL = off */
 extern "C" int trk_lsap_set_prof(unsigned long long* buf) {
   g_lsap_prof = buf;
   return TRK_OK;

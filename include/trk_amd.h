@@ -171,8 +171,9 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
              int32_t* assign, int64_t nr_max, double cost_max, void* stream);
 
 /* Diagnostics: later trk_lsap / trk_lsap_dev launches write a per-matrix solver
- * cycle breakdown into buf [F][8] u64 (shader clocks: waiting for rows, scans +
- * argmin, dual updates, augmentation; iterations, total, nr, nc).  NULL = off. */
+ * cycle breakdown into buf [F][16] u64 (shader clocks: waiting for rows, scans +
+ * argmin, dual updates, augmentation; iterations, total, nr, nc; then the workgroup's
+ * shortcut pass, loaders + solver, outputs, total).  NULL = off. */
 int trk_lsap_set_prof(unsigned long long* buf);
 /* diagnostics: per-workgroup timestamps of the 256x256 encoder GEMM (enc_gemm=2);
  * buf >= 16 u64 per workgroup, NULL = off */
