@@ -104,44 +104,6 @@ __device__ __forceinline__ void argmin_step(double& v, int& key, int& col) {
   col = take ? oc : col;
 }
 
-// min over the wave of a double (DPP row shifts + row broadcasts; +inf identity),
-// returned wave-uniform
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ double dpp_min_step(double v) {
-  const int olo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWMASK, 0xF, false);
-  const int ohi = __builtin_amdgcn_update_dpp(0x7ff00000, __double2hiint(v), CTRL, ROWMASK, 0xF, false);
-  const double o = __hiloint2double(ohi, olo);
-  return o < v ? o : v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-  v = dpp_min_step<0x111, 0xF>(v);
-  v = dpp_min_step<0x112, 0xF>(v);
-  v = dpp_min_step<0x114, 0xF>(v);
-  v = dpp_min_step<0x118, 0xF>(v);
-  v = dpp_min_step<0x142, 0xA>(v);
-  v = dpp_min_step<0x143, 0xC>(v);
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
-  return __hiloint2double(hi, lo);
-}
-
-// the same for a float (exact: a float minimum widened to double is the double minimum)
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ float dpp_min_step_f(float v) {
-  const float o = __int_as_float(__builtin_amdgcn_update_dpp(0x7f800000, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
-  return o < v ? o : v;
-}
-__device__ __forceinline__ float wave_min_t(float v) {
-  v = dpp_min_step_f<0x111, 0xF>(v);
-  v = dpp_min_step_f<0x112, 0xF>(v);
-  v = dpp_min_step_f<0x114, 0xF>(v);
-  v = dpp_min_step_f<0x118, 0xF>(v);
-  v = dpp_min_step_f<0x142, 0xA>(v);
-  v = dpp_min_step_f<0x143, 0xC>(v);
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ double wave_min_t(double v) { return wave_min(v); }
-
 // lexicographic min over the wave; the result is returned wave-uniform
 // (row_shr 1/2/4/8 inside each row of 16, then row_bcast15 / row_bcast31,
 // total in lane 63).  (value, key) pairs are unique per column, so the order
@@ -217,59 +179,38 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   if (threadIdx.x == 0) ctl[3] = nr;
   __syncthreads();
   {
-    // rows in flight per wave: every row's loads are issued before the first reduction, so a
-    // 256-column frame takes 4 load round trips (8 at 8 rows; the cost matrix was just written
-    // on another XCD, so each round trip is an L2 miss)
-    constexpr int R = KS >= 16 ? 2 : (KS >= 8 ? 4 : 16);
+    // one lane per working row: lane l of wave w scans row 64 w + l (+ 256 per pass) for its
+    // minimum, the minimum's first column and how many entries equal it -- plain compares, no
+    // cross-lane reduction (the wave-per-row version spent ~2,500 instructions per 16 rows on
+    // DPP reductions, ballots and read-lanes: 64K cycles for 256 rows).  The row's entries are
+    // loaded in batches of CH from clamped addresses (unconditional loads, all in flight at
+    // once); a transposed problem's rows are C's columns, so its loads are coalesced
+    constexpr int CH = sizeof(T) == 4 ? 64 : 32;
     int bad = 0;
-    for (int i0 = wave * R; i0 < nr; i0 += 4 * R) {
-      T x[R][KS];
+    for (int i0 = wave * 64; i0 < nr; i0 += 4 * 64) {
+      const int i = i0 + lane, ii = min(i, nr - 1);
+      T m = (T)INFINITY;
+      int col = 0, cnt = 0;
+      for (int j0 = 0; j0 < nc; j0 += CH) {
+        T e[CH];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+        for (int q = 0; q < CH; ++q) e[q] = gload(ii, min(j0 + q, nc - 1));
 #pragma unroll
-        for (int k = 0; k < KS; ++k) {
-          const int c = lane + 64 * k;
-          x[r][k] = (i0 + r < nr && k < ks && c < nc) ? gload(i0 + r, c) : (T)INFINITY;
+        for (int q = 0; q < CH; ++q) {
+          const T x = e[q];
+          const bool in = j0 + q < nc;
+          if (in && (x != x || x == (T)-INFINITY)) bad = 1;
+          const bool lt = in && x < m, eq = in && x == m;
+          col = lt ? j0 + q : col;
+          cnt = lt ? 1 : cnt + (eq ? 1 : 0);
+          m = lt ? x : m;
         }
-      // the R rows' reductions are independent chains (the compiler interleaves them); each
-      // row's result is parked in lane r, and lanes < R publish the R rows at once
-      T m[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        T lm = (T)INFINITY;  // this lane's minimum (invalid slots hold +inf)
-#pragma unroll
-        for (int k = 0; k < KS; ++k) {
-          const T e = x[r][k];
-          if (e != e || e == (T)-INFINITY) bad = 1;
-          lm = e < lm ? e : lm;
-        }
-        m[r] = wave_min_t(lm);
       }
-      double my_m = 0.0;
-      int my_col = -1;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        // entries equal to the minimum: unique iff one lane holds exactly one
-        int cnt = 0, col = 0;
-#pragma unroll
-        for (int k = 0; k < KS; ++k) {
-          const bool eq = x[r][k] == m[r];
-          col = (eq && cnt == 0) ? lane + 64 * k : col;
-          cnt += eq ? 1 : 0;
-        }
-        const uint64_t holders = __ballot(cnt > 0);
-        const int hl = (int)__builtin_ctzll(holders | (1ull << 63));
-        const int hcnt = __builtin_amdgcn_readlane(cnt, hl);
-        const int hcol = __builtin_amdgcn_readlane(col, hl);
-        const bool uniq = m[r] < (T)INFINITY && __popcll(holders) == 1 && hcnt == 1;
-        my_m = lane == r ? (double)m[r] : my_m;
-        my_col = lane == r ? (uniq ? hcol : -1) : my_col;
-      }
-      if (lane < R && i0 + lane < nr) {
-        const int i = i0 + lane;
-        u[i] = my_m;
-        col4row[i] = my_col;
-        if (my_col >= 0) atomicMin(&firstrow[my_col], i);
+      if (i < nr) {
+        const bool uniq = m < (T)INFINITY && cnt == 1;
+        u[i] = (double)m;
+        col4row[i] = uniq ? col : -1;
+        if (uniq) atomicMin(&firstrow[col], i);
         else atomicMin(&ctl[3], i);
       }
     }
