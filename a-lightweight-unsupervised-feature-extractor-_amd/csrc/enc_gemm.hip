@@ -45,6 +45,7 @@ int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X r
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
 int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
+int g_rf_sumlanes = 0;  // trk_set_tuning("rf_sumlanes"): rf2's ROI sums one channel per lane (1) or 16 per lane fr == 0
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
@@ -1193,6 +1194,7 @@ struct RfArgs {
   int pf;               // trk_set_tuning("rf_pf"): L2 prefetch distance in ROIs (X rows of ROI + pf), 0 = none
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
   int lag;              // trk_set_tuning("rf_lag"), rf2_body: half B starts GEMM1 once A is past K step lag
+  int sum_lanes;        // trk_set_tuning("rf_sumlanes"): rf2_body's ROI sums converted one channel per lane
   // fused mode (trk_enc_rmb_fused: SE and the transition inside the kernel)
   const uint4* Wtp;     // [32 k steps][32 col tiles][64 lanes] 16-B fragments of Wt [512][1024]
   const float* bt;      // [512] transition bias
@@ -2233,6 +2235,16 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     rf3_tail<G>(a, roi, smem, acc, lb, prof ? pst[0] : 0ull);
     return;
   }
+  if (a.sum_lanes) {
+    // every lane converts and stores one channel's sum (the butterfly leaves all 16 sums
+    // of a row group in every lane of it): one fixed-point conversion per lane instead of
+    // 16 on the lanes fr == 0; the same bits
+    const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
+    const float x = rf3_colsum(acc, fr);
+    long long* o = a.sums + roi * kPart * 1024 + G * 512 + rf3_lane_ch(wave, fr, fc);
+    o[0] = llrintf(x * kFix);
+    for (int j = 1; j < cnt; ++j) o[j * 1024] = 0;
+  } else
   {
     const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
 #pragma unroll
@@ -2847,6 +2859,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.pf = g_rf_pf;
   a.prof = g_enc_prof;
   a.lag = g_rf_lag;
+  a.sum_lanes = g_rf_sumlanes;
   if (g_rf_v == 2) {
     hipLaunchKernelGGL(rmb_front2_kernel, dim3((unsigned)nwg), dim3(512), RF2_LDS,
                        reinterpret_cast<hipStream_t>(stream), a);
@@ -2893,6 +2906,7 @@ extern "C" int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, cons
   a.R = R;
   a.pf = g_rf_pf;
   a.lag = g_rf_lag;
+  a.sum_lanes = g_rf_sumlanes;
   a.Wtp = (const uint4*)Wtp;
   a.bt = bt;
   a.se_w1 = se_w1; a.se_b1 = se_b1; a.se_w2 = se_w2; a.se_b2 = se_b2;

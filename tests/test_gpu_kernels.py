@@ -774,6 +774,31 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag):
         L.trk_set_tuning(b"rf_lag", 16)
 
 
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_front_sum_lanes_identical(trk, gpu, R):
+    """rf_sumlanes 1 (each lane converts and stores one channel's ROI sum) vs 0 (16 sums per
+    lane fr == 0): the column-sum butterfly leaves the same bits in every lane of a row
+    group, so XRN and the int64 partials must be identical."""
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(300 + R)
+    X = torch.randn(R * 100, 512, generator=g).to(gpu).bfloat16()
+    W1p = ops.enc_pack_fragments((torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16())
+    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
+    W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16())
+    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
+    L = trk.lib()
+    res = {}
+    try:
+        for v in (0, 1):
+            assert L.trk_set_tuning(b"rf_sumlanes", v) == 0
+            XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+            res[v] = (XRN, ops.enc_sums_reduce(s, 100))
+    finally:
+        L.trk_set_tuning(b"rf_sumlanes", 0)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
 def _rmb_front_vs_two_kernel(gpu, R):
     from importlib import import_module
     ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
