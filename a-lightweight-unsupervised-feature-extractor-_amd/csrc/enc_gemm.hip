@@ -51,7 +51,8 @@ int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straig
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
 int g_t4_mode = 5;  // trk_set_tuning("t4_mode"): trans4 pipeline (K steps per LDS stage, B distance):
                     // 0 = (1, 2), 1 = (2, 2), 2 = (1, 3), 3 = (2, 3); 4..6 = (1, 2) + setprio / mid-step issue /
-                    // both; 7 = (2, 3) + both.  Isolated medians (tools/exp/trans_ab.py): 244.1, 240.0 (3),
+                    // both; 7 = (2, 3) + both; 8 / 9 = mid-step issue + counted fragment reads at (1, 2) /
+                    // (2, 3).  Isolated medians (tools/exp/trans_ab.py): 244.1, 240.0 (3),
                     // 248.7 (4), 235.4 (5), 241.3 (6), 245.0 (7) us; pipeline 5 vs 0 in three interleaved pairs
                     // 1.983/1.990/1.952M vs 1.954/1.954/1.942M ROIs/s: 5 (mid-step issue) is the default
 int g_enc_trans_wide = 0;  // trk_set_tuning("enc_trans_wide"): 1 = gemm4's transition on 256 x 256 tiles (8
@@ -2402,7 +2403,8 @@ __device__ __forceinline__ void seq_for(F&& f, std::integer_sequence<int, K...>)
 }
 
 // OPT bit 0: s_setprio(1) over each step's MFMAs; bit 1: the step's B loads and A DMA issued
-// between its MFMAs (after row tiles 1 and 3) instead of after them
+// between its MFMAs (after row tiles 1 and 3) instead of after them; bit 2: the A fragments
+// read by asm with counted waits per row tile
 template <int SPS, int BD, int OPT = 0>
 __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uint4* Wtp, int64_t ntiles) {
   static_assert(t4_vm_ok<SPS, BD>(), "trans4 vmcnt out of the rf_vmwait range");
@@ -2524,11 +2526,40 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
     constexpr int kt = decltype(ktc)::value;
     const uint4* buf = ring + (kt % NSLOT) * T4_BUF;
     bf8v afr[8];
+    if constexpr (OPT & 4) {
+      // the 8 fragment reads issued up front as asm; each row tile's MFMAs wait (counted
+      // lgkmcnt) for their own fragment only, as rf_mfma_step (the compiler's schedule read two,
+      // waited for everything, read six, waited again)
+      const uint32_t ab = lds_addr(buf + lterm);
+      u32x4 aq[8];
+      asm volatile("ds_read_b128 %0, %1" : "=v"(aq[0]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(aq[1]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(aq[2]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(aq[3]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(aq[4]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(aq[5]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(aq[6]) : "v"(ab) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:7168" : "=v"(aq[7]) : "v"(ab) : "memory");
 #pragma unroll
-    for (int i = 0; i < 8; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + lterm + i * 64);
+      for (int i = 0; i < 8; ++i) afr[i] = __builtin_bit_cast(bf8v, aq[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + lterm + i * 64);
+    }
     if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      if constexpr (OPT & 4) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == 0) asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(afr[0]));
+        else if (i == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(afr[1]));
+        else if (i == 2) asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(afr[2]));
+        else if (i == 3) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(afr[3]));
+        else if (i == 4) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(afr[4]));
+        else if (i == 5) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(afr[5]));
+        else if (i == 6) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(afr[6]));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(afr[7]));
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], __builtin_bit_cast(bf8v, bq[kt % (BD + 1)][t]),
@@ -2780,6 +2811,10 @@ extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, i
       hipLaunchKernelGGL((trans4_kernel<1, 2, 3>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
     else if (g_t4_mode == 7)
       hipLaunchKernelGGL((trans4_kernel<2, 3, 3>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 8)
+      hipLaunchKernelGGL((trans4_kernel<1, 2, 6>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    else if (g_t4_mode == 9)
+      hipLaunchKernelGGL((trans4_kernel<2, 3, 6>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
     else
       hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
     return trk::check_launch("trans4_kernel");

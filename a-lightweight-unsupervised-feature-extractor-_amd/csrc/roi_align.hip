@@ -932,7 +932,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "roi_wlds")) { TRK_REQUIRE(value == 0 || value == 1, "roi_wlds in {0, 1}"); g_roi_wlds = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
   if (!strcmp(key, "rf_pf")) { extern int g_rf_pf; TRK_REQUIRE(value >= 0 && value <= 64, "rf_pf in [0, 64]"); g_rf_pf = value; return TRK_OK; }
-  if (!strcmp(key, "t4_mode")) { extern int g_t4_mode; TRK_REQUIRE(value >= 0 && value <= 7, "t4_mode in [0, 7]"); g_t4_mode = value; return TRK_OK; }
+  if (!strcmp(key, "t4_mode")) { extern int g_t4_mode; TRK_REQUIRE(value >= 0 && value <= 9, "t4_mode in [0, 9]"); g_t4_mode = value; return TRK_OK; }
   if (!strcmp(key, "enc_trans")) { extern int g_enc_trans; TRK_REQUIRE(value == 0 || value == 1, "enc_trans in {0, 1}"); g_enc_trans = value; return TRK_OK; }
   if (!strcmp(key, "enc_trans_wide")) { extern int g_enc_trans_wide; TRK_REQUIRE(value == 0 || value == 1, "enc_trans_wide in {0, 1}"); g_enc_trans_wide = value; return TRK_OK; }
   if (!strcmp(key, "rf_sumlanes")) { extern int g_rf_sumlanes; TRK_REQUIRE(value == 0 || value == 1, "rf_sumlanes in {0, 1}"); g_rf_sumlanes = value; return TRK_OK; }

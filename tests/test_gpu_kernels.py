@@ -722,7 +722,7 @@ def test_enc_transition_wide_tile_vs_default(trk, gpu, P, R):
     assert torch.equal(got, ref) and torch.equal(got2, ref)  # (no fragments given: gemm4 either way)
 
 
-@pytest.mark.parametrize("t4_mode", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("t4_mode", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (49, 29)])
 def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R, t4_mode):
     """trans4 (enc_trans 1: the weights straight into VGPRs from the packed fragments,

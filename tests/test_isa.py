@@ -58,4 +58,4 @@ def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
         found += 1
         bad = IC.scan(body)
         assert not bad, (name, bad[:5])
-    assert found == 3 + 8  # rmb_front, rmb_front2, rmb_fused + the 8 trans4 variants
+    assert found == 3 + 10  # rmb_front, rmb_front2, rmb_fused + the 10 trans4 variants

@@ -16,8 +16,7 @@ bt = torch.randn(512, device=dev, generator=g) / 4
 Wtp = ops.enc_pack_fragments_k(Wt)
 L = ops.lib()
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-VARS = {"gemm4": (0, 0, 0), "trans4_1x2": (0, 1, 0), "trans4_2x3": (0, 1, 3), "t4_prio": (0, 1, 4),
-        "t4_mid": (0, 1, 5), "t4_prio_mid": (0, 1, 6), "t4_2x3_prio_mid": (0, 1, 7)}
+VARS = {"gemm4": (0, 0, 0), "t4_mid": (0, 1, 5), "t4_mid_asm": (0, 1, 8), "t4_2x3_mid_asm": (0, 1, 9)}
 res = {k: [] for k in VARS}
 outs = {}
 
