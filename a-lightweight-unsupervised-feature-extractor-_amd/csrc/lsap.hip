@@ -104,6 +104,39 @@ __device__ __forceinline__ void argmin_step(double& v, int& key, int& col) {
   col = take ? oc : col;
 }
 
+// all-reduce over a DPP row of 16 lanes (row_ror 1, 2, 4, 8: every lane ends with the result)
+template <int CTRL>
+__device__ __forceinline__ int ror16(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ float row16_min(float v) {
+  v = fminf(v, __int_as_float(ror16<0x121>(__float_as_int(v))));
+  v = fminf(v, __int_as_float(ror16<0x122>(__float_as_int(v))));
+  v = fminf(v, __int_as_float(ror16<0x124>(__float_as_int(v))));
+  return fminf(v, __int_as_float(ror16<0x128>(__float_as_int(v))));
+}
+__device__ __forceinline__ double row16_min(double v) {
+  auto step = [](double x, auto ctrl) {
+    constexpr int C = decltype(ctrl)::value;
+    const double o = __hiloint2double(ror16<C>(__double2hiint(x)), ror16<C>(__double2loint(x)));
+    return o < x ? o : x;
+  };
+  v = step(v, std::integral_constant<int, 0x121>{});
+  v = step(v, std::integral_constant<int, 0x122>{});
+  v = step(v, std::integral_constant<int, 0x124>{});
+  return step(v, std::integral_constant<int, 0x128>{});
+}
+__device__ __forceinline__ int row16_sum(int v) {
+  v += ror16<0x121>(v);
+  v += ror16<0x122>(v);
+  v += ror16<0x124>(v);
+  return v + ror16<0x128>(v);
+}
+__device__ __forceinline__ int row16_mini(int v) {
+  v = min(v, ror16<0x121>(v));
+  v = min(v, ror16<0x122>(v));
+  v = min(v, ror16<0x124>(v));
+  return min(v, ror16<0x128>(v));
+}
+
 // lexicographic min over the wave; the result is returned wave-uniform
 // (row_shr 1/2/4/8 inside each row of 16, then row_bcast15 / row_bcast31,
 // total in lane 63).  (value, key) pairs are unique per column, so the order
@@ -179,39 +212,104 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   if (threadIdx.x == 0) ctl[3] = nr;
   __syncthreads();
   {
-    // one lane per working row: lane l of wave w scans row 64 w + l (+ 256 per pass) for its
-    // minimum, the minimum's first column and how many entries equal it -- plain compares, no
-    // cross-lane reduction (the wave-per-row version spent ~2,500 instructions per 16 rows on
-    // DPP reductions, ballots and read-lanes: 64K cycles for 256 rows).  The row's entries are
-    // loaded in batches of CH from clamped addresses (unconditional loads, all in flight at
-    // once); a transposed problem's rows are C's columns, so its loads are coalesced
-    constexpr int CH = sizeof(T) == 4 ? 64 : 32;
+    // Each working row's minimum, the first column holding it and how many entries equal it.
+    // A row of C (the untransposed case) is read by a 16-lane group, 4 consecutive columns
+    // per lane per 64-column chunk, so a load instruction covers 4 rows x 256 contiguous
+    // bytes; the group reduces with DPP row rotations (min, count, first column).  One lane
+    // per row would read 64 rows per instruction (64 L2 line requests: 72K cycles for a
+    // 256 x 256 frame); one wave per row spent ~150 instructions per row on wave-wide
+    // reductions (64K).  A transposed problem's working rows are C's columns, so there one
+    // lane per row reads contiguous memory.
     int bad = 0;
-    for (int i0 = wave * 64; i0 < nr; i0 += 4 * 64) {
-      const int i = i0 + lane, ii = min(i, nr - 1);
-      T m = (T)INFINITY;
-      int col = 0, cnt = 0;
-      for (int j0 = 0; j0 < nc; j0 += CH) {
-        T e[CH];
+    auto publish = [&](int i, T m, int col, int cnt) {
+      const bool uniq = m < (T)INFINITY && cnt == 1;
+      u[i] = (double)m;
+      col4row[i] = uniq ? col : -1;
+      if (uniq) atomicMin(&firstrow[col], i);
+      else atomicMin(&ctl[3], i);
+    };
+    if (tr) {
+      constexpr int CH = sizeof(T) == 4 ? 64 : 32;
+      for (int i0 = wave * 64; i0 < nr; i0 += 4 * 64) {
+        const int i = i0 + lane, ii = min(i, nr - 1);
+        T m = (T)INFINITY;
+        int col = 0, cnt = 0;
+        for (int j0 = 0; j0 < nc; j0 += CH) {
+          T e[CH];
 #pragma unroll
-        for (int q = 0; q < CH; ++q) e[q] = gload(ii, min(j0 + q, nc - 1));
+          for (int q = 0; q < CH; ++q) e[q] = gload(ii, min(j0 + q, nc - 1));
 #pragma unroll
-        for (int q = 0; q < CH; ++q) {
-          const T x = e[q];
-          const bool in = j0 + q < nc;
-          if (in && (x != x || x == (T)-INFINITY)) bad = 1;
-          const bool lt = in && x < m, eq = in && x == m;
-          col = lt ? j0 + q : col;
-          cnt = lt ? 1 : cnt + (eq ? 1 : 0);
-          m = lt ? x : m;
+          for (int q = 0; q < CH; ++q) {
+            const T x = e[q];
+            const bool in = j0 + q < nc;
+            if (in && (x != x || x == (T)-INFINITY)) bad = 1;
+            const bool lt = in && x < m, eq = in && x == m;
+            col = lt ? j0 + q : col;
+            cnt = lt ? 1 : cnt + (eq ? 1 : 0);
+            m = lt ? x : m;
+          }
         }
+        if (i < nr) publish(i, m, col, cnt);
       }
-      if (i < nr) {
-        const bool uniq = m < (T)INFINITY && cnt == 1;
-        u[i] = (double)m;
-        col4row[i] = uniq ? col : -1;
-        if (uniq) atomicMin(&firstrow[col], i);
-        else atomicMin(&ctl[3], i);
+    } else {
+      constexpr int VEC = 4, CW = 64;                       // columns per lane / per chunk
+      constexpr int CG = KS < 4 ? KS : 4;                   // chunks loaded per round
+      constexpr int RR = KS <= 4 ? 4 : (KS == 8 ? 2 : 1);   // rows per lane group
+      const int grp = lane >> 4, p = lane & 15;
+      for (int i0 = wave * 4 * RR; i0 < nr; i0 += 16 * RR) {
+        T m[RR];
+        int col[RR], cnt[RR];
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+          m[r] = (T)INFINITY;
+          col[r] = 0;
+          cnt[r] = 0;
+        }
+        for (int c0 = 0; c0 < ks; c0 += CG) {
+          T e[CG][RR][VEC];
+#pragma unroll
+          for (int c = 0; c < CG; ++c)
+#pragma unroll
+            for (int r = 0; r < RR; ++r)
+#pragma unroll
+              for (int v = 0; v < VEC; ++v)
+                e[c][r][v] = gload(min(i0 + grp + 4 * r, nr - 1), min((c0 + c) * CW + p * VEC + v, nc - 1));
+#pragma unroll
+          for (int c = 0; c < CG; ++c)
+#pragma unroll
+            for (int r = 0; r < RR; ++r) {
+              T lm = (T)INFINITY;
+#pragma unroll
+              for (int v = 0; v < VEC; ++v) {
+                const int cc = (c0 + c) * CW + p * VEC + v;
+                T x = e[c][r][v];
+                if (cc < nc && (x != x || x == (T)-INFINITY)) bad = 1;
+                x = cc < nc ? x : (T)INFINITY;
+                e[c][r][v] = x;
+                lm = x < lm ? x : lm;
+              }
+              const T cm = row16_min(lm);
+              int lc = 0, lf = 0x7fffffff;
+#pragma unroll
+              for (int v = 0; v < VEC; ++v) {
+                const bool eq = e[c][r][v] == cm;
+                lc += eq ? 1 : 0;
+                lf = (eq && lf == 0x7fffffff) ? (c0 + c) * CW + p * VEC + v : lf;
+              }
+              const int ccnt = row16_sum(lc), cfirst = row16_mini(lf);
+              const bool lt = cm < m[r], eq = cm == m[r];
+              col[r] = lt ? cfirst : col[r];
+              cnt[r] = lt ? ccnt : cnt[r] + (eq ? ccnt : 0);
+              m[r] = lt ? cm : m[r];
+            }
+        }
+        if (p == 0) {
+#pragma unroll
+          for (int r = 0; r < RR; ++r) {
+            const int i = i0 + grp + 4 * r;
+            if (i < nr) publish(i, m[r], col[r], cnt[r]);
+          }
+        }
       }
     }
     if (__any(bad) && lane == 0) ctl[1] = 1;

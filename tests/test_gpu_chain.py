@@ -4,7 +4,7 @@
   of 10x10 = 2,048 ROIs = 204,800 encoder GEMM rows, through the bf16 fused
   encoder (default g1dw / gemm4 paths, full XCD-remapped grids) against the
   fp32 encoder path, which tests/test_gpu_kernels.py pins to the reference's
-  golden (<= 1e-4).  Tolerances: per-row cosine >= 0.999; LSAP assignments
+  golden (<= 1e-4).  Tolerances: about 2x the measured bf16 error (|d| <= 2e-3, cosine >= 1 - 1e-5); LSAP assignments
   from build_cost identical (and equal to the synthetic identity) on
   margin-separated tracks.
 * c2 chain (configs[1]): [1,512,40,40], N = M = 64, fp32:
@@ -75,7 +75,10 @@ def test_c3_bf16_encoder_full_size_vs_fp32(trk, gpu):
     assert torch.isfinite(zb).all()
     cos = (zb * z32).sum(1)
     print(f"\nc3 bf16 vs fp32 encoder: max |d| {(zb - z32).abs().max().item():.3e}, min cosine {cos.min().item():.7f}")
-    assert cos.min().item() >= 0.999, cos.min().item()
+    # measured on MI355X (r04, gpurun_out/r4k_chain.log): max |d| 9.57e-4, min cosine 1 - 4.7e-6;
+    # the bounds are about 2x that
+    assert (zb - z32).abs().max().item() <= 2e-3
+    assert cos.min().item() >= 1.0 - 1e-5, cos.min().item()
     # deterministic at full size (fixed-point ROI sums, no atomics on values)
     with torch.no_grad():
         zb2 = model(roib)
@@ -178,8 +181,8 @@ def test_reference_half_configuration(trk, gpu):
     tracking.py:209-221 rois built in feat.dtype, so fp16 boxes; :313 normalize(z.float())):
     an fp16 map through roi_align_from_input_boxes and the .half() model does not raise,
     and at the c3 size (8 maps x 256 ROIs) its embeddings agree with the fp32 path on the
-    same fp16 inputs (per-row cosine >= 0.999); on the golden inputs it matches the
-    reference's fp32 embeddings (cosine >= 0.999)."""
+    same fp16 inputs (per-row cosine >= 1 - 1e-6, 2x measured); on the golden inputs it matches
+    the reference's fp32 embeddings (cosine >= 1 - 5e-7)."""
     import os
     from conftest import GOLDEN
     rng = np.random.default_rng(16)
@@ -200,11 +203,15 @@ def test_reference_half_configuration(trk, gpu):
     cos = (z16 * z32).sum(1)
     print(f"\nfp16 model vs fp32 on fp16 inputs: max |d| {(z16 - z32).abs().max().item():.3e}, "
           f"min cosine {float(cos.min()):.7f}")
-    assert float(cos.min()) >= 0.999, float(cos.min())
+    # measured (r04): max |d| 2.39e-4, min cosine 1 - 4e-7 (fp16 inputs); bounds about 2x
+    assert (z16 - z32).abs().max().item() <= 5e-4
+    assert float(cos.min()) >= 1.0 - 1e-6, float(cos.min())
     d = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
     x = torch.from_numpy(G.encoder_input(int(d["seed_s10"]), 16, 10)).to(gpu)
     with torch.no_grad():
         z = torch.nn.functional.normalize(m16(x.half()).float(), dim=1).cpu().numpy()
     print(f"fp16 model vs golden: max |d| {np.abs(z - d['z_s10']).max():.3e}, "
           f"min cosine {float((z * d['z_s10']).sum(1).min()):.7f}")
-    assert float((z * d["z_s10"]).sum(1).min()) >= 0.999
+    # measured (r04): max |d| 1.38e-4, min cosine 1 - 2e-7 vs the reference-run golden
+    assert float(np.abs(z - d["z_s10"]).max()) <= 3e-4
+    assert float((z * d["z_s10"]).sum(1).min()) >= 1.0 - 5e-7

@@ -5,7 +5,7 @@ the reference's golden vectors.  Tolerances are written in each test:
     of test_roi_align_sweep_variants
   cost: |d| <= 2e-6 (f32 dot-order / logf ulp differences), gate decisions equal
   lsap: indices bit-exact (scipy semantics)
-  encoder fp32: <= 1e-4 (north star);  bf16: cosine >= 0.999 vs fp32
+  encoder fp32: <= 1e-4 (north star);  bf16: |d| <= 1.2e-3, cosine >= 1 - 5e-6 vs fp32 (2x measured)
 """
 import os
 
@@ -595,7 +595,10 @@ def test_encoder_gpu_vs_reference_golden(trk, gpu, s):
     assert np.max(np.abs(z - exp)) <= 1e-4
     print(f"\nbf16 encoder vs golden s={s}: max |d| {np.max(np.abs(zb - exp)):.3e}, "
           f"min cosine {(zb * exp).sum(1).min():.7f}")
-    assert (zb * exp).sum(1).min() >= 0.999
+    # measured on MI355X (r04, gpurun_out/r4k_chain.log): s=7 max |d| 5.51e-4, min cosine
+    # 1 - 2.2e-6; s=10 4.94e-4, 1 - 1.8e-6.  Bounds: about 2x
+    assert np.max(np.abs(zb - exp)) <= 1.2e-3
+    assert (zb * exp).sum(1).min() >= 1.0 - 5e-6
     # bf16: fused trk GEMMs vs the hipBLASLt + separate-pass graph (same bf16 rounding points
     # except the means, which the fused epilogues take in f32 before rounding)
     try:
