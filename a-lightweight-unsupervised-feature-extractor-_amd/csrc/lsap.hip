@@ -188,7 +188,7 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   T* ring = reinterpret_cast<T*>(smem + ring_off);
 
   // diagnostics: workgroup phase stamps [entry, shortcut pass done, solver done, end]
-  unsigned long long ts[4] = {0, 0, 0, 0};
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (A.prof) ts[0] = stamp();
   for (int q = threadIdx.x; q < RB; q += blockDim.x) ready[q] = 0;
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
@@ -211,6 +211,7 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
   for (int j = threadIdx.x; j < nc; j += blockDim.x) firstrow[j] = 0x7fffffff;
   if (threadIdx.x == 0) ctl[3] = nr;
   __syncthreads();
+  if (A.prof) ts[7] = stamp();
   {
     // Each working row's minimum, the first column holding it and how many entries equal it.
     // A row of C (the untransposed case) is read by a 16-lane group, 4 consecutive columns
@@ -242,8 +243,8 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
           for (int q = 0; q < CH; ++q) {
             const T x = e[q];
             const bool in = j0 + q < nc;
-            if (in && (x != x || x == (T)-INFINITY)) bad = 1;
-            const bool lt = in && x < m, eq = in && x == m;
+            bad |= (int)(in & ((x != x) | (x == (T)-INFINITY)));
+            const bool lt = in & (x < m), eq = in & (x == m);
             col = lt ? j0 + q : col;
             cnt = lt ? 1 : cnt + (eq ? 1 : 0);
             m = lt ? x : m;
@@ -257,12 +258,15 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
       constexpr int RR = KS <= 4 ? 4 : (KS == 8 ? 2 : 1);   // rows per lane group
       const int grp = lane >> 4, p = lane & 15;
       for (int i0 = wave * 4 * RR; i0 < nr; i0 += 16 * RR) {
+        // lane-local (minimum, count, first column) over the lane's entries of each row, then
+        // one 16-lane reduction per row (the group's minimum; count and first column of the
+        // lanes holding it)
         T m[RR];
         int col[RR], cnt[RR];
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
           m[r] = (T)INFINITY;
-          col[r] = 0;
+          col[r] = 0x7fffffff;
           cnt[r] = 0;
         }
         for (int c0 = 0; c0 < ks; c0 += CG) {
@@ -277,31 +281,26 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
 #pragma unroll
           for (int c = 0; c < CG; ++c)
 #pragma unroll
-            for (int r = 0; r < RR; ++r) {
-              T lm = (T)INFINITY;
+            for (int r = 0; r < RR; ++r)
 #pragma unroll
               for (int v = 0; v < VEC; ++v) {
                 const int cc = (c0 + c) * CW + p * VEC + v;
-                T x = e[c][r][v];
-                if (cc < nc && (x != x || x == (T)-INFINITY)) bad = 1;
-                x = cc < nc ? x : (T)INFINITY;
-                e[c][r][v] = x;
-                lm = x < lm ? x : lm;
+                const T x = e[c][r][v];
+                const bool in = cc < nc;
+                bad |= (int)(in & ((x != x) | (x == (T)-INFINITY)));
+                const bool lt = in & (x < m[r]), eq = in & (x == m[r]);
+                col[r] = lt ? cc : col[r];             // columns rise along (c, v): the first stays
+                cnt[r] = lt ? 1 : cnt[r] + (int)eq;
+                m[r] = lt ? x : m[r];
               }
-              const T cm = row16_min(lm);
-              int lc = 0, lf = 0x7fffffff;
+        }
 #pragma unroll
-              for (int v = 0; v < VEC; ++v) {
-                const bool eq = e[c][r][v] == cm;
-                lc += eq ? 1 : 0;
-                lf = (eq && lf == 0x7fffffff) ? (c0 + c) * CW + p * VEC + v : lf;
-              }
-              const int ccnt = row16_sum(lc), cfirst = row16_mini(lf);
-              const bool lt = cm < m[r], eq = cm == m[r];
-              col[r] = lt ? cfirst : col[r];
-              cnt[r] = lt ? ccnt : cnt[r] + (eq ? ccnt : 0);
-              m[r] = lt ? cm : m[r];
-            }
+        for (int r = 0; r < RR; ++r) {
+          const T gm = row16_min(m[r]);
+          const bool mine = m[r] == gm;
+          cnt[r] = row16_sum(mine ? cnt[r] : 0);
+          col[r] = row16_mini(mine ? col[r] : 0x7fffffff);
+          m[r] = gm;
         }
         if (p == 0) {
 #pragma unroll
@@ -314,12 +313,15 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
     }
     if (__any(bad) && lane == 0) ctl[1] = 1;
   }
+  if (A.prof) ts[4] = stamp();
   __syncthreads();
+  if (A.prof) ts[5] = stamp();
   for (int i = threadIdx.x; i < nr; i += blockDim.x) {
     const int c = col4row[i];
     if (c >= 0 && firstrow[c] != i) atomicMin(&ctl[3], i);  // an earlier row's minimum took c
   }
   __syncthreads();
+  if (A.prof) ts[6] = stamp();
   const int kpre = ctl[1] ? nr : ctl[3];  // invalid entries: the result is the error, solve nothing
   for (int i = threadIdx.x; i < nr; i += blockDim.x) {
     if (i < kpre) {
@@ -537,6 +539,10 @@ __device__ __forceinline__ void lsap_body(const LsapArgs& A, unsigned char* smem
       o[1] = ts[2] - ts[1];  // loaders + solver
       o[2] = ts[3] - ts[2];  // outputs
       o[3] = ts[3] - ts[0];
+      o[4] = ts[7] - ts[0];  // set-up (ring words, firstrow)
+      o[5] = ts[4] - ts[7];  // the row scans
+      o[6] = ts[5] - ts[4];  // their barrier
+      o[7] = ts[1] - ts[5];  // claim check, duals, hand-over
     }
   };
   if (!tr) {

@@ -39,7 +39,9 @@ def breakdown(C, nr, nc):
     tot = max(p[:, 5].mean(), 1.0)
     nrow = max(float(np.asarray(nr).mean()), 1.0)
     return {"wg_cycles": {"shortcut": round(p[:, 8].mean()), "solver": round(p[:, 9].mean()),
-                          "outputs": round(p[:, 10].mean()), "total": round(p[:, 11].mean())},
+                          "outputs": round(p[:, 10].mean()), "total": round(p[:, 11].mean()),
+                          "setup": round(p[:, 12].mean()), "scans": round(p[:, 13].mean()),
+                          "scan_barrier": round(p[:, 14].mean()), "claims_duals": round(p[:, 15].mean())},
             "wait%": round(100 * p[:, 0].mean() / tot, 1), "scan%": round(100 * p[:, 1].mean() / tot, 1),
             "dual%": round(100 * p[:, 2].mean() / tot, 1), "aug%": round(100 * p[:, 3].mean() / tot, 1),
             "iters/row": round(p[:, 4].sum() / max(p[:, 6].sum(), 1.0), 3),
