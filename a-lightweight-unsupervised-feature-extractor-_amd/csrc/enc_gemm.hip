@@ -45,7 +45,9 @@ int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X r
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
 int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
-int g_rf_sumlanes = 0;  // trk_set_tuning("rf_sumlanes"): rf2's ROI sums one channel per lane (1) or 16 per lane fr == 0
+int g_rf_sumlanes = 1;  // trk_set_tuning("rf_sumlanes"): rf2's ROI sums one channel per lane (1, default: the
+                        // activation + sums phase 10.6K vs 12.1K cycles per wave, 569 vs 582 us isolated, pipeline
+                        // 1.998/1.993/1.996M vs 1.964/2.001/2.017M -- rule (b)) or 16 per lane fr == 0 (0)
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)

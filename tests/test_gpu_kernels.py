@@ -798,7 +798,7 @@ def test_enc_rmb_front_sum_lanes_identical(trk, gpu, R):
             XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
             res[v] = (XRN, ops.enc_sums_reduce(s, 100))
     finally:
-        L.trk_set_tuning(b"rf_sumlanes", 0)
+        L.trk_set_tuning(b"rf_sumlanes", 1)  # the default
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
