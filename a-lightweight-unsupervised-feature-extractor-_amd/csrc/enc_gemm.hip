@@ -45,6 +45,7 @@ int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X r
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
 int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
+int g_rf_dwprio = 0;  // trk_set_tuning("rf_dwprio"): rf2's depthwise at priority 2: 0 none, 1 half B, 2 both
 int g_rf_sumlanes = 1;  // trk_set_tuning("rf_sumlanes"): rf2's ROI sums one channel per lane (1, default: the
                         // activation + sums phase 10.6K vs 12.1K cycles per wave, 569 vs 582 us isolated, pipeline
                         // 1.998/1.993/1.996M vs 1.964/2.001/2.017M -- rule (b)) or 16 per lane fr == 0 (0)
@@ -1198,6 +1199,7 @@ struct RfArgs {
   unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
   int lag;              // trk_set_tuning("rf_lag"), rf2_body: half B starts GEMM1 once A is past K step lag
   int sum_lanes;        // trk_set_tuning("rf_sumlanes"): rf2_body's ROI sums converted one channel per lane
+  int dwprio;           // trk_set_tuning("rf_dwprio"): rf2_body's depthwise at s_setprio 2 (1: half B, 2: both)
   // fused mode (trk_enc_rmb_fused: SE and the transition inside the kernel)
   const uint4* Wtp;     // [32 k steps][32 col tiles][64 lanes] 16-B fragments of Wt [512][1024]
   const float* bt;      // [512] transition bias
@@ -2157,6 +2159,11 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   // same 128 channels, so the read-before-overwrite hand-off is between those two only
   const int NPF = (G == 0 && a.pf) ? 2 : 0;
   uint32_t pf0 = 0, pf1 = 0;
+  // the depthwise of half B is on the workgroup's critical path (half A's GEMM2 waits for it at
+  // K step 8) and shares each SIMD with half A's GEMM2: rf_dwprio 1 issues it at priority 2
+  // over those MFMAs (2: both halves' depthwise)
+  const bool dwp = a.dwprio == 2 || (a.dwprio == 1 && half == 1);
+  if (dwp) __builtin_amdgcn_s_setprio(2);
   {
     const int kb0 = rf2_yblk(cg * 4 + (lane >> 4)), c0 = (lane & 15) >> 2, d0 = lane & 3;
     const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
@@ -2189,6 +2196,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
       rf_dw5q_store<1, 1>(Y, yb, o1);
     }
   }
+  if (dwp) __builtin_amdgcn_s_setprio(0);
   rf2_signal(ctr + RF2_CY2 + half, lane);
   if (prof) pst[3] = eg_stamp();
 
@@ -2897,6 +2905,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.prof = g_enc_prof;
   a.lag = g_rf_lag;
   a.sum_lanes = g_rf_sumlanes;
+  a.dwprio = g_rf_dwprio;
   if (g_rf_v == 2) {
     hipLaunchKernelGGL(rmb_front2_kernel, dim3((unsigned)nwg), dim3(512), RF2_LDS,
                        reinterpret_cast<hipStream_t>(stream), a);
@@ -2944,6 +2953,7 @@ extern "C" int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, cons
   a.pf = g_rf_pf;
   a.lag = g_rf_lag;
   a.sum_lanes = g_rf_sumlanes;
+  a.dwprio = g_rf_dwprio;
   a.Wtp = (const uint4*)Wtp;
   a.bt = bt;
   a.se_w1 = se_w1; a.se_b1 = se_b1; a.se_w2 = se_w2; a.se_b2 = se_b2;

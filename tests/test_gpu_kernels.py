@@ -797,9 +797,15 @@ def test_enc_rmb_front_sum_lanes_identical(trk, gpu, R):
             assert L.trk_set_tuning(b"rf_sumlanes", v) == 0
             XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
             res[v] = (XRN, ops.enc_sums_reduce(s, 100))
+        for v in (1, 2):  # issue priority of the depthwise: scheduling only, the same bits
+            assert L.trk_set_tuning(b"rf_dwprio", v) == 0
+            XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+            res[10 + v] = (XRN, ops.enc_sums_reduce(s, 100))
     finally:
-        L.trk_set_tuning(b"rf_sumlanes", 1)  # the default
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+        L.trk_set_tuning(b"rf_sumlanes", 1)  # the defaults
+        L.trk_set_tuning(b"rf_dwprio", 0)
+    for k in (0, 11, 12):
+        assert torch.equal(res[k][0], res[1][0]) and torch.equal(res[k][1], res[1][1]), k
 
 
 def _rmb_front_vs_two_kernel(gpu, R):
