@@ -109,6 +109,20 @@ class DeferredHead:
             return self._fn()
 
 
+class DeferredTail:
+    """The fused path after the front kernel, not yet enqueued on the producing stream:
+    the SE already runs on `Model.se_stream` (behind the front); `finish()` enqueues the
+    transition GEMM on the current stream (after the SE's event) and returns what the
+    forward would have (a DeferredHead, or the embeddings).  A caller that runs the next
+    frame's front before `finish()` takes the SE off the embedding stream's critical path."""
+
+    def __init__(self, fn):
+        self._fn = fn
+
+    def finish(self):
+        return self._fn()
+
+
 class Model(nn.Module):
     """encoderAndHead.Model(in_channels, out_channels, warmup_epochs, proj_dim)."""
 
@@ -226,6 +240,8 @@ class Model(nn.Module):
     fused_full = False   # with fused_front and fused_tail: the SE and the transition GEMM inside the
                          # front kernel too (enc_rmb_fused; the [M, 1024] XRN never reaches HBM)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
+    defer_tail = False   # fused front + tail: return a DeferredTail after the front; the SE runs on
+    se_stream = None     # se_stream behind the front, the transition only when the caller finishes it
     stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
                          # enqueued (a caller can record an event there to place other streams' work)
 
@@ -276,6 +292,28 @@ class Model(nn.Module):
                 XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
                 if self.stage_hook is not None:
                     self.stage_hook("dsc")
+            if self.fused_tail and front and self.defer_tail and self.se_stream is not None:
+                e_front = torch.cuda.Event()
+                e_front.record()
+                se_st = self.se_stream
+                with torch.cuda.stream(se_st):
+                    se_st.wait_event(e_front)
+                    sums.record_stream(se_st)
+                    m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+                    e_se = torch.cuda.Event()
+                    e_se.record(se_st)
+                defer_head = self.defer_head
+
+                def finish():
+                    st = torch.cuda.current_stream()
+                    st.wait_event(e_se)
+                    for t in (m_r, m_n, s):
+                        t.record_stream(st)
+                    tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True, Wtp=W.get("wt_pk"))
+                    head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
+                                            self.head.net[1].eps, W["h4"], W["h4b"])
+                    return DeferredHead(head, (tsums, s, m_r, m_n)) if defer_head else head()
+                return DeferredTail(finish)
             if self.fused_tail:
                 # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
                 m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])

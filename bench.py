@@ -211,6 +211,12 @@ class Pipeline:
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
                            if os.environ.get("TRK_ROI_STREAM", "1") == "1" else None)
         self.roi_pending = {}
+        # TRK_SE_DEFER=1: the encoder stops after the front kernel; the SE runs on a stream of its
+        # own behind it and frame f's transition is enqueued after frame f+1's front, so the SE
+        # is off the embedding stream (which then runs front(f+1), transition(f), front(f+2), ...)
+        self.defer_tail = (os.environ.get("TRK_SE_DEFER", "0") == "1" and self.defer_head and n_side == 1)
+        self.se_stream = torch.cuda.Stream(device=sc["feat"].device) if self.defer_tail else None
+        self.tails = {}  # frame -> DeferredTail (front enqueued, transition not yet)
         # TRK_ROI_AFTER=g1|dsc: frame f+1's ROI Align waits for frame f's first GEMM / DSC GEMM
         # (an event recorded through encoder.Model.stage_hook), so it runs beside the
         # encoder's later kernels instead of as soon as it is enqueued
@@ -284,8 +290,9 @@ class Pipeline:
             return self.model(roi).view(self.sc["streams"], self.sc["N"], 128)
 
     def embed_async(self, f):
-        """enqueue frame f's roi_align + encoder on the side stream"""
-        if f in self.pending or f >= len(self.sc["rois"]):
+        """enqueue frame f's roi_align + encoder on the side stream (deferred tail: frame f's
+        front, then frame f-1's transition)"""
+        if f in self.pending or f in self.tails or f >= len(self.sc["rois"]):
             return
         main = torch.cuda.current_stream()
         side = self.sides[f % len(self.sides)]
@@ -302,6 +309,7 @@ class Pipeline:
             else:
                 roi = self._roi_for(f, side)
                 self.model.defer_head = self.defer_head
+                self.model.defer_tail, self.model.se_stream = self.defer_tail, self.se_stream
                 try:
                     if self.defer_head:
                         with torch.no_grad():
@@ -310,7 +318,13 @@ class Pipeline:
                         emb = self.stage_embed(roi)
                 finally:
                     self.model.defer_head = False
+                    self.model.defer_tail, self.model.se_stream = False, None
                 self._roi_ahead(f + 1)
+                if hasattr(emb, "finish"):  # deferred tail: the previous frame's transition now
+                    self.tails[f] = emb
+                    if f - 1 in self.tails:
+                        self._finish_tail(f - 1)
+                    return
                 if hasattr(emb, "launch"):  # deferred head: launched by _step on the tracker's stream
                     self.pending[f] = (emb, None)
                     return
@@ -319,6 +333,12 @@ class Pipeline:
             ev.record(side)
         emb.record_stream(main)
         self.pending[f] = (emb, ev)
+
+    def _finish_tail(self, f):
+        """enqueue frame f's transition (and leave its head deferred) on its embedding stream"""
+        side = self.sides[f % len(self.sides)]
+        with torch.cuda.stream(side), torch.no_grad():
+            self.pending[f] = (self.tails.pop(f).finish(), None)
 
     def _roi_ahead(self, f):
         """ROI Align of frame f on its own stream, now: it runs beside the encoder
@@ -353,6 +373,10 @@ class Pipeline:
     def _step(self, f):
         sc = self.sc
         self.embed_async(f)
+        if self.defer_tail:
+            self.embed_async(f + 1)  # frame f+1's front, then frame f's transition
+            if f in self.tails:  # no frame after f: its transition now
+                self._finish_tail(f)
         emb, ev = self.pending.pop(f)
         if ev is None:  # deferred head: launched here, on the tracker's stream, before the step
             with torch.no_grad():
@@ -751,7 +775,8 @@ def main():
     live = probe.means_us()
     live = {k: v for k, v in live.items() if not k.endswith("_live")}
     tracker_live = {"lsap": probe.stage_means_us("lsap_live"), "cost": probe.stage_means_us("cost_live")}
-    side_gap = probe.embed_gaps_us(len(pipe.sides), pipe.defer_head, pipe.roi_stream is not None)
+    side_gap = (None if pipe.defer_tail else  # frames interleave on the embedding stream on purpose
+                probe.embed_gaps_us(len(pipe.sides), pipe.defer_head, pipe.roi_stream is not None))
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
@@ -870,6 +895,7 @@ def main():
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
     rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
+                     "se_deferred": pipe.defer_tail,
                      "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
                      "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,
