@@ -1593,7 +1593,7 @@ __device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned ch
 constexpr int RF2_NB = 24;
 constexpr size_t RF2_CTR = (size_t)(RF2_NB - 1) * RF_KBS * 4 + 112 * 64;  // past block 23's row-111 reads
 enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16,
-       RF3_CPUB = 18, RF3_CYF = 19, RF3_CH = 20, RF3_CS = 21, RF3_CYS = 22, RF2_NCTR = 32 };
+       RF3_CPUB = 18, RF3_CYF = 19, RF3_CH = 20, RF3_CS = 21, RF3_CYS = 22, RF2_CSD = 24, RF2_NCTR = 32 };
 constexpr size_t RF2_LDS = RF2_CTR + RF2_NCTR * 4;
 // fused mode: the SE vectors after the counters (m_r, relu(W1 m_r + b1), s)
 constexpr size_t RF3_M = RF2_LDS, RF3_H = RF3_M + 512 * 4, RF3_S = RF3_H + 128 * 4;
@@ -2026,23 +2026,35 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
   }
 }
 
+// MODE 0: one ROI (lb >> 1) per workgroup; 1: rmb_fused (one ROI + the fused tail); 2: persistent
+// (rmb_front3): the workgroup runs ROIs roi0, roi0 + stride, ... of its group G, the LDS counters
+// count on across ROIs (targets 4 (it + 1)), and ROI it + 1's X DMA and GEMM1 start as soon as
+// the blocks they need are free -- half A's GEMM1 of the next ROI runs under half B's epilogue
+// of this one instead of behind a workgroup boundary
 template <int G, int MODE>
-__device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned char* smem) {
-  const int64_t roi = lb >> 1;
-  unsigned long long pst[8];
-  const bool prof = a.prof != nullptr;
-  if (prof) pst[0] = eg_stamp();
+__device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned char* smem, int64_t roi0 = -1,
+                                         int64_t stride = 0) {
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = wave >> 2, hw = wave & 3;  // half A = 0, B = 1; wave within the half
-  const int fr = lane & 15, fc = lane >> 4;
-  const int64_t r0 = roi * RF_S;
   constexpr int NK = 512 / BK;
-  if (tid < RF2_NCTR) ctr[tid] = 0;
+  const bool prof = a.prof != nullptr;
+  if (threadIdx.x < RF2_NCTR) ctr[threadIdx.x] = 0;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   g4_barrier();  // the only full barrier: counters zeroed
+  int64_t roi = MODE == 2 ? roi0 : (lb >> 1);
+  for (uint32_t it = 0; roi < a.R; ++it, roi += stride) {
+  const uint32_t t4 = 4u * (it + 1), p4 = 4u * it;  // counter targets: this ROI's / the previous one's
+  // lane-dependent values re-derived per ROI through an opaque copy: hoisted out of the ROI
+  // loop, every address the body derives from them stayed live across it (268 VGPRs spilled)
+  int tid_o = threadIdx.x;
+  asm volatile("" : "+v"(tid_o));
+  const int tid = tid_o, lane = tid & 63;
+  const int fr = lane & 15, fc = lane >> 4;
+  unsigned long long pst[8];
+  if (prof) pst[0] = eg_stamp();
+  const int64_t r0 = roi * RF_S;
 
   // X -> blocks 0..15, moved by half A only (2 DMA ops per block per wave: pieces
   // 100 hw + lane and 100 hw + 64 + lane < 400, piece p = row p >> 2, slot p & 3)
@@ -2075,9 +2087,17 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   // ---- GEMM1 (K = 512 over X blocks 0..15); A: 8 DMA ops per group, B: none.  One
   // loop per half (HALF a template constant): a half test inside the unrolled loop costs
   // spills
+  // (persistent mode, targets 0 on the first ROI: before the previous ROI's blocks are
+  // overwritten, half A's staging reads (X blocks 0..7) and both halves' GEMM2 (blocks 8..15
+  // held Y2(B)) are done)
   auto gemm1 = [&](auto half_c) {
     constexpr int HALF = decltype(half_c)::value;
-    if (HALF == 0) issueX(0);
+    if (HALF == 0) {
+      rf2_wait(ctr + RF2_CSD + 0, p4);
+      rf2_wait(ctr + RF2_CG2 + 0, p4);
+      rf2_wait(ctr + RF2_CG2 + 1, p4);
+      issueX(0);
+    }
     rf_loadB(b1p, 0, bq[0]);
     rf_loadB(b1p, 1, bq[1]);
 #pragma unroll
@@ -2089,14 +2109,14 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
         if (kt % 4 == 0) {
           rf_vmwait(0, b);
           rf2_signal(ctr + RF2_CX + kt / 4, lane);
-          rf2_wait(ctr + RF2_CX + kt / 4, 4);
+          rf2_wait(ctr + RF2_CX + kt / 4, t4);
           if (kt / 4 + 1 < 4) issueX(kt / 4 + 1);
         } else {
           rf_vmwait(((kt - 1) % 4 == 0 && (kt - 1) / 4 + 1 < 4 ? 8 : 0) + (kt + 1 < NK ? 4 : 0), b);
         }
       } else {
         rf_vmwait(kt + 1 < NK ? 4 : 0, b);
-        if (kt % 4 == 0) rf2_wait(ctr + RF2_CX + kt / 4, 4);
+        if (kt % 4 == 0) rf2_wait(ctr + RF2_CX + kt / 4, t4);
       }
       if (kt + 2 < NK) rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
       rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
@@ -2108,8 +2128,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   } else {
     // B starts behind A (rf_lag K steps; 16 = after A's whole GEMM1): run together, the
     // two halves share every SIMD's matrix pipe and reach their VALU phases together
-    if (a.lag >= 16) rf2_wait(ctr + RF2_CG1 + 0, 4);
-    else if (a.lag > 0) rf2_wait(ctr + RF2_CX + a.lag / 4, 4);
+    if (a.lag >= 16) rf2_wait(ctr + RF2_CG1 + 0, t4);
+    else if (a.lag > 0) rf2_wait(ctr + RF2_CX + a.lag / 4, t4);
     gemm1(std::integral_constant<int, 1>{});
   }
   __builtin_amdgcn_s_setprio(0);
@@ -2118,10 +2138,13 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     asm volatile("" ::"v"(acc[6][3][3]));
     pst[1] = eg_stamp();
   }
-  // B's Y1 goes over X blocks 8..15: every wave of both halves must be past GEMM1
+  // B's Y1 goes over X blocks 8..15: every wave of both halves must be past GEMM1; A's over
+  // blocks 16..23, which held the previous ROI's B staging until B's stores read it
   if (half == 1) {
-    rf2_wait(ctr + RF2_CG1 + 0, 4);
-    rf2_wait(ctr + RF2_CG1 + 1, 4);
+    rf2_wait(ctr + RF2_CG1 + 0, t4);
+    rf2_wait(ctr + RF2_CG1 + 1, t4);
+  } else {
+    rf2_wait(ctr + RF2_CSD + 1, p4);
   }
   // ---- Y1 -> LDS (the wave's 64 channels of its half's region)
 #pragma unroll
@@ -2147,7 +2170,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   rf_loadB(b2p, 0, bq[0]);
   rf_loadB(b2p, 1, bq[1]);
   rf2_signal(ctr + RF2_CY1 + half, lane);
-  rf2_wait(ctr + RF2_CY1 + half, 4);  // the half's Y1 is in
+  rf2_wait(ctr + RF2_CY1 + half, t4);  // the half's Y1 is in
   if (prof) pst[2] = eg_stamp();
   asm volatile("s_waitcnt vmcnt(8)" : "+v"(wreg[0]), "+v"(wreg[1]), "+v"(wreg[2]), "+v"(wreg[3]), "+v"(wreg[4]),
                "+v"(wreg[5]), "+v"(wreg[6]), "+v"(wreg[7]), "+v"(wreg[8]), "+v"(wreg[9]), "+v"(wreg[10]),
@@ -2171,7 +2194,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     uint32_t o0[25], o1[25];
     auto prefetch = [&]() {  // rf_body's L2 prefetch of ROI + a.pf's X rows (reinforce workgroups)
       if (G == 0 && a.pf) {
-        const int64_t rn = min(roi + a.pf, a.R - 1);
+        const int64_t rn = min(MODE == 2 ? roi + stride : roi + a.pf, a.R - 1);
         const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
         const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
         asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
@@ -2183,7 +2206,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
       rf_dw5q<0, 1>(Y, yb, wreg, o1);
       prefetch();
       rf2_signal(ctr + RF2_CDW + cg, lane);
-      rf2_wait(ctr + RF2_CDW + cg, 2);
+      rf2_wait(ctr + RF2_CDW + cg, 2 * (it + 1));
       rf_dw5q_store<0, 0>(Y, yb, o0);
       rf_dw5q_store<0, 1>(Y, yb, o1);
     } else {
@@ -2191,7 +2214,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
       rf_dw5q<1, 1>(Y, yb, wreg, o1);
       prefetch();
       rf2_signal(ctr + RF2_CDW + cg, lane);
-      rf2_wait(ctr + RF2_CDW + cg, 2);
+      rf2_wait(ctr + RF2_CDW + cg, 2 * (it + 1));
       rf_dw5q_store<1, 0>(Y, yb, o0);
       rf_dw5q_store<1, 1>(Y, yb, o1);
     }
@@ -2212,8 +2235,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     u32x4(&b)[4] = bq[kt % 3];
     rf_vmwait(kt + 1 < NK ? 4 + (kt < 2 ? NPF : 0) : 0, b);
     if (kt == 2 && G == 0) asm volatile("" : "+v"(pf0), "+v"(pf1));  // retired by the wait above
-    if (kt == 0) rf2_wait(ctr + RF2_CY2 + 0, 4);
-    if (kt == 8) rf2_wait(ctr + RF2_CY2 + 1, 4);
+    if (kt == 0) rf2_wait(ctr + RF2_CY2 + 0, t4);
+    if (kt == 8) rf2_wait(ctr + RF2_CY2 + 1, t4);
     if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
     if (kt == NK - 3) {
 #pragma unroll
@@ -2245,7 +2268,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   if constexpr (MODE == 1) {
     rf3_tail<G>(a, roi, smem, acc, lb, prof ? pst[0] : 0ull);
     return;
-  }
+  } else {
   if (a.sum_lanes) {
     // every lane converts and stores one channel's sum (the butterfly leaves all 16 sums
     // of a row group in every lane of it): one fixed-point conversion per lane instead of
@@ -2290,10 +2313,10 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   // ---- output staging: A over blocks 0..7 (X, dead once B is past GEMM1), B over Y(A)
   // (dead once both halves are past GEMM2); 16-B chunk c of row r at slot c ^ (r & 15)
   if (half == 0) {
-    rf2_wait(ctr + RF2_CG1 + 1, 4);
+    rf2_wait(ctr + RF2_CG1 + 1, t4);
   } else {
-    rf2_wait(ctr + RF2_CG2 + 0, 4);
-    rf2_wait(ctr + RF2_CG2 + 1, 4);
+    rf2_wait(ctr + RF2_CG2 + 0, t4);
+    rf2_wait(ctr + RF2_CG2 + 1, t4);
   }
   uint32_t* stg = Y + (half ? 16 * RF_KBS : 0);
 #pragma unroll
@@ -2310,7 +2333,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     }
   }
   rf2_signal(ctr + RF2_CST + half, lane);
-  rf2_wait(ctr + RF2_CST + half, 4);
+  rf2_wait(ctr + RF2_CST + half, t4);
   if (prof) pst[6] = eg_stamp();
   {
     uint16_t* dst = a.XRN + r0 * 1024 + G * 512 + half * 256;
@@ -2322,15 +2345,19 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
           *reinterpret_cast<const uint4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2));
     }
   }
+  rf2_signal(ctr + RF2_CSD + half, lane);  // this wave's staging reads are done (the next ROI may write)
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pst[7] = eg_stamp();
     if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
-      unsigned long long* o = a.prof + (lb * 8 + wave) * 8;
+      unsigned long long* o = a.prof + ((roi * 2 + G) * 8 + wave) * 8;
       for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
       o[7] = pst[7] - pst[0];
     }
   }
+  }  // MODE != 1
+  if constexpr (MODE != 2) break;
+  }  // ROI loop
 }
 
 // workgroup (roi, g) = logical id 2 roi + g, XCD-remapped: a ROI's two groups run on one
@@ -2349,6 +2376,18 @@ __global__ void __launch_bounds__(512, 1) rmb_front2_kernel(RfArgs a) {
 }
 // fused: rmb_front + SE + transition; the grid is padded to a multiple of 16 workgroups so
 // xcd_remap never splits a ROI's pair across XCDs (the pair hands x_n over through L2)
+// persistent front (rf_v 3): 16 k workgroups; workgroup w sits on XCD w % 8, runs group
+// G = (w / 8) & 1 and the ROIs xcd + 8 (p + P k), p = w / 16, P = gridDim / 16 -- both groups of
+// a ROI on one XCD (its X rows read from HBM once), every ROI once
+__global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int w = blockIdx.x, xcd = w & 7, slot = w >> 3;
+  const int64_t P = gridDim.x / 16;
+  const int64_t roi0 = xcd + 8 * (int64_t)(slot >> 1), stride = 8 * P;
+  if (slot & 1) rf2_body<1, 2>(a, 0, smem, roi0, stride);
+  else rf2_body<0, 2>(a, 0, smem, roi0, stride);
+}
+
 __global__ void __launch_bounds__(512, 1) rmb_fused_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -2890,6 +2929,8 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF_LDS);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front2_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
     attr = true;
   }
   RfArgs a;
@@ -2906,6 +2947,20 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.lag = g_rf_lag;
   a.sum_lanes = g_rf_sumlanes;
   a.dwprio = g_rf_dwprio;
+  if (g_rf_v == 3) {
+    // persistent: 16 workgroups per 8 ROIs up to one per CU (a multiple of 16, so both groups
+    // of a ROI share an XCD)
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16) ncu = 16;
+    }
+    const int64_t groups = std::min<int64_t>((a.R + 7) / 8, ncu / 16);
+    hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups)), dim3(512), RF2_LDS,
+                       reinterpret_cast<hipStream_t>(stream), a);
+    return trk::check_launch("rmb_front3_kernel");
+  }
   if (g_rf_v == 2) {
     hipLaunchKernelGGL(rmb_front2_kernel, dim3((unsigned)nwg), dim3(512), RF2_LDS,
                        reinterpret_cast<hipStream_t>(stream), a);

@@ -759,7 +759,7 @@ def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R, t4_mode):
         ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp[:-1])
 
 
-@pytest.mark.parametrize("rf_v,rf_lag", [(2, 16), (2, 8), (2, 0), (1, 16)])
+@pytest.mark.parametrize("rf_v,rf_lag", [(2, 16), (2, 8), (2, 0), (1, 16), (3, 16), (3, 0)])
 @pytest.mark.parametrize("R", [1, 37, 2048])
 def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag):
     """trk_enc_rmb_front (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
@@ -767,7 +767,8 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag):
     roundings, so XRN must be bit-identical; the ROI sums add the same f32 activations in
     another order (tol 1e-5 of the largest sum).  R = 2048 is the bench's c3 launch.
     rf_v 2 (default): the two wave halves hand off through LDS counters, half B starting
-    GEMM1 rf_lag K steps behind half A; 1: lockstep phases."""
+    GEMM1 rf_lag K steps behind half A; 1: lockstep phases; 3: rf_v 2 as a persistent grid (a
+    workgroup runs 1..16 ROIs of one group, the next ROI's GEMM1 under this one's epilogue)."""
     L = trk.lib()
     assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf_lag", rf_lag) == 0
     try:
