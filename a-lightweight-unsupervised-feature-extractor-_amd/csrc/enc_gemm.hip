@@ -1647,6 +1647,22 @@ __device__ __forceinline__ void rf2_wait(uint32_t* ctr, uint32_t target) {
       : "memory", "scc");
 }
 
+// 16-B LDS-DMA of every lane (LDS byte address base + 16 lane); and of lanes 0..35 only
+__device__ __forceinline__ void rf_dma16(const void* g, uint32_t base) {
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(base) : "memory");
+}
+__device__ __forceinline__ void rf_dma16_lanes36(const void* g, uint32_t base) {
+  uint64_t saved;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[mk]\n\t"
+      "global_load_lds_dwordx4 %[g], off\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [sv] "=&s"(saved)
+      : [mk] "s"(0xFFFFFFFFFull), [b] "{m0}"(base), [g] "v"(g)
+      : "memory");
+}
+
 // ---- fused tail (trk_enc_rmb_fused): what trk_enc_se and trk_enc_transition_gemm did for
 // the ROI, inside the ROI's two workgroups.  acc holds the group's activated 64 x 112 tile.
 //   normal group (G = 1): m_n, then its bf16 Hardswish(x_n) rows -> XN with sc1 stores,
@@ -2061,15 +2077,19 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   const int xp1 = 100 * hw + lane, xp2 = 100 * hw + 64 + lane;
   const uint16_t* xs1 = a.X + (r0 + (xp1 >> 2)) * 512 + (((xp1 & 3) ^ rf_sw(xp1 >> 2)) * 8);
   const uint16_t* xs2 = a.X + (r0 + min(xp2 >> 2, RF_S - 1)) * 512 + (((xp2 & 3) ^ rf_sw(xp2 >> 2)) * 8);
+  // the X DMA as asm (M0 and, for the 36-lane second op, exec set explicitly): with the
+  // builtin under `if (lane < 36)` the persistent variant's compiler merged the two ops of
+  // consecutive blocks across the divergent region and issued a 36-lane op with every lane
+  const uint32_t ybase = lds_addr(Y);
   auto issueX = [&](int grp) {
     const uint16_t* p1 = xs1;
     const uint16_t* p2 = xs2;
     asm volatile("" : "+v"(p1), "+v"(p2));  // per group: the block addresses are not all hoisted
 #pragma unroll
     for (int kb = 4 * grp; kb < 4 * grp + 4; ++kb) {
-      __builtin_amdgcn_global_load_lds(GPTR(p1 + kb * BK), LPTR(Y + kb * RF_KBS + 400 * hw), 16, 0, 0);
-      if (lane < 36)
-        __builtin_amdgcn_global_load_lds(GPTR(p2 + kb * BK), LPTR(Y + kb * RF_KBS + 400 * hw + 256), 16, 0, 0);
+      const uint32_t d = __builtin_amdgcn_readfirstlane(ybase + (kb * RF_KBS + 400 * hw) * 4);
+      rf_dma16(p1 + kb * BK, d);
+      rf_dma16_lanes36(p2 + kb * BK, d + 1024);
     }
   };
   const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
