@@ -44,7 +44,9 @@ int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column s
 int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + rf_pf, 0: none (GEMM1
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
-int g_rf_v = 2;   // trk_set_tuning("rf_v"): rmb_front body, 2 = decoupled halves, 1 = lockstep phases
+int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rf_v 3 workgroup pairs per XCD (0 = CUs / 16 - 2)
+int g_rf_v = 3;  // trk_set_tuning("rf_v"): rmb_front body, 3 = persistent rf_v 2, 2 = decoupled halves,
+                 // 1 = lockstep phases
 int g_rf_dwprio = 0;  // trk_set_tuning("rf_dwprio"): rf2's depthwise at priority 2: 0 none, 1 half B, 2 both
 int g_rf_sumlanes = 1;  // trk_set_tuning("rf_sumlanes"): rf2's ROI sums one channel per lane (1, default: the
                         // activation + sums phase 10.6K vs 12.1K cycles per wave, 569 vs 582 us isolated, pipeline
@@ -2976,7 +2978,11 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
       (void)hipGetDevice(&dev);
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16) ncu = 16;
     }
-    const int64_t groups = std::min<int64_t>((a.R + 7) / 8, ncu / 16);
+    // (0: two CUs per XCD left free -- the tracker's and the ROI stream's kernels start there
+    // instead of waiting for a persistent workgroup to end: 2.03-2.05 vs 1.96-1.98M ROIs/s
+    // over four interleaved pairs against rf_v 2, where all 16 pairs measured a tie)
+    const int64_t groups =
+        std::min<int64_t>((a.R + 7) / 8, g_rf3_groups > 0 ? g_rf3_groups : std::max(1, ncu / 16 - 2));
     hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups)), dim3(512), RF2_LDS,
                        reinterpret_cast<hipStream_t>(stream), a);
     return trk::check_launch("rmb_front3_kernel");

@@ -60,9 +60,12 @@ const char* trk_last_error(void);
  *                    prefetched into L2; 4: without the prefetch
  *   "rf_pf"          8 (default): trk_enc_rmb_front prefetches the X rows of ROI + rf_pf into
  *                    L2 (0..64; 0: no prefetch)
- *   "rf_v"           2 (default): trk_enc_rmb_front's wave halves hand off through LDS counters
- *                    (decoupled phases); 1: lockstep phases (both bit-identical)
- *   "rf_lag"         16 (default): with rf_v 2 (and in trk_enc_rmb_fused), half B starts its
+ *   "rf_v"           3 (default): trk_enc_rmb_front as a persistent grid, each workgroup running
+ *                    the ROIs of one channel group back to back; 2: one ROI per workgroup, the
+ *                    wave halves handing off through LDS counters; 1: lockstep phases (all
+ *                    bit-identical)
+ *   "rf3_groups"     0 (default: CUs / 16 - 2): rf_v 3 workgroup pairs per XCD (1..64)
+ *   "rf_lag"         16 (default): with rf_v 2 / 3 (and in trk_enc_rmb_fused), half B starts its
  *                    first GEMM once half A is past that K step (0, 4, 8, 12, 16)
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is

@@ -17,7 +17,7 @@ for R in (1, 2, 9, 37, 2048):
         L.trk_set_tuning(b"rf_v", v)
         XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
         out[v] = (XRN.float(), ops.enc_sums_reduce(s, 100))
-    L.trk_set_tuning(b"rf_v", 2)
+    L.trk_set_tuning(b"rf_v", 3)
     d = (out[2][0] - out[3][0]).abs()
     bad = d > 0
     rows = bad.any(1).nonzero().flatten()

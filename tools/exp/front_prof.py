@@ -22,7 +22,7 @@ buf = torch.zeros(2 * R * 8 * 8, dtype=torch.int64, device=dev)
 names = ["gemm1", "y1_store", "depthwise", "gemm2", "act_sums", "staging", "stores", "total"]
 
 
-DEFAULTS = {"rf_pf": 8, "rf_v": 2, "rf_lag": 16, "rf_sumlanes": 1, "rf_dwprio": 0}  # knobs whose default is not 0
+DEFAULTS = {"rf_pf": 8, "rf_v": 3, "rf_lag": 16, "rf_sumlanes": 1, "rf_dwprio": 0}  # knobs whose default is not 0
 
 
 def apply(v, reset=False):

@@ -12,7 +12,7 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"roi_sweep_kernel": "roi_align", "nchw_to_nhwc_kernel": "nchw_to_nhwc", "g1dw_kernel": "enc_g1_dwconv", "g1dw4_kernel": "enc_g1_dwconv", "rmb_front_kernel": "enc_rmb_front", "rmb_front2_kernel": "enc_rmb_front", "rmb_fused_kernel": "enc_rmb_fused", "trans4_kernel": "enc_gemm_trans", "gemm4w_trans_kernel": "enc_gemm_trans",
+SHORT = {"roi_sweep_kernel": "roi_align", "nchw_to_nhwc_kernel": "nchw_to_nhwc", "g1dw_kernel": "enc_g1_dwconv", "g1dw4_kernel": "enc_g1_dwconv", "rmb_front_kernel": "enc_rmb_front", "rmb_front2_kernel": "enc_rmb_front", "rmb_front3_kernel": "enc_rmb_front", "rmb_fused_kernel": "enc_rmb_fused", "trans4_kernel": "enc_gemm_trans", "gemm4w_trans_kernel": "enc_gemm_trans",
          "gemm4_kernel<0": "enc_gemm_dsc", "gemm4_kernel<1": "enc_gemm_trans", "enc_se_kernel": "enc_se",
          "enc_head_kernel": "enc_head", "cost_kernel": "cost", "cost3_kernel": "cost", "det_prep_kernel": "cost_prep", "lsap_kernel": "lsap",
          "step_begin_kernel": "step_begin", "step_mid_kernel": "step_mid", "step_end_kernel": "step_end",
