@@ -44,6 +44,9 @@ int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column s
 int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + rf_pf, 0: none (GEMM1
                   // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
 int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
+int g_rf3_pf = 0;  // trk_set_tuning("rf3_pf"): rf_v 3 L2 prefetch of the workgroup's next ROI (0: off --
+                  // its X DMA already starts under this ROI's epilogue; 537 vs 597 MB fetched per
+                  // launch, the pipeline ahead in 4 of 4 interleaved pairs)
 int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rf_v 3 workgroup pairs per XCD (0 = CUs / 16 - 2)
 int g_rf_v = 3;  // trk_set_tuning("rf_v"): rmb_front body, 3 = persistent rf_v 2, 2 = decoupled halves,
                  // 1 = lockstep phases
@@ -2964,7 +2967,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.XRN = (uint16_t*)XRN;
   a.sums = sums;
   a.R = M / RF_S;
-  a.pf = g_rf_pf;
+  a.pf = g_rf_v == 3 ? g_rf3_pf : g_rf_pf;
   a.prof = g_enc_prof;
   a.lag = g_rf_lag;
   a.sum_lanes = g_rf_sumlanes;

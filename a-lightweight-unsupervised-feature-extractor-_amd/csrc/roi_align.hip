@@ -938,6 +938,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "rf_sumlanes")) { extern int g_rf_sumlanes; TRK_REQUIRE(value == 0 || value == 1, "rf_sumlanes in {0, 1}"); g_rf_sumlanes = value; return TRK_OK; }
   if (!strcmp(key, "rf_dwprio")) { extern int g_rf_dwprio; TRK_REQUIRE(value >= 0 && value <= 2, "rf_dwprio in {0, 1, 2}"); g_rf_dwprio = value; return TRK_OK; }
   if (!strcmp(key, "rf_lag")) { extern int g_rf_lag; TRK_REQUIRE(value >= 0 && value <= 16 && value % 4 == 0, "rf_lag in {0, 4, 8, 12, 16}"); g_rf_lag = value; return TRK_OK; }
+  if (!strcmp(key, "rf3_pf")) { extern int g_rf3_pf; TRK_REQUIRE(value == 0 || value == 1, "rf3_pf in {0, 1}"); g_rf3_pf = value; return TRK_OK; }
   if (!strcmp(key, "rf3_groups")) { extern int g_rf3_groups; TRK_REQUIRE(value >= 0 && value <= 64, "rf3_groups in 0..64"); g_rf3_groups = value; return TRK_OK; }
   if (!strcmp(key, "rf_v")) { extern int g_rf_v; TRK_REQUIRE(value >= 1 && value <= 3, "rf_v in {1, 2, 3}"); g_rf_v = value; return TRK_OK; }
   if (!strcmp(key, "g1dw")) { extern int g_g1dw; TRK_REQUIRE(value == 4 || value == 6, "g1dw in {4, 6}"); g_g1dw = value; return TRK_OK; }

@@ -58,13 +58,14 @@ const char* trk_last_error(void);
  *                    relative of the lane-reduction sums, 0)
  *   "g1dw"           6 (default): fused first GEMM + depthwise with the next round's rows
  *                    prefetched into L2; 4: without the prefetch
- *   "rf_pf"          8 (default): trk_enc_rmb_front prefetches the X rows of ROI + rf_pf into
- *                    L2 (0..64; 0: no prefetch)
+ *   "rf_pf"          8 (default): trk_enc_rmb_front rf_v 1 / 2 prefetches the X rows of ROI + rf_pf
+ *                    into L2 (0..64; 0: no prefetch)
  *   "rf_v"           3 (default): trk_enc_rmb_front as a persistent grid, each workgroup running
  *                    the ROIs of one channel group back to back; 2: one ROI per workgroup, the
  *                    wave halves handing off through LDS counters; 1: lockstep phases (all
  *                    bit-identical)
  *   "rf3_groups"     0 (default: CUs / 16 - 2): rf_v 3 workgroup pairs per XCD (1..64)
+ *   "rf3_pf"         0 (default): rf_v 3 without the L2 prefetch of the workgroup's next ROI; 1: with
  *   "rf_lag"         16 (default): with rf_v 2 / 3 (and in trk_enc_rmb_fused), half B starts its
  *                    first GEMM once half A is past that K step (0, 4, 8, 12, 16)
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup

@@ -759,10 +759,11 @@ def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R, t4_mode):
         ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp[:-1])
 
 
-@pytest.mark.parametrize("rf_v,rf_lag,groups", [(2, 16, 0), (2, 8, 0), (2, 0, 0), (1, 16, 0), (3, 16, 0), (3, 0, 0),
-                                                (3, 16, 1), (3, 16, 16), (3, 16, 64)])
+@pytest.mark.parametrize("rf_v,rf_lag,groups,pf", [(2, 16, 0, 0), (2, 8, 0, 0), (2, 0, 0, 0), (1, 16, 0, 0),
+                                                   (3, 16, 0, 0), (3, 0, 0, 0), (3, 16, 1, 0), (3, 16, 16, 1),
+                                                   (3, 16, 64, 0)])
 @pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag, groups):
+def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag, groups, pf):
     """trk_enc_rmb_front (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
     LDS) vs enc_g1_dwconv -> enc_dsc_gemm: the same MFMA shape, K order and bf16
     roundings, so XRN must be bit-identical; the ROI sums add the same f32 activations in
@@ -772,16 +773,18 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag, groups):
     epilogue; 1 pair: 256 ROIs per workgroup at R = 2048, the LDS counters counting on
     across all of them; 64: more pairs than ROIs); 2: one ROI per workgroup, the two wave
     halves handing off through LDS counters, half B starting GEMM1 rf_lag K steps behind
-    half A; 1: lockstep phases."""
+    half A; 1: lockstep phases.  pf: rf3_pf, the persistent grid's L2 prefetch of the next ROI
+    (off by default)."""
     L = trk.lib()
     assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf_lag", rf_lag) == 0
-    assert L.trk_set_tuning(b"rf3_groups", groups) == 0
+    assert L.trk_set_tuning(b"rf3_groups", groups) == 0 and L.trk_set_tuning(b"rf3_pf", pf) == 0
     try:
         _rmb_front_vs_two_kernel(gpu, R)
     finally:
         L.trk_set_tuning(b"rf_v", 3)
         L.trk_set_tuning(b"rf_lag", 16)
         L.trk_set_tuning(b"rf3_groups", 0)
+        L.trk_set_tuning(b"rf3_pf", 0)
 
 
 @pytest.mark.parametrize("R", [1, 37, 2048])
