@@ -946,6 +946,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "enc_sums")) { extern int g_enc_sums; TRK_REQUIRE(value == 0 || value == 1, "enc_sums in {0, 1}"); g_enc_sums = value; return TRK_OK; }
   if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value == 0 || value == 1, "enc_gemm in {0, 1}"); g_enc_gemm = value; return TRK_OK; }
   if (!strcmp(key, "dw_fast")) { extern int g_dw_fast; TRK_REQUIRE(value == 0 || value == 1, "dw_fast in {0,1}"); g_dw_fast = value; return TRK_OK; }
+  if (!strcmp(key, "lsap_split")) { extern int g_lsap_split; TRK_REQUIRE(value == 0 || value == 1, "lsap_split in {0, 1}"); g_lsap_split = value; return TRK_OK; }
   if (!strcmp(key, "lsap_dev_lds_kb")) { extern int g_lsap_dev_lds_kb; TRK_REQUIRE(value >= 8 && value <= 156, "lsap_dev_lds_kb in [8, 156]"); g_lsap_dev_lds_kb = value; return TRK_OK; }
   if (!strcmp(key, "roi_vec")) { TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "roi_vec in {0,1,2,4}"); g_roi_vec = value; return TRK_OK; }
   trk::set_error("set_tuning: unknown key '%s'", key);

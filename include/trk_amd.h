@@ -72,6 +72,9 @@ const char* trk_last_error(void);
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
  *                    given (the device tracker), else the detection-tile kernel; 1: the
  *                    LDS bank-resident cost2 kernel (all bit-identical)
+ *   "lsap_split"     0 (default): trk_lsap_dev launches the bound's kernel once; 1: a kernel sized
+ *                    for 256 columns for the matrices that fit it, then the bound's kernel for the
+ *                    wider ones (it exits at once when there are none)
  *   "lsap_dev_lds_kb" LDS budget of trk_lsap_dev workgroups (default 24: they fit beside the
  *                    encoder's workgroups instead of waiting for a whole CU) */
 int trk_set_tuning(const char* key, int value);

@@ -1146,3 +1146,51 @@ def test_roi_align_a1_boundary_branches_gpu(trk, oracle, gpu):
             finally:
                 L.trk_set_tuning(b"roi_fma", 1)
             assert torch.equal(nhwc.float().cpu(), torch.from_numpy(exp).to(od).float()), (S, od)
+
+
+@pytest.mark.parametrize("split", [1, 0])
+def test_lsap_dev_split_launch_vs_host_sizes(trk, gpu, split):
+    """trk_lsap_dev (shapes in device memory, one bound for the batch) vs trk_lsap (host
+    shapes, the kernel sized by the widest matrix): lsap_split 1 (off by default) solves the matrices of at
+    most 256 columns in the narrow kernel and the wider ones in the bound's kernel; the
+    narrow launch also owns the empty and the out-of-bound matrices (status -4, assign -1
+    over the bound's rows).  Every output is bit-identical to the host-sized launch."""
+    from importlib import import_module
+    ops = import_module(trk.__name__ + ".ops")
+    L = trk.lib()
+    shapes = [(0, 5), (3, 0), (40, 60), (256, 256), (200, 300), (300, 260), (600, 700), (64, 1), (700, 600)]
+    B = 720  # nr / nc bound (16 column slots: the bench's c3 bound class)
+    rng = np.random.default_rng(11)
+    F = len(shapes) + 1  # + one matrix outside the bound
+    C = np.full((F, B + 8, B), 1e3, np.float32)
+    for k, (r, c) in enumerate(shapes):
+        C[k, :r, :c] = rng.uniform(0, 100, (r, c)).astype(np.float32)
+    Cg = torch.from_numpy(C).to(gpu)
+    nr = shapes + [(B + 8, 10)]
+    kmax = B  # trk_lsap_dev: kmax >= min(nr, nc) bound
+    ref = {"rows": torch.empty((F, kmax), dtype=torch.int64, device=gpu),
+           "cols": torch.empty((F, kmax), dtype=torch.int64, device=gpu),
+           "count": torch.empty((F,), dtype=torch.int32, device=gpu),
+           "status": torch.empty((F,), dtype=torch.int32, device=gpu),
+           "assign": torch.empty((F, B + 8), dtype=torch.int32, device=gpu)}
+    trk.lsap_batched(Cg, [r for r, _ in shapes] + [0], [c for _, c in shapes] + [0], cost_max=50.0, out=ref)
+    dnr = torch.tensor([r for r, _ in nr], dtype=torch.int32, device=gpu)
+    dnc = torch.tensor([c for _, c in nr], dtype=torch.int32, device=gpu)
+    out = {k: torch.full_like(v, -7) for k, v in ref.items()}
+    assert L.trk_set_tuning(b"lsap_split", split) == 0
+    try:
+        rc = L.trk_lsap_dev(F, ops._ptr(Cg), ops._lib.TRK_F32, B, (B + 8) * B, ops._ptr(dnr), ops._ptr(dnc), B, B,
+                            kmax, ops._ptr(out["rows"]), ops._ptr(out["cols"]), ops._ptr(out["count"]),
+                            ops._ptr(out["status"]), ops._ptr(out["assign"]), B + 8, 50.0, ops._stream(gpu))
+        assert rc == 0
+        torch.cuda.synchronize()
+    finally:
+        L.trk_set_tuning(b"lsap_split", 0)
+    cnt = ref["count"].cpu().numpy()
+    assert (out["status"][:-1].cpu() == ref["status"][:-1].cpu()).all() and int(out["status"][-1]) == -4
+    assert int(out["count"][-1]) == 0 and (out["assign"][-1, :B].cpu() == -1).all()
+    for k, (r, c) in enumerate(shapes):
+        n = int(cnt[k])
+        assert int(out["count"][k]) == n, k
+        assert torch.equal(out["rows"][k, :n], ref["rows"][k, :n]) and torch.equal(out["cols"][k, :n], ref["cols"][k, :n]), k
+        assert torch.equal(out["assign"][k, :r], ref["assign"][k, :r]), k
