@@ -33,6 +33,7 @@
 //             SiLU(T); T is never stored.
 //   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
 #include "trk_common.h"
+#include "rb_linear.h"
 
 #include <utility>
 
@@ -1214,6 +1215,10 @@ struct RfArgs {
   int epoch;
   float *m_r, *m_n, *s; // [R][512] squeeze means and SE scales (trk_enc_se's outputs)
   long long* tsums;     // [R][kPart][512] sums of SiLU(T) (partial 0; the others 0)
+  // front + SE (trk_enc_rmb_front_se, rf_v 3): each workgroup writes its ROIs' squeeze means
+  // (group 0 m_r, group 1 m_n) and group 0 then runs the SE over its ROIs in batches of 16;
+  // sums may be null (then not written)
+  int se_front, se_H;
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
@@ -2047,6 +2052,34 @@ __device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned 
   }
 }
 
+// front + SE: the SE of the workgroup's ROIs roi0, roi0 + stride, ... in batches of 16 rows --
+// enc_se_kernel's arithmetic (rb_linear, the same tiles and K order, 8 waves), so s is
+// bit-identical to trk_enc_se on the means this kernel wrote
+__device__ __forceinline__ void rf_se_batches(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride) {
+  constexpr int C = 512;
+  const int H = a.se_H, ldx = ld_rows(C), ldh = ld_rows(H);
+  float* Xs = reinterpret_cast<float*>(smem);
+  float* Hs = Xs + RB * ldx;
+  for (int64_t b0 = roi0; b0 < a.R; b0 += RB * stride) {
+    const int nrow = (int)min<int64_t>(RB, (a.R - b0 + stride - 1) / stride);
+    for (int q = threadIdx.x; q < RB * (C / 4); q += blockDim.x) {
+      const int rr = q / (C / 4), c = (q % (C / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rr < nrow) v = *reinterpret_cast<const float4*>(a.m_r + (b0 + rr * stride) * C + c);
+      *reinterpret_cast<float4*>(Xs + swz_at(rr, c, ldx)) = v;
+    }
+    __syncthreads();
+    rb_linear<8>(Xs, ldx, a.se_w1, a.se_b1, H, C,
+                 [&](int row, int col, float v) { Hs[swz_at(row, col, ldh)] = fmaxf(v, 0.f); });
+    __syncthreads();
+    float* __restrict__ sout = a.s;
+    rb_linear<8>(Hs, ldh, a.se_w2, a.se_b2, C, H, [&](int row, int col, float v) {
+      if (row < nrow) sout[(b0 + row * stride) * C + col] = fminf(fmaxf(v + 3.0f, 0.f), 6.0f) / 6.0f;
+    });
+    __syncthreads();
+  }
+}
+
 // MODE 0: one ROI (lb >> 1) per workgroup; 1: rmb_fused (one ROI + the fused tail); 2: persistent
 // (rmb_front3): the workgroup runs ROIs roi0, roi0 + stride, ... of its group G, the LDS counters
 // count on across ROIs (targets 4 (it + 1)), and ROI it + 1's X DMA and GEMM1 start as soon as
@@ -2300,9 +2333,12 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     // 16 on the lanes fr == 0; the same bits
     const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
     const float x = rf3_colsum(acc, fr);
-    long long* o = a.sums + roi * kPart * 1024 + G * 512 + rf3_lane_ch(wave, fr, fc);
-    o[0] = llrintf(x * kFix);
-    for (int j = 1; j < cnt; ++j) o[j * 1024] = 0;
+    if (a.sums) {
+      long long* o = a.sums + roi * kPart * 1024 + G * 512 + rf3_lane_ch(wave, fr, fc);
+      o[0] = llrintf(x * kFix);
+      for (int j = 1; j < cnt; ++j) o[j * 1024] = 0;
+    }
+    if (MODE == 2 && a.se_front) (G == 0 ? a.m_r : a.m_n)[roi * 512 + rf3_lane_ch(wave, fr, fc)] = rf3_mean(x);
   } else
   {
     const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
@@ -2325,12 +2361,19 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
         sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
       }
       if (fr == 0) {
-        long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
+        if (a.sums) {
+          long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[e] * kFix);
-        for (int j = 1; j < cnt; ++j)
+          for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[e] * kFix);
+          for (int j = 1; j < cnt; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[j * 1024 + e] = 0;
+            for (int e = 0; e < 4; ++e) o[j * 1024 + e] = 0;
+        }
+        if (MODE == 2 && a.se_front) {
+          float* m = (G == 0 ? a.m_r : a.m_n) + roi * 512 + wave * 64 + t * 16 + fc * 4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) m[e] = rf3_mean(sv[e]);
+        }
       }
     }
   }
@@ -2383,6 +2426,13 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   }  // MODE != 1
   if constexpr (MODE != 2) break;
   }  // ROI loop
+  if constexpr (MODE == 2 && G == 0) {
+    if (a.se_front) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's m_r rows are in
+      g4_barrier();                                      // ... from every wave; LDS is free
+      rf_se_batches(a, smem, roi0, stride);
+    }
+  }
 }
 
 // workgroup (roi, g) = logical id 2 roi + g, XCD-remapped: a ROI's two groups run on one
@@ -2939,12 +2989,63 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
   return trk::check_launch("g1dw4_kernel");
 }
 
+namespace {
+struct FrontSe {  // trk_enc_rmb_front_se's SE operands (null: the plain front)
+  const float *w1, *b1, *w2, *b2;
+  int64_t H;
+  float *m_r, *m_n, *s;
+};
+int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p, const float* bias,
+                     void* XRN, long long* sums, const FrontSe* se, void* stream);
+}  // namespace
+
 extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                                  const float* bias, void* XRN, long long* sums, void* stream) {
+  TRK_REQUIRE(sums, "enc_rmb_front: null sums");
+  return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sums, nullptr, stream);
+}
+
+extern "C" int trk_enc_rmb_front_se(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                                    const float* bias, void* XRN, long long* sums, const float* se_w1,
+                                    const float* se_b1, int64_t H, const float* se_w2, const float* se_b2, float* m_r,
+                                    float* m_n, float* s, void* stream) {
+  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front_se: 10x10 ROIs (M %% 100 == 0)");
+  if (M == 0) return TRK_OK;
+  TRK_REQUIRE(H > 0 && H % 16 == 0 && H <= 512, "enc_rmb_front_se: SE hidden size H a multiple of 16 in [16, 512]");
+  TRK_REQUIRE(se_w1 && se_b1 && se_w2 && se_b2 && m_r && m_n && s && aligned16(se_w1) && aligned16(se_w2) &&
+                  aligned16(m_r) && aligned16(m_n) && aligned16(s),
+              "enc_rmb_front_se: null or unaligned SE pointer");
+  if (g_rf_v == 3) {
+    const FrontSe se{se_w1, se_b1, se_w2, se_b2, H, m_r, m_n, s};
+    return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sums, &se, stream);
+  }
+  // the one-ROI-per-workgroup fronts: the front, then trk_enc_se on its sums (a grow-only
+  // workspace when the caller passes none)
+  long long* sp = sums;
+  if (!sp) {
+    static long long* ws = nullptr;
+    static size_t ws_n = 0;
+    const size_t need = (size_t)(M / RF_S) * kPart * 1024;
+    if (need > ws_n) {
+      if (ws) (void)hipFree(ws);
+      ws = nullptr;
+      ws_n = 0;
+      TRK_REQUIRE(hipMalloc(&ws, need * sizeof(long long)) == hipSuccess, "enc_rmb_front_se: workspace allocation");
+      ws_n = need;
+    }
+    sp = ws;
+  }
+  if (int e = rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sp, nullptr, stream)) return e;
+  return trk_enc_se(sp, M / RF_S, 1024, RF_S, 512, se_w1, se_b1, H, se_w2, se_b2, m_r, m_n, s, stream);
+}
+
+namespace {
+int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p, const float* bias,
+                     void* XRN, long long* sums, const FrontSe* se, void* stream) {
   TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
   if (M == 0) return TRK_OK;
-  TRK_REQUIRE(X && W1p && wdw && W2p && bias && XRN && sums && aligned16(X) && aligned16(W1p) && aligned16(W2p) &&
-                  aligned16(XRN) && aligned16(wdw),
+  TRK_REQUIRE(X && W1p && wdw && W2p && bias && XRN && (sums || se) && aligned16(X) && aligned16(W1p) &&
+                  aligned16(W2p) && aligned16(XRN) && aligned16(wdw),
               "enc_rmb_front: null or unaligned pointer");
   const int64_t nwg = M / RF_S * 2;
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_rmb_front: too many workgroups");
@@ -2959,6 +3060,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
     attr = true;
   }
   RfArgs a;
+  memset(&a, 0, sizeof a);
   a.X = (const uint16_t*)X;
   a.W1p = (const uint4*)W1p;
   a.wdw = wdw;
@@ -2972,6 +3074,12 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
   a.lag = g_rf_lag;
   a.sum_lanes = g_rf_sumlanes;
   a.dwprio = g_rf_dwprio;
+  if (se) {
+    a.se_front = 1;
+    a.se_H = (int)se->H;
+    a.se_w1 = se->w1; a.se_b1 = se->b1; a.se_w2 = se->w2; a.se_b2 = se->b2;
+    a.m_r = se->m_r; a.m_n = se->m_n; a.s = se->s;
+  }
   if (g_rf_v == 3) {
     // persistent: 16 workgroups per 8 ROIs up to one per CU (a multiple of 16, so both groups
     // of a ROI share an XCD)
@@ -2999,6 +3107,7 @@ extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, cons
                      a);
   return trk::check_launch("rmb_front_kernel");
 }
+}  // namespace
 
 extern "C" int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                                  const float* bias, const void* Wtp, const float* bt, const float* se_w1,

@@ -237,6 +237,9 @@ class Model(nn.Module):
     fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel
                          # (enc_rmb_front; Y2 never reaches HBM); False: enc_g1_dwconv + enc_dsc_gemm
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
+    front_se = True      # with fused_front and fused_tail: the SE inside the front kernel (enc_rmb_front_se:
+                         # the persistent front's reinforce workgroups run it over their ROIs; no sums
+                         # round trip, no enc_se launch)
     fused_full = False   # with fused_front and fused_tail: the SE and the transition GEMM inside the
                          # front kernel too (enc_rmb_fused; the [M, 1024] XRN never reaches HBM)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
@@ -248,7 +251,8 @@ class Model(nn.Module):
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_rmb_front, enc_rmb_fused, enc_transition_gemm, enc_se, enc_head, enc_sums_reduce)
+                          enc_rmb_front, enc_rmb_front_se, enc_rmb_fused, enc_transition_gemm, enc_se, enc_head,
+                          enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -270,7 +274,15 @@ class Model(nn.Module):
             head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                     self.head.net[1].eps, W["h4"], W["h4b"])
             return DeferredHead(head, (tsums, s, m_r, m_n)) if self.defer_head else head()
-        if front:
+        se_out = None
+        if front and self.fused_tail and self.front_se and not (self.defer_tail and self.se_stream is not None):
+            XRN, _, m_r, m_n, s = enc_rmb_front_se(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"], W["se_w1"],
+                                                  W["se_b1"], W["se_w2"], W["se_b2"])
+            se_out = (m_r, m_n, s)
+            if self.stage_hook is not None:
+                self.stage_hook("g1")
+                self.stage_hook("dsc")
+        elif front:
             XRN, sums = enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
             if self.stage_hook is not None:
                 self.stage_hook("g1")
@@ -315,8 +327,10 @@ class Model(nn.Module):
                     return DeferredHead(head, (tsums, s, m_r, m_n)) if defer_head else head()
                 return DeferredTail(finish)
             if self.fused_tail:
-                # squeeze means + SE MLP, then Shake2 mix + projection head: one kernel each
-                m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+                # squeeze means + SE MLP (unless the front ran them), then Shake2 mix + projection
+                # head: one kernel each
+                m_r, m_n, s = se_out if se_out is not None else enc_se(sums, ss, W["se_w1"], W["se_b1"],
+                                                                      W["se_w2"], W["se_b2"])
                 tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True, Wtp=W.get("wt_pk"))
                 head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                         self.head.net[1].eps, W["h4"], W["h4b"])

@@ -305,6 +305,38 @@ def enc_sums_reduce(part: torch.Tensor, P: int) -> torch.Tensor:
     return out
 
 
+def enc_rmb_front_se(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
+                     bias: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+                     b2: torch.Tensor, want_sums: bool = False):
+    """enc_rmb_front + enc_se in one launch (trk_enc_rmb_front_se): returns (XRN, sums or
+    None, m_r, m_n, s) -- XRN as enc_rmb_front's, m_r / m_n / s bit-identical to enc_se on
+    its sums (card.py:59-78).  want_sums: also write the raw partial sums."""
+    _need_gpu(X, "enc_rmb_front_se")
+    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
+        raise TypeError("enc_rmb_front_se: bf16 operands required")
+    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
+        raise ValueError("enc_rmb_front_se: X must be contiguous [R*100, 512]")
+    pk = (2, 16, 32, 4, 16, 8)
+    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or not (W1p.is_contiguous() and W2p.is_contiguous()):
+        raise ValueError("enc_rmb_front_se: W1p / W2p must be enc_pack_fragments output [2, 16, 32, 4, 16, 8]")
+    if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
+        raise ValueError("enc_rmb_front_se: wdw [25, 1024] f32 and bias [1024] required")
+    H, C = w1.shape
+    if C != 512 or w2.shape != (512, H) or b1.numel() != H or b2.numel() != 512:
+        raise ValueError("enc_rmb_front_se: SE weights w1 [H, 512], b1 [H], w2 [512, H], b2 [512]")
+    M = X.shape[0]
+    R = M // 100
+    XRN = torch.empty((M, 1024), device=X.device, dtype=torch.bfloat16)
+    sums = (torch.empty((R, _lib.TRK_ENC_PARTS, 1024), device=X.device, dtype=torch.int64) if want_sums else None)
+    out = torch.empty((3, R, 512), device=X.device, dtype=torch.float32)
+    w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
+    check(lib().trk_enc_rmb_front_se(_ptr(X), M, _ptr(W1p), _ptr(wdw.contiguous()), _ptr(W2p),
+                                     _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(sums),
+                                     _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2), _ptr(out[0]), _ptr(out[1]),
+                                     _ptr(out[2]), _stream(X.device)), "enc_rmb_front_se")
+    return XRN, sums, out[0], out[1], out[2]
+
+
 def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.float32).contiguous()
 

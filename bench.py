@@ -429,7 +429,8 @@ class LiveProbe:
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_nchw_to_nhwc": "map_nhwc", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
              "trk_enc_transition_gemm2": "enc_gemm_trans",
-             "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_rmb_fused": "enc_rmb_fused",
+             "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_rmb_front_se": "enc_rmb_front",
+             "trk_enc_rmb_fused": "enc_rmb_fused",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
              "trk_step_begin": "step_begin", "trk_step_mid": "step_mid", "trk_step_end": "step_end",
@@ -749,6 +750,10 @@ def main():
     # encoder.Model's default
     if "TRK_FULL" in os.environ:
         model.fused_full = os.environ["TRK_FULL"] == "1"
+    # TRK_FRONT_SE=1/0: the SE inside the front kernel (enc_rmb_front_se) or its own enc_se
+    # launch; unset: encoder.Model's default
+    if "TRK_FRONT_SE" in os.environ:
+        model.front_se = os.environ["TRK_FRONT_SE"] == "1"
 
     # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
     # the syncs around the timed region make it do exactly `steps` embeddings (those of
@@ -895,7 +900,7 @@ def main():
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
     rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
-                     "se_deferred": pipe.defer_tail,
+                     "se_deferred": pipe.defer_tail, "se_in_front": bool(getattr(pipe.model, "front_se", False)),
                      "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
                      "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,

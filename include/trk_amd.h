@@ -262,6 +262,21 @@ int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const voi
  *   ROI's whole sum in partial 0 and 0 in its other partials. */
 int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                       const float* bias, void* XRN, long long* sums, void* stream);
+
+/* trk_enc_rmb_front + trk_enc_se in one launch (rf_v 3, the persistent front): every
+ * workgroup also writes its ROIs' squeeze means (m_r = mean SiLU(x_r) from the reinforce
+ * group, m_n = mean Hardswish(x_n) from the normal group, [R][512] f32, the bits trk_enc_se
+ * computes from the sums) and the reinforce-group workgroups then run the SE excitation
+ * s = hardsigmoid(W2 relu(W1 m_r + b1) + b2) over their ROIs in batches of 16 with
+ * trk_enc_se's arithmetic (bit-identical s).  Replaces the reference's SEBlock call after the
+ * DSC pair (model/utils/modules/card.py:59-78, 128-148).  sums may be NULL (not written);
+ * with rf_v 1 / 2 the call is the front followed by trk_enc_se (on sums, or on an internal
+ * workspace when NULL).  se_w1 [H][512], se_b1 [H], se_w2 [512][H], se_b2 [512] f32, H a
+ * multiple of 16 in [16, 512]. */
+int trk_enc_rmb_front_se(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                         const float* bias, void* XRN, long long* sums, const float* se_w1, const float* se_b1,
+                         int64_t H, const float* se_w2, const float* se_b2, float* m_r, float* m_n, float* s,
+                         void* stream);
 /* trk_enc_rmb_fused: trk_enc_rmb_front + trk_enc_se + trk_enc_transition_gemm in ONE kernel
  *   (10x10 ROIs, C = 512; card.py:28-78, :138-146).  A ROI's two workgroups hand data over
  *   through global memory and flags[roi][4] (= epoch once published): the normal group its

@@ -846,6 +846,49 @@ def _rmb_front_vs_two_kernel(gpu, R):
         ops.enc_rmb_front(X, W1p, wdw, W2.reshape(1024, 512), b2)
 
 
+@pytest.mark.parametrize("rf_v,groups,want_sums", [(3, 0, False), (3, 0, True), (3, 1, False), (3, 64, False),
+                                                   (2, 0, False), (2, 0, True)])
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_front_se_vs_front_then_se(trk, gpu, R, rf_v, groups, want_sums):
+    """trk_enc_rmb_front_se (the persistent front writing the squeeze means, its reinforce
+    workgroups then running the SE over their ROIs in batches of 16) vs trk_enc_rmb_front +
+    trk_enc_se: XRN, m_r, m_n and s bit-identical (the means are the bits enc_se takes from
+    the int64 sums; the SE runs enc_se's rb_linear tiles); the sums, when asked for, equal the
+    plain front's.  R = 1 / 37: batches of fewer than 16 rows; 1 pair per XCD: 256 ROIs and 16
+    SE batches per workgroup at R = 2048; rf_v 2: the two-launch path (own workspace when
+    want_sums is off)."""
+    from importlib import import_module
+    ops = import_module(trk.__name__ + ".ops")
+    L = trk.lib()
+    g = torch.Generator().manual_seed(100 + R)
+    X = torch.randn(R * 100, 512, generator=g).to(gpu).bfloat16()
+    W1p = ops.enc_pack_fragments((torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16())
+    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
+    W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16())
+    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
+    w1 = (torch.randn(128, 512, generator=g) / 20).to(gpu)
+    bb1 = (torch.randn(128, generator=g) / 10).to(gpu)
+    w2 = (torch.randn(512, 128, generator=g) / 10).to(gpu)
+    bb2 = (torch.randn(512, generator=g) / 10).to(gpu)
+    assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf3_groups", groups) == 0
+    try:
+        XRN0, sums0 = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+        m_r0, m_n0, s0 = ops.enc_se(sums0, 100, w1, bb1, w2, bb2)
+        XRN1, sums1, m_r1, m_n1, s1 = ops.enc_rmb_front_se(X, W1p, wdw, W2p, b2, w1, bb1, w2, bb2,
+                                                          want_sums=want_sums)
+        torch.cuda.synchronize()
+    finally:
+        L.trk_set_tuning(b"rf_v", 3)
+        L.trk_set_tuning(b"rf3_groups", 0)
+    assert torch.equal(XRN1, XRN0)
+    assert torch.equal(m_r1, m_r0) and torch.equal(m_n1, m_n0)
+    assert torch.equal(s1, s0)
+    if want_sums:  # (partials past a ROI's count are never written: compare what a reader reads)
+        assert torch.equal(ops.enc_sums_reduce(sums1, 100), ops.enc_sums_reduce(sums0, 100))
+    else:
+        assert sums1 is None
+
+
 @pytest.mark.parametrize("R", [1, 37, 2048])
 def test_enc_rmb_fused_vs_separate_kernels(trk, gpu, R):
     """trk_enc_rmb_fused (front + SE + transition in one kernel; the normal group hands its
