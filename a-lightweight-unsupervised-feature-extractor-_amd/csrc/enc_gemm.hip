@@ -3001,7 +3001,6 @@ int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw
 
 extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                                  const float* bias, void* XRN, long long* sums, void* stream) {
-  TRK_REQUIRE(sums, "enc_rmb_front: null sums");
   return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sums, nullptr, stream);
 }
 

@@ -91,3 +91,12 @@ def test_rmb_front_fragment_packing_and_argument_errors(trk):
     assert b"M % 100" in L.trk_last_error()
     assert L.trk_enc_rmb_front(None, 100, None, None, None, None, None, None, None) == -1
     assert L.trk_enc_rmb_front(None, 0, None, None, None, None, None, None, None) == 0
+    # trk_enc_rmb_front_se: the same front checks plus its SE operands (host-side, no launch)
+    v = ctypes.c_void_p(16)
+    assert L.trk_enc_rmb_front_se(None, 0, *([None] * 8), 128, *([None] * 6)) == 0
+    assert L.trk_enc_rmb_front_se(v, 150, *([v] * 8), 128, *([v] * 6)) == -1
+    assert b"M % 100" in L.trk_last_error()
+    assert L.trk_enc_rmb_front_se(v, 100, *([v] * 8), 120, *([v] * 6)) == -1
+    assert b"multiple of 16" in L.trk_last_error()
+    assert L.trk_enc_rmb_front_se(v, 100, *([v] * 8), 128, v, v, None, v, v, v, v) == -1
+    assert b"SE pointer" in L.trk_last_error()
