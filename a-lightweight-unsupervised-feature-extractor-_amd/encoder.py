@@ -237,9 +237,12 @@ class Model(nn.Module):
     fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel
                          # (enc_rmb_front; Y2 never reaches HBM); False: enc_g1_dwconv + enc_dsc_gemm
     fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
-    front_se = True      # with fused_front and fused_tail: the SE inside the front kernel (enc_rmb_front_se:
+    front_se = False     # with fused_front and fused_tail: the SE inside the front kernel (enc_rmb_front_se:
                          # the persistent front's reinforce workgroups run it over their ROIs; no sums
-                         # round trip, no enc_se launch)
+                         # round trip, no enc_se launch).  Measured r04: the front grows by the SE's
+                         # 36 us (two 16-row batches per workgroup) and the transition by 25 (the ROI
+                         # stage gated behind the front now lands on it alone): 2.011-2.021 vs
+                         # 2.029-2.058M ROIs/s, so off
     fused_full = False   # with fused_front and fused_tail: the SE and the transition GEMM inside the
                          # front kernel too (enc_rmb_fused; the [M, 1024] XRN never reaches HBM)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
