@@ -94,6 +94,10 @@ def _declare(L):
     L.trk_enc_rmb_front.restype = i32
     L.trk_enc_rmb_front_se.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, P, P, P]
     L.trk_enc_rmb_front_se.restype = i32
+    L.trk_enc_rmb_front_means.argtypes = [P, i64, P, P, P, P, P, P, P, P]
+    L.trk_enc_rmb_front_means.restype = i32
+    L.trk_enc_se_means.argtypes = [P, i64, i64, P, P, i64, P, P, P, P]
+    L.trk_enc_se_means.restype = i32
     L.trk_enc_rmb_fused.argtypes = [P, i64, P, P, P, P, P, P, P, P, P, P, P, P, i32, P, P, P, P, P]
     L.trk_enc_rmb_fused.restype = i32
     L.trk_enc_transition_gemm.argtypes = [P, i64, i64, i64, P, i64, P, P, i64, P, P]

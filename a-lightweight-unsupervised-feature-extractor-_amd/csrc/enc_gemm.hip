@@ -1218,7 +1218,7 @@ struct RfArgs {
   // front + SE (trk_enc_rmb_front_se, rf_v 3): each workgroup writes its ROIs' squeeze means
   // (group 0 m_r, group 1 m_n) and group 0 then runs the SE over its ROIs in batches of 16;
   // sums may be null (then not written)
-  int se_front, se_H;
+  int se_front, se_H;  // se_front 2 (trk_enc_rmb_front_means): the means only, no SE
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
@@ -2427,7 +2427,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   if constexpr (MODE != 2) break;
   }  // ROI loop
   if constexpr (MODE == 2 && G == 0) {
-    if (a.se_front) {
+    if (a.se_front == 1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's m_r rows are in
       g4_barrier();                                      // ... from every wave; LDS is free
       rf_se_batches(a, smem, roi0, stride);
@@ -2990,11 +2990,24 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
 }
 
 namespace {
-struct FrontSe {  // trk_enc_rmb_front_se's SE operands (null: the plain front)
+struct FrontSe {  // trk_enc_rmb_front_se's SE operands (null: the plain front; w1 null: the means only)
   const float *w1, *b1, *w2, *b2;
   int64_t H;
   float *m_r, *m_n, *s;
 };
+// grow-only device workspace of the two-launch fallbacks (rf_v 1 / 2)
+void* front_ws(size_t bytes) {
+  static void* ws = nullptr;
+  static size_t ws_n = 0;
+  if (bytes > ws_n) {
+    if (ws) (void)hipFree(ws);
+    ws = nullptr;
+    ws_n = 0;
+    if (hipMalloc(&ws, bytes) != hipSuccess) return nullptr;
+    ws_n = bytes;
+  }
+  return ws;
+}
 int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p, const float* bias,
                      void* XRN, long long* sums, const FrontSe* se, void* stream);
 }  // namespace
@@ -3022,20 +3035,36 @@ extern "C" int trk_enc_rmb_front_se(const void* X, int64_t M, const void* W1p, c
   // workspace when the caller passes none)
   long long* sp = sums;
   if (!sp) {
-    static long long* ws = nullptr;
-    static size_t ws_n = 0;
-    const size_t need = (size_t)(M / RF_S) * kPart * 1024;
-    if (need > ws_n) {
-      if (ws) (void)hipFree(ws);
-      ws = nullptr;
-      ws_n = 0;
-      TRK_REQUIRE(hipMalloc(&ws, need * sizeof(long long)) == hipSuccess, "enc_rmb_front_se: workspace allocation");
-      ws_n = need;
-    }
-    sp = ws;
+    sp = static_cast<long long*>(front_ws((size_t)(M / RF_S) * kPart * 1024 * sizeof(long long)));
+    TRK_REQUIRE(sp, "enc_rmb_front_se: workspace allocation");
   }
   if (int e = rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sp, nullptr, stream)) return e;
   return trk_enc_se(sp, M / RF_S, 1024, RF_S, 512, se_w1, se_b1, H, se_w2, se_b2, m_r, m_n, s, stream);
+}
+
+extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                                       const float* bias, void* XRN, float* m_r, float* m_n, void* stream) {
+  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front_means: 10x10 ROIs (M %% 100 == 0)");
+  if (M == 0) return TRK_OK;
+  TRK_REQUIRE(m_r && m_n && aligned16(m_r) && aligned16(m_n), "enc_rmb_front_means: null or unaligned m_r / m_n");
+  if (g_rf_v == 3) {
+    const FrontSe se{nullptr, nullptr, nullptr, nullptr, 0, m_r, m_n, nullptr};
+    return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, nullptr, &se, stream);
+  }
+  // the one-ROI-per-workgroup fronts: the front, then trk_enc_se's means phase on its sums (its
+  // s, into the workspace, is discarded)
+  const size_t nsum = (size_t)(M / RF_S) * kPart * 1024 * sizeof(long long);
+  char* ws = static_cast<char*>(front_ws(nsum + (size_t)(M / RF_S) * 512 * sizeof(float)));
+  TRK_REQUIRE(ws, "enc_rmb_front_means: workspace allocation");
+  long long* sp = reinterpret_cast<long long*>(ws);
+  if (int e = rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sp, nullptr, stream)) return e;
+  static float* zw = nullptr;  // a zero 16 x 512 SE (only the means are wanted)
+  if (!zw) {
+    TRK_REQUIRE(hipMalloc(&zw, (16 * 512 * 2 + 16 + 512) * sizeof(float)) == hipSuccess, "enc_rmb_front_means: alloc");
+    TRK_REQUIRE(hipMemset(zw, 0, (16 * 512 * 2 + 16 + 512) * sizeof(float)) == hipSuccess, "enc_rmb_front_means: alloc");
+  }
+  return trk_enc_se(sp, M / RF_S, 1024, RF_S, 512, zw, zw + 16 * 512 * 2, 16, zw + 16 * 512, zw + 16 * 512 * 2 + 16,
+                    m_r, m_n, reinterpret_cast<float*>(ws + nsum), stream);
 }
 
 namespace {
@@ -3074,7 +3103,7 @@ int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw
   a.sum_lanes = g_rf_sumlanes;
   a.dwprio = g_rf_dwprio;
   if (se) {
-    a.se_front = 1;
+    a.se_front = se->w1 ? 1 : 2;
     a.se_H = (int)se->H;
     a.se_w1 = se->w1; a.se_b1 = se->b1; a.se_w2 = se->w2; a.se_b2 = se->b2;
     a.m_r = se->m_r; a.m_n = se->m_n; a.s = se->s;

@@ -44,6 +44,7 @@ __device__ __forceinline__ float fix_mean(long long v, float P) {
 }
 
 struct SeArgs {
+  const float* means;  // trk_enc_se_means: m_r rows given (sums unused, m_r / m_n not written)
   const long long* sums;
   int64_t ld_sums;
   const float *w1, *b1, *w2, *b2;
@@ -66,7 +67,9 @@ __global__ void __launch_bounds__(64 * NW) enc_se_kernel(const SeArgs a) {
   for (int q = threadIdx.x; q < RB * C4; q += blockDim.x) {
     const int rr = q / C4, c = (q % C4) * 4;
     float4 mr = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rr < nrow) {
+    if (a.means) {
+      if (rr < nrow) mr = *reinterpret_cast<const float4*>(a.means + (r0 + rr) * C + c);
+    } else if (rr < nrow) {
       // the ROI's 1..3 partial sums (one per 128-row tile of the DSC GEMM)
       const int64_t roi = r0 + rr;
       const int cnt = part_count(roi, a.Pi);
@@ -243,6 +246,26 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
 
+namespace {
+int se_launch(const SeArgs& a, void* stream) {
+  const size_t lds = (size_t)RB * (ld_rows(a.C) + ld_rows(a.H)) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const unsigned nwg = (unsigned)((a.R + RB - 1) / RB);
+  if (g_se_waves == 16)
+    hipLaunchKernelGGL(enc_se_kernel<16>, dim3(nwg), dim3(64 * 16), lds, reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(enc_se_kernel<8>, dim3(nwg), dim3(64 * 8), lds, reinterpret_cast<hipStream_t>(stream), a);
+  return trk::check_launch("enc_se_kernel");
+}
+}  // namespace
+
 extern "C" int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int64_t P, int64_t C,
                           const float* w1, const float* b1, int64_t H, const float* w2, const float* b2,
                           float* m_r, float* m_n, float* s, void* stream) {
@@ -253,23 +276,19 @@ extern "C" int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int
   TRK_REQUIRE(sums && w1 && b1 && w2 && b2 && m_r && m_n && s, "enc_se: null pointer");
   TRK_REQUIRE(al16(sums) && al16(w1) && al16(w2) && al16(m_r) && al16(m_n) && al16(s),
               "enc_se: operands must be 16-byte aligned");
-  SeArgs a{sums, ld_sums, w1, b1, w2, b2, m_r, m_n, s, (int)R, (int)C, (int)H, (int)P, (float)P};
-  const size_t lds = (size_t)RB * (ld_rows((int)C) + ld_rows((int)H)) * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<8>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_se_kernel<16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  if (g_se_waves == 16)
-    hipLaunchKernelGGL(enc_se_kernel<16>, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * 16), lds,
-                       reinterpret_cast<hipStream_t>(stream), a);
-  else
-    hipLaunchKernelGGL(enc_se_kernel<8>, dim3((unsigned)((R + RB - 1) / RB)), dim3(64 * 8), lds,
-                       reinterpret_cast<hipStream_t>(stream), a);
-  return trk::check_launch("enc_se_kernel");
+  SeArgs a{nullptr, sums, ld_sums, w1, b1, w2, b2, m_r, m_n, s, (int)R, (int)C, (int)H, (int)P, (float)P};
+  return se_launch(a, stream);
+}
+
+extern "C" int trk_enc_se_means(const float* m_r, int64_t R, int64_t C, const float* w1, const float* b1, int64_t H,
+                                const float* w2, const float* b2, float* s, void* stream) {
+  TRK_REQUIRE(R >= 0 && C > 0 && C % 16 == 0 && C <= MAXC && H > 0 && H % 16 == 0 && H <= MAXC,
+              "enc_se_means: need C, H multiples of 16 in [16, %d]", MAXC);
+  if (R == 0) return TRK_OK;
+  TRK_REQUIRE(m_r && w1 && b1 && w2 && b2 && s, "enc_se_means: null pointer");
+  TRK_REQUIRE(al16(m_r) && al16(w1) && al16(w2) && al16(s), "enc_se_means: operands must be 16-byte aligned");
+  SeArgs a{m_r, nullptr, 0, w1, b1, w2, b2, nullptr, nullptr, s, (int)R, (int)C, (int)H, 1, 1.f};
+  return se_launch(a, stream);
 }
 
 extern "C" int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_t C, const float* s,

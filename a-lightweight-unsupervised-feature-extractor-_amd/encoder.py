@@ -243,6 +243,9 @@ class Model(nn.Module):
                          # 36 us (two 16-row batches per workgroup) and the transition by 25 (the ROI
                          # stage gated behind the front now lands on it alone): 2.011-2.021 vs
                          # 2.029-2.058M ROIs/s, so off
+    front_means = True   # with fused_front and fused_tail (front_se off): the front writes the squeeze means
+                         # (enc_rmb_front_means) and the SE reads them (enc_se_means) -- no int64 sums
+                         # round trip, no means phase in the SE
     fused_full = False   # with fused_front and fused_tail: the SE and the transition GEMM inside the
                          # front kernel too (enc_rmb_fused; the [M, 1024] XRN never reaches HBM)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
@@ -254,8 +257,8 @@ class Model(nn.Module):
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
         from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_rmb_front, enc_rmb_front_se, enc_rmb_fused, enc_transition_gemm, enc_se, enc_head,
-                          enc_sums_reduce)
+                          enc_rmb_front, enc_rmb_front_se, enc_rmb_front_means, enc_rmb_fused, enc_transition_gemm,
+                          enc_se, enc_se_means, enc_head, enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -285,6 +288,12 @@ class Model(nn.Module):
             if self.stage_hook is not None:
                 self.stage_hook("g1")
                 self.stage_hook("dsc")
+        elif front and self.fused_tail and self.front_means and not (self.defer_tail and self.se_stream is not None):
+            XRN, m_r, m_n = enc_rmb_front_means(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
+            if self.stage_hook is not None:
+                self.stage_hook("g1")
+                self.stage_hook("dsc")
+            se_out = (m_r, m_n, enc_se_means(m_r, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"]))
         elif front:
             XRN, sums = enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
             if self.stage_hook is not None:

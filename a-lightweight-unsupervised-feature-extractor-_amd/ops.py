@@ -337,6 +337,48 @@ def enc_rmb_front_se(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p:
     return XRN, sums, out[0], out[1], out[2]
 
 
+def enc_rmb_front_means(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
+                        bias: torch.Tensor):
+    """enc_rmb_front writing the squeeze means instead of the raw sums
+    (trk_enc_rmb_front_means): returns (XRN, m_r, m_n) -- m_r / m_n bit-identical to
+    enc_se's on enc_rmb_front's sums."""
+    _need_gpu(X, "enc_rmb_front_means")
+    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
+        raise TypeError("enc_rmb_front_means: bf16 operands required")
+    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
+        raise ValueError("enc_rmb_front_means: X must be contiguous [R*100, 512]")
+    pk = (2, 16, 32, 4, 16, 8)
+    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or not (W1p.is_contiguous() and W2p.is_contiguous()):
+        raise ValueError("enc_rmb_front_means: W1p / W2p must be enc_pack_fragments output [2, 16, 32, 4, 16, 8]")
+    if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
+        raise ValueError("enc_rmb_front_means: wdw [25, 1024] f32 and bias [1024] required")
+    M = X.shape[0]
+    XRN = torch.empty((M, 1024), device=X.device, dtype=torch.bfloat16)
+    m = torch.empty((2, M // 100, 512), device=X.device, dtype=torch.float32)
+    check(lib().trk_enc_rmb_front_means(_ptr(X), M, _ptr(W1p), _ptr(wdw.contiguous()), _ptr(W2p),
+                                        _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(m[0]), _ptr(m[1]),
+                                        _stream(X.device)), "enc_rmb_front_means")
+    return XRN, m[0], m[1]
+
+
+def enc_se_means(m_r: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor):
+    """SE excitation from given squeeze means (trk_enc_se_means): s [R, C] f32, bit-identical
+    to enc_se's s for the same m_r (card.py:59-78)."""
+    _need_gpu(m_r, "enc_se_means")
+    if m_r.dtype != torch.float32 or m_r.dim() != 2:
+        raise TypeError("enc_se_means: m_r must be [R, C] f32")
+    H, C = w1.shape
+    R = m_r.shape[0]
+    if m_r.shape[1] != C or w2.shape != (C, H) or b1.numel() != H or b2.numel() != C:
+        raise ValueError("enc_se_means: shape mismatch")
+    m_r = m_r.contiguous()
+    s = torch.empty((R, C), device=m_r.device, dtype=torch.float32)
+    w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
+    check(lib().trk_enc_se_means(_ptr(m_r), R, C, _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2), _ptr(s),
+                                 _stream(m_r.device)), "enc_se_means")
+    return s
+
+
 def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.float32).contiguous()
 

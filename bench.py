@@ -430,6 +430,7 @@ class LiveProbe:
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
              "trk_enc_transition_gemm2": "enc_gemm_trans",
              "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_rmb_front_se": "enc_rmb_front",
+             "trk_enc_rmb_front_means": "enc_rmb_front", "trk_enc_se_means": "enc_se",
              "trk_enc_rmb_fused": "enc_rmb_fused",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
@@ -754,6 +755,10 @@ def main():
     # launch; unset: encoder.Model's default
     if "TRK_FRONT_SE" in os.environ:
         model.front_se = os.environ["TRK_FRONT_SE"] == "1"
+    # TRK_FRONT_MEANS=1/0: the front writes the squeeze means for enc_se_means, or the int64
+    # sums for enc_se; unset: encoder.Model's default
+    if "TRK_FRONT_MEANS" in os.environ:
+        model.front_means = os.environ["TRK_FRONT_MEANS"] == "1"
 
     # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
     # the syncs around the timed region make it do exactly `steps` embeddings (those of
@@ -901,6 +906,7 @@ def main():
                  if os.environ.get(k) is not None}
     rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
                      "se_deferred": pipe.defer_tail, "se_in_front": bool(getattr(pipe.model, "front_se", False)),
+                     "front_means": bool(getattr(pipe.model, "front_means", False)) and not getattr(pipe.model, "front_se", False),
                      "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
                      "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,

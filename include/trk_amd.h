@@ -277,6 +277,13 @@ int trk_enc_rmb_front_se(const void* X, int64_t M, const void* W1p, const float*
                          const float* bias, void* XRN, long long* sums, const float* se_w1, const float* se_b1,
                          int64_t H, const float* se_w2, const float* se_b2, float* m_r, float* m_n, float* s,
                          void* stream);
+
+/* trk_enc_rmb_front writing the ROI squeeze means instead of the int64 sums: m_r / m_n
+ * [R][512] f32, the bits trk_enc_se derives from the sums (rf_v 3: from the kernel's own
+ * column sums, no sums round trip; rf_v 1 / 2: the front, then trk_enc_se's means phase on
+ * an internal workspace).  Pair with trk_enc_se_means. */
+int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
+                            const float* bias, void* XRN, float* m_r, float* m_n, void* stream);
 /* trk_enc_rmb_fused: trk_enc_rmb_front + trk_enc_se + trk_enc_transition_gemm in ONE kernel
  *   (10x10 ROIs, C = 512; card.py:28-78, :138-146).  A ROI's two workgroups hand data over
  *   through global memory and flags[roi][4] (= epoch once published): the normal group its
@@ -317,6 +324,11 @@ int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, int64_t K, c
 int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int64_t P, int64_t C, const float* w1,
                const float* b1, int64_t H, const float* w2, const float* b2, float* m_r, float* m_n, float* s,
                void* stream);
+
+/* trk_enc_se's excitation from given squeeze means: s = hardsigmoid(W2 relu(W1 m_r + b1) + b2)
+ * [R][C] f32, bit-identical to trk_enc_se's s for the same m_r (card.py:59-78). */
+int trk_enc_se_means(const float* m_r, int64_t R, int64_t C, const float* w1, const float* b1, int64_t H,
+                     const float* w2, const float* b2, float* s, void* stream);
 int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_t C, const float* s, const float* m_r,
                  const float* m_n, double alpha, const float* w0, const float* ln_w, const float* ln_b,
                  float ln_eps, const float* w4, const float* b4, int64_t D, float* out, void* stream);

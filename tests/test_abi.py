@@ -100,3 +100,10 @@ def test_rmb_front_fragment_packing_and_argument_errors(trk):
     assert b"multiple of 16" in L.trk_last_error()
     assert L.trk_enc_rmb_front_se(v, 100, *([v] * 8), 128, v, v, None, v, v, v, v) == -1
     assert b"SE pointer" in L.trk_last_error()
+    assert L.trk_enc_rmb_front_means(None, 0, *([None] * 8)) == 0
+    assert L.trk_enc_rmb_front_means(v, 150, *([v] * 8)) == -1
+    assert b"M % 100" in L.trk_last_error()
+    assert L.trk_enc_rmb_front_means(v, 100, *([v] * 5), None, v, v) == -1
+    assert L.trk_enc_se_means(None, 0, 512, None, None, 128, None, None, None, None) == 0
+    assert L.trk_enc_se_means(v, 4, 512, v, v, 120, v, v, v, v) == -1
+    assert b"multiples of 16" in L.trk_last_error()

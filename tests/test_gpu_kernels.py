@@ -889,6 +889,40 @@ def test_enc_rmb_front_se_vs_front_then_se(trk, gpu, R, rf_v, groups, want_sums)
         assert sums1 is None
 
 
+@pytest.mark.parametrize("rf_v,groups", [(3, 0), (3, 1), (2, 0)])
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_front_means_and_se_means(trk, gpu, R, rf_v, groups):
+    """trk_enc_rmb_front_means (the front writing the squeeze means instead of the int64 sums)
+    + trk_enc_se_means (the excitation from those means) vs trk_enc_rmb_front + trk_enc_se:
+    XRN, m_r, m_n and s bit-identical.  rf_v 2: the front + enc_se's means phase on a workspace."""
+    from importlib import import_module
+    ops = import_module(trk.__name__ + ".ops")
+    L = trk.lib()
+    g = torch.Generator().manual_seed(200 + R)
+    X = torch.randn(R * 100, 512, generator=g).to(gpu).bfloat16()
+    W1p = ops.enc_pack_fragments((torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16())
+    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
+    W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16())
+    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
+    w1 = (torch.randn(128, 512, generator=g) / 20).to(gpu)
+    bb1 = (torch.randn(128, generator=g) / 10).to(gpu)
+    w2 = (torch.randn(512, 128, generator=g) / 10).to(gpu)
+    bb2 = (torch.randn(512, generator=g) / 10).to(gpu)
+    assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf3_groups", groups) == 0
+    try:
+        XRN0, sums0 = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+        m_r0, m_n0, s0 = ops.enc_se(sums0, 100, w1, bb1, w2, bb2)
+        XRN1, m_r1, m_n1 = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        s1 = ops.enc_se_means(m_r1, w1, bb1, w2, bb2)
+        torch.cuda.synchronize()
+    finally:
+        L.trk_set_tuning(b"rf_v", 3)
+        L.trk_set_tuning(b"rf3_groups", 0)
+    assert torch.equal(XRN1, XRN0)
+    assert torch.equal(m_r1, m_r0) and torch.equal(m_n1, m_n0)
+    assert torch.equal(s1, s0)
+
+
 @pytest.mark.parametrize("R", [1, 37, 2048])
 def test_enc_rmb_fused_vs_separate_kernels(trk, gpu, R):
     """trk_enc_rmb_fused (front + SE + transition in one kernel; the normal group hands its
