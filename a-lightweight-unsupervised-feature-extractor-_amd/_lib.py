@@ -84,22 +84,14 @@ def _declare(L):
     L.trk_scale_rows.restype = i32
     L.trk_act_scale_rows.argtypes = [P, P, i64, i64, i64, i64, i32, i32, P]
     L.trk_act_scale_rows.restype = i32
-    L.trk_enc_gemm.argtypes = [P, i64, i64, i64, P, i64, P, i64, P]
-    L.trk_enc_gemm.restype = i32
     L.trk_enc_g1_dwconv.argtypes = [P, i64, P, i64, P, P, P]
     L.trk_enc_g1_dwconv.restype = i32
     L.trk_enc_dsc_gemm.argtypes = [P, i64, i64, i64, P, P, i64, P, P, P]
     L.trk_enc_dsc_gemm.restype = i32
-    L.trk_enc_rmb_front.argtypes = [P, i64, P, P, P, P, P, P, P]
-    L.trk_enc_rmb_front.restype = i32
-    L.trk_enc_rmb_front_se.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, P, P, P]
-    L.trk_enc_rmb_front_se.restype = i32
     L.trk_enc_rmb_front_means.argtypes = [P, i64, P, P, P, P, P, P, P, P]
     L.trk_enc_rmb_front_means.restype = i32
     L.trk_enc_se_means.argtypes = [P, i64, i64, P, P, i64, P, P, P, P]
     L.trk_enc_se_means.restype = i32
-    L.trk_enc_rmb_fused.argtypes = [P, i64, P, P, P, P, P, P, P, P, P, P, P, P, i32, P, P, P, P, P]
-    L.trk_enc_rmb_fused.restype = i32
     L.trk_enc_transition_gemm.argtypes = [P, i64, i64, i64, P, i64, P, P, i64, P, P]
     L.trk_enc_transition_gemm.restype = i32
     L.trk_enc_transition_gemm2.argtypes = [P, i64, i64, i64, P, i64, P, P, P, i64, P, P]
@@ -175,7 +167,7 @@ def lib():
                         "or __graft_entry__.build() (there is no CPU fallback)")
                 L = ctypes.CDLL(LIB_PATH)
                 _declare(L)
-                if L.trk_abi_version() != 1:
+                if L.trk_abi_version() != 2:
                     raise TrkError("libtrk_amd ABI version mismatch")
                 # TRK_TUNE="key=value,..." applies trk_set_tuning knobs at load (A/B runs)
                 for kv in filter(None, os.environ.get("TRK_TUNE", "").split(",")):

@@ -1,104 +1,38 @@
 // bf16 GEMMs of the encoder (reference model/utils/modules/card.py: DSC :48-57,
 // SEBlock :73-78, RMB.forward :128-148) for gfx950, with the elementwise work
-// of the eval graph fused into their prologues / epilogues.
-//
-// C = A . B^T on MFMA 32x32x16 bf16 (f32 accumulate): A = activation rows
-// [M, K] (row stride lda), B = weights [N, K] (the conv weight's [out, in]
-// layout, K contiguous).  Workgroup tile 256 x 256, BK = 32, 8 waves as
-// 2 (M) x 4 (N), each wave 128 x 64 (4 x 2 accumulators): 0.75 KB of LDS
-// fragment reads per MFMA, inside the ~1 KB / 32-cycle MFMA the CU's LDS
-// delivers (64 x 32 wave tiles were LDS-bound at 1.5 KB).
-//
-// K loop: operands are staged with LDS-DMA (global_load_lds, 16 B per lane)
-// into a three-stage LDS ring; the wave writes its 1 KB lane-linearly and the XOR
-// swizzle of the image is applied to the per-lane SOURCE address (chunk c of
-// row r at position r*4 + (c ^ ((r >> 2) & 3))), so the 16-B fragment reads of
-// 16 consecutive rows hit 16 distinct bank groups.  Two K steps stay in flight
-// (counted vmcnt + raw s_barrier); no staging registers.
-//
-// Epilogue:
-//   * per-ROI column sums of the activation straight from the accumulators
-//     (lane = column, registers = rows; a 32-row tile spans <= 2 ROIs since
-//     P >= 32), as int64 fixed point (x 2^24) in LDS, then one 64-bit global
-//     atomic per (ROI, column): integer adds, so the sums are identical
-//     whatever order tiles finish in;
-//   * stores through an f32 LDS block [64][264] (row stride chosen so the two
-//     lane halves of a write hit disjoint banks) as 16-B bf16 vectors.
-// Variants:
-//   EPI_DSC   both DSC 1x1 GEMMs (group 0 = reinforce, 1 = normal) + BN-folded
-//             bias; stores SiLU(x_r) / Hardswish(x_n) into the [x_r | x_n]
-//             rows; sums SiLU(x_r) (SE squeeze) / Hardswish(x_n) (GAP).
-//   EPI_TRANS transition: the SE excitation (x_r * s[roi]) is applied in LDS to
-//             the staged A tiles of the first kscale columns; + bias, sums
-//             SiLU(T); T is never stored.
-//   EPI_PLAIN plain bf16 store (the four first 1x1 convs as one GEMM).
+// of the eval graph fused into their prologues / epilogues.  All on MFMA
+// 16x16x32 bf16 with f32 accumulation:
+//   rmb_front3 (trk_enc_rmb_front_means, the default front): per 10x10 ROI and DSC
+//             group, the first 1x1 convs + depthwise 5x5 + the DSC 1x1 GEMM + BN +
+//             activation, Y1 / Y2 only in LDS; writes [x_r | x_n] rows and the SE's
+//             squeeze means.  A persistent grid, two workgroups per ROI on one XCD.
+//   g1dw4 + gemm4<EPI_DSC> (trk_enc_g1_dwconv + trk_enc_dsc_gemm): the same front as two
+//             kernels with Y2 in HBM (the alternative the front's tests compare against).
+//   trans4 / gemm4<EPI_TRANS> (trk_enc_transition_gemm2): the SE excitation applied to
+//             the staged x_f tiles, the transition GEMM + bias + SiLU and the per-ROI
+//             sums of SiLU(T); T is never stored.  trans4 reads its weights straight
+//             into VGPRs as pre-packed fragments; gemm4 streams them through LDS.
+// Per-ROI sums leave the GEMMs as int64 fixed point (x 2^24) partials written with plain
+// stores, so they do not depend on the order tiles finish in.
 #include "trk_common.h"
 #include "rb_linear.h"
 
 #include <utility>
 
-unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: gemm8 / gemm4 phase stamps)
-int g_enc_gemm = 1;  // trk_set_tuning("enc_gemm"): 1 = gemm4 (default), 0 = the 128 x 128 / 128 x 256 kernels
-int g_enc_lds_tight = 1;  // trk_set_tuning("enc_lds_tight"): gemm4 launched with the LDS its tile uses (1) or 80 KiB
-int g_enc_sums = 1;  // trk_set_tuning("enc_sums"): 1 = gemm4's per-ROI column sums on the MFMA (DSC
-                     // 355 vs 364 us, transition 279 vs 281; bf16 hi only: 344 / 275 but 5e-4 off), 0 = lane sums
-int g_rf_pf = 8;  // trk_set_tuning("rf_pf"): rmb_front's L2 prefetch of the X rows of ROI + rf_pf, 0: none (GEMM1
-                  // 19-20K vs 26.8K cycles per workgroup without it; XRN non-temporal stores: no change)
-int g_rf_lag = 16;  // trk_set_tuning("rf_lag"): rmb_front rf_v 2, K steps half A runs ahead in GEMM1
-int g_rf3_pf = 0;  // trk_set_tuning("rf3_pf"): rf_v 3 L2 prefetch of the workgroup's next ROI (0: off --
-                  // its X DMA already starts under this ROI's epilogue; 537 vs 597 MB fetched per
-                  // launch, the pipeline ahead in 4 of 4 interleaved pairs)
-int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rf_v 3 workgroup pairs per XCD (0 = CUs / 16 - 2)
-int g_rf_v = 3;  // trk_set_tuning("rf_v"): rmb_front body, 3 = persistent rf_v 2, 2 = decoupled halves,
-                 // 1 = lockstep phases
-int g_rf_dwprio = 0;  // trk_set_tuning("rf_dwprio"): rf2's depthwise at priority 2: 0 none, 1 half B, 2 both
-int g_rf_sumlanes = 1;  // trk_set_tuning("rf_sumlanes"): rf2's ROI sums one channel per lane (1, default: the
-                        // activation + sums phase 10.6K vs 12.1K cycles per wave, 569 vs 582 us isolated, pipeline
-                        // 1.998/1.993/1.996M vs 1.964/2.001/2.017M -- rule (b)) or 16 per lane fr == 0 (0)
+unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: per-workgroup phase stamps)
+int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rmb_front3 workgroup pairs per XCD (0 = CUs / 16 - 2)
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
-int g_t4_mode = 5;  // trk_set_tuning("t4_mode"): trans4 pipeline (K steps per LDS stage, B distance):
-                    // 0 = (1, 2), 1 = (2, 2), 2 = (1, 3), 3 = (2, 3); 4..6 = (1, 2) + setprio / mid-step issue /
-                    // both; 7 = (2, 3) + both; 8 / 9 = mid-step issue + counted fragment reads at (1, 2) /
-                    // (2, 3).  Isolated medians (tools/exp/trans_ab.py): 244.1, 240.0 (3),
-                    // 248.7 (4), 235.4 (5), 241.3 (6), 245.0 (7) us; pipeline 5 vs 0 in three interleaved pairs
-                    // 1.983/1.990/1.952M vs 1.954/1.954/1.942M ROIs/s: 5 (mid-step issue) is the default
-int g_enc_trans_wide = 0;  // trk_set_tuning("enc_trans_wide"): 1 = gemm4's transition on 256 x 256 tiles (8
-                           // waves, one workgroup per CU; P >= 86; 301 vs 282 us isolated, pipeline 2 of 3 pairs
-                           // lost: kept as a tested variant), 0 = 128 x 256 tiles, two workgroups per CU
-int g_g1dw = 6;      // trk_set_tuning("g1dw"): 6 = g1dw4 + next-round A prefetch (default), 4 = without it
 
 namespace {
 
-typedef __bf16 bf8_t __attribute__((ext_vector_type(8)));
-typedef float f16_t __attribute__((ext_vector_type(16)));
 #define GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-enum { EPI_DSC = 0, EPI_TRANS = 1, EPI_PLAIN = 2 };
+enum { EPI_DSC = 0, EPI_TRANS = 1 };
 
 constexpr int BK = 32;
-constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
-constexpr int NSTAGE = 3;                   // LDS-DMA ring: two K steps in flight
-constexpr int EROWS = 64;                   // rows per epilogue store block
-
-// Tile configuration: workgroup BM x BN, 8 waves as 2 (M) x 4 (N).  Measured
-// per variant (M = 204800, K = 512 / 1024): 256 x 256 (wave 128 x 64, 0.75 KB of
-// LDS fragment reads per MFMA) for the plain GEMM; 128 x 256 (wave 64 x 64) for
-// the transition; 128 x 128 (wave 64 x 32) for the DSC pair, whose store +
-// activation epilogue overlaps best with 3 workgroups per CU.
-template <int BM_, int BN_>
-struct Tile {
-  static constexpr int BM = BM_, BN = BN_;
-  static constexpr int WM = BM / 2, WN = BN / 4, TM = WM / 32, TN = WN / 32;
-  static constexpr int AI = BM * CPR / 512, BI = BN * CPR / 512;  // DMA ops per thread per stage
-  static constexpr int TLD = BN + 8;                               // epilogue block row stride (floats)
-  static constexpr int kSlots = BM / 32 + 1;                       // ROIs a tile can touch (P >= 32)
-  static constexpr size_t kStageBytes = NSTAGE * (size_t)(BM + BN) * CPR * 16;
-  static constexpr size_t kEpiBytes = (size_t)EROWS * TLD * 4 + (size_t)kSlots * BN * 8;
-  static constexpr size_t kLds = kStageBytes > kEpiBytes ? kStageBytes : kEpiBytes;
-};
 constexpr float kFix = 16777216.0f;         // 2^24
 // per-ROI sums leave the GEMMs as int64 partials, one per 128-row M tile that
 // covers the ROI (<= 3 for P <= 256), written with plain stores (no atomics,
@@ -121,14 +55,6 @@ struct EncGemmArgs {
   unsigned long long* prof;  // trk_enc_set_prof (gemm4: per-workgroup phase stamps; diagnostics)
 };
 
-// bf16-path activations: hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32), a
-// few ulp of f32 -- far below the bf16 rounding these kernels feed
-__device__ __forceinline__ float silu_f(float v) {
-  return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * v));
-}
-__device__ __forceinline__ float hswish_f(float v) {
-  return v * fminf(fmaxf(v + 3.0f, 0.0f), 6.0f) * (1.0f / 6.0f);
-}
 __device__ __forceinline__ unsigned long long eg_stamp() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -137,21 +63,10 @@ __device__ __forceinline__ unsigned long long eg_stamp() {
   return t;
 }
 
-// cross-lane exchanges without the LDS pipe (ds_bpermute): DPP quad_perm for lane ^ 1,
-// gfx950's v_permlane16/32_swap for the half-row / half-wave sums; a + b in either
-// order, so the sums equal x + __shfl_xor(x, 16 / 32) bit for bit
+// lane ^ 1 without the LDS pipe (ds_bpermute): DPP quad_perm
 __device__ __forceinline__ float lane_xor1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // quad_perm [1,0,3,2]
 }
-__device__ __forceinline__ float sum_xor16(float v) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float sum_xor32(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
 __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
   const int64_t nx = 8;
   if (nwg < nx) return bid;
@@ -160,270 +75,10 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
   return base + bid / nx;
 }
 
-// chunk c (of CPR = 4) of row r lives at r*4 + (c ^ ((r >> 2) & 3)): 16 consecutive
-// rows of one chunk land in 16 distinct 16-B bank groups
 typedef float dw_pair_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ int swz(int r, int c) { return r * CPR + (c ^ ((r >> 2) & 3)); }
-__device__ __forceinline__ int unswz_c(int p) { return (p % CPR) ^ (((p / CPR) >> 2) & 3); }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return trk::pack2_bf16(a, b);
-}
-
-template <int EPI, int BM_, int BN_>
-__global__ void __launch_bounds__(512) enc_gemm_kernel(EncGemmArgs a) {
-  using T = Tile<BM_, BN_>;
-  constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, TM = T::TM, TN = T::TN;
-  constexpr int AI = T::AI, BI = T::BI, TLD = T::TLD, kSlots = T::kSlots;
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint4* As = reinterpret_cast<uint4*>(smem);  // [NSTAGE][BM * CPR]
-  uint4* Bs = As + NSTAGE * BM * CPR;           // [NSTAGE][BN * CPR]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int ntile_n = a.N / BN;
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = (int)(lb % (ntile_n * a.groups));
-  const int64_t mt = lb / (ntile_n * a.groups);
-  const int g = nt / ntile_n, n0 = (nt % ntile_n) * BN;
-  const int64_t m0 = mt * BM;
-  const uint16_t* Ag = a.A + (int64_t)g * a.K;  // group g's K columns of the A rows
-  const uint16_t* Bg = a.B + (int64_t)g * a.N * a.K;
-
-  // LDS-DMA sources: the lane writes LDS position (wave*AI + q)*64 + lane, which
-  // holds (row, chunk) = inverse swizzle of that position
-  const uint16_t* asrc[AI];
-  const uint16_t* bsrc[BI];
-#pragma unroll
-  for (int q = 0; q < AI; ++q) {
-    const int p = (wave * AI + q) * 64 + lane, r = p / CPR, c = unswz_c(p);
-    const int64_t row = min(m0 + r, (int64_t)a.M - 1);  // clamp: rows >= M are never stored
-    asrc[q] = Ag + row * a.lda + c * 8;
-  }
-#pragma unroll
-  for (int q = 0; q < BI; ++q) {
-    const int p = (wave * BI + q) * 64 + lane, r = p / CPR, c = unswz_c(p);
-    bsrc[q] = Bg + (int64_t)(n0 + r) * a.K + c * 8;
-  }
-  auto issue = [&](int stage, int k0) {
-#pragma unroll
-    for (int q = 0; q < AI; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + k0), LPTR(As + stage * BM * CPR + (wave * AI + q) * 64), 16,
-                                       0, 0);
-#pragma unroll
-    for (int q = 0; q < BI; ++q)
-      __builtin_amdgcn_global_load_lds(GPTR(bsrc[q] + k0), LPTR(Bs + stage * BN * CPR + (wave * BI + q) * 64), 16,
-                                       0, 0);
-  };
-  // EPI_TRANS: x_r * s[roi] on a staged A tile whose K range is < kscale.  The
-  // thread's s values for step k are loaded during step k-1 (sv registers), so
-  // the transform never waits on a global load.
-  constexpr int TPT = BM * CPR / 512;  // A pieces per thread per step
-  float4 sv[TPT][2];
-  auto sload = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < TPT; ++q) {
-      const int p = tid + 512 * q, r = p / CPR, c = unswz_c(p);
-      const int64_t row = min(m0 + r, (int64_t)a.M - 1);
-      const float* sp = a.scale + (row / a.P) * a.kscale + k0 + c * 8;
-      sv[q][0] = *reinterpret_cast<const float4*>(sp);
-      sv[q][1] = *reinterpret_cast<const float4*>(sp + 4);
-    }
-  };
-  auto transform = [&](int stage) {
-    uint4* as = As + stage * BM * CPR;
-#pragma unroll
-    for (int q = 0; q < TPT; ++q) {
-      const int p = tid + 512 * q;
-      const float s8[8] = {sv[q][0].x, sv[q][0].y, sv[q][0].z, sv[q][0].w,
-                           sv[q][1].x, sv[q][1].y, sv[q][1].z, sv[q][1].w};
-      uint4 v = as[p];
-      uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x0 = __uint_as_float(w[e] << 16), x1 = __uint_as_float(w[e] & 0xffff0000u);
-        w[e] = pack_bf16x2(x0 * s8[2 * e], x1 * s8[2 * e + 1]);
-      }
-      as[p] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-  };
-
-  f16_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // K loop over an NSTAGE ring.  Each stage is 2 LDS-DMA ops per thread
-  // (AI + BI); waiting for stage kt while stage kt+1 stays in flight is a
-  // counted vmcnt(AI + BI), and the barrier is a raw s_barrier (__syncthreads would
-  // drain every DMA in flight with vmcnt(0), MI355X guide "glds ... across a
-  // barrier").  Stage (kt+2) % 3 is refilled right after the barrier of step
-  // kt: every wave has finished reading it (step kt-1) by then.
-  static_assert(AI + BI >= 2 && AI + BI <= 4, "vmcnt immediates below assume 2..4 DMA ops per stage");
-  const int nk = a.K / BK;
-  issue(0, 0);
-  if (nk > 1) issue(1, BK);
-  if (EPI == EPI_TRANS && a.kscale > 0) sload(0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int st = kt % NSTAGE;
-    if (kt + 1 < nk) {
-      if constexpr (AI + BI == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if constexpr (AI + BI == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (EPI == EPI_TRANS && kt * BK < a.kscale) {
-      transform(st);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    if (kt + 2 < nk) issue((kt + 2) % NSTAGE, (kt + 2) * BK);
-    if (EPI == EPI_TRANS && (kt + 1) * BK < a.kscale) sload((kt + 1) * BK);
-    const uint4* as = As + st * BM * CPR;
-    const uint4* bs = Bs + st * BN * CPR;
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int c = ks * 2 + (lane >> 5);
-      bf8_t bfr[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf8_t*>(&bs[swz(wn * WN + j * 32 + (lane & 31), c)]);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bf8_t af = *reinterpret_cast<const bf8_t*>(&as[swz(wm * WM + i * 32 + (lane & 31), c)]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
-      }
-    }
-  }
-  __syncthreads();  // all LDS reads of the ring done before the epilogue reuses it
-
-  // ---- epilogue
-  float* tile = reinterpret_cast<float*>(smem);                                                  // [EROWS][TLD]
-  unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + (size_t)EROWS * TLD * 4);  // [kSlots][BN]
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int cl = wn * WN + j * 32 + (lane & 31);
-    const float bv = a.bias ? a.bias[g * a.N + n0 + cl] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        // the activation, once: both the ROI sums and the stores use it
-        const float v = acc[i][j][r] + bv;
-        acc[i][j][r] = EPI == EPI_PLAIN ? v : (EPI == EPI_DSC && g == 1) ? hswish_f(v) : silu_f(v);
-      }
-  }
-
-  if (EPI != EPI_PLAIN) {
-    // per-ROI column sums of the activation from the registers (lane = column,
-    // registers = 16 rows of a 32-row tile; <= 2 ROI segments per tile)
-    for (int q = tid; q < kSlots * BN; q += 512) red[q] = 0ull;
-    __syncthreads();
-    const int64_t roi_base = m0 / a.P;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cl = wn * WN + j * 32 + (lane & 31);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int64_t r0 = m0 + wm * WM + i * 32;
-        const int64_t roi0 = r0 / a.P;
-        const int64_t split = (roi0 + 1) * a.P;
-        float s_lo = 0.f, s_hi = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = r0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const float act = acc[i][j][r];
-          if (row < a.M) {
-            if (row < split) s_lo += act;
-            else s_hi += act;
-          }
-        }
-        s_lo = sum_xor32(s_lo);
-        s_hi = sum_xor32(s_hi);
-        if (lane < 32 && r0 < a.M) {
-          const int slot = (int)(roi0 - roi_base);
-          atomicAdd(&red[slot * BN + cl], (unsigned long long)llrintf(s_lo * kFix));
-          if (split < r0 + 32 && split < a.M)
-            atomicAdd(&red[(slot + 1) * BN + cl], (unsigned long long)llrintf(s_hi * kFix));
-        }
-      }
-    }
-    __syncthreads();
-    const int64_t last_row = min(m0 + BM, (int64_t)a.M) - 1;
-    const int nslot = (int)(last_row / a.P - roi_base) + 1;
-    for (int q = tid; q < nslot * BN; q += 512) {
-      const int slot = q / BN, c = q % BN;
-      const int64_t roi = roi_base + slot;
-      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);  // this tile among the ROI's tiles
-      a.sums[(roi * kPart + j) * a.ld_sums + g * a.N + n0 + c] = (long long)red[q];
-    }
-  }
-  if (EPI == EPI_TRANS) return;
-
-  // stores: 64-row blocks through the f32 LDS tile, then 16-B bf16 vectors per
-  // thread (coalesced rows).  Block h holds rows [64h, 64h + 64): wave row-group
-  // wm = h / (WM / 64), its accumulator tiles i = 2 (h % (WM / 64)) .. + 1.
-  constexpr int HPW = WM / EROWS;  // store blocks per wave row-group
-  const int64_t cbase = (int64_t)(EPI == EPI_DSC ? g * a.N : 0) + n0;
-#pragma unroll
-  for (int h = 0; h < BM / EROWS; ++h) {
-    if (wm == h / HPW) {
-#pragma unroll
-      for (int i2 = 0; i2 < 2; ++i2) {
-        const int i = 2 * (h % HPW) + i2;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int cl = wn * WN + j * 32 + (lane & 31);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = i2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            tile[rl * TLD + cl] = acc[i][j][r];
-          }
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < EROWS * BN / 8 / 512; ++q) {
-      const int p = tid + 512 * q, rl = p / (BN / 8), c8 = (p % (BN / 8)) * 8;
-      const int64_t row = m0 + h * EROWS + rl;
-      if (row < a.M) {
-        const float4 v0 = *reinterpret_cast<const float4*>(&tile[rl * TLD + c8]);
-        const float4 v1 = *reinterpret_cast<const float4*>(&tile[rl * TLD + c8 + 4]);
-        *reinterpret_cast<uint4*>(a.C + row * a.ldc + cbase + c8) =
-            make_uint4(pack_bf16x2(v0.x, v0.y), pack_bf16x2(v0.z, v0.w), pack_bf16x2(v1.x, v1.y),
-                       pack_bf16x2(v1.z, v1.w));
-      }
-    }
-    __syncthreads();
-  }
-}
-
-template <int EPI, int BM, int BN>
-int launch(const EncGemmArgs& a, hipStream_t st) {
-  using T = Tile<BM, BN>;
-  const int64_t mt = ((int64_t)a.M + BM - 1) / BM;
-  const int64_t nwg = mt * (a.N / BN) * a.groups;
-  TRK_REQUIRE(a.N % BN == 0, "enc_gemm: N must be a multiple of %d", BN);
-  TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm: too many workgroups");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc_gemm_kernel<EPI, BM, BN>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::kLds);
-    attr = true;
-  }
-  hipLaunchKernelGGL((enc_gemm_kernel<EPI, BM, BN>), dim3((unsigned)nwg), dim3(512), T::kLds, st, a);
-  return trk::check_launch("enc_gemm_kernel");
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -486,7 +141,6 @@ constexpr int G4_SLD = 132;                 // stage row stride (u32): conflict-
 constexpr int G4_BUF = 1536;                // uint4 per buffer: A 512 (128 rows) | B 1024 (256 rows)
 constexpr size_t G4_RING = (size_t)3 * G4_BUF * 16;     // 72 KiB
 constexpr int G4_SLOTS = 4;                 // ROIs a 128-row tile spans (P >= 43)
-constexpr int G4_WSLOTS = 3;                // ROIs a wave's 64 rows span (P >= 43)
 constexpr int G4_SQ = 2;                    // s-tile DMA per thread (8 KiB)
 constexpr size_t G4_STILE = (size_t)G4_SQ * 256 * 16;
 constexpr size_t G4_STAGE = (size_t)128 * G4_SLD * 4;   // 66 KiB
@@ -494,15 +148,10 @@ constexpr size_t G4_RED = (size_t)G4_SLOTS * 256 * 8;   // 8 KiB
 constexpr size_t G4_LDS = (G4_RING + G4_STILE) > (G4_STAGE + G4_RED) ? (G4_RING + G4_STILE) : (G4_STAGE + G4_RED);
 static_assert(G4_LDS <= 80 * 1024, "two gemm4 workgroups per CU");
 
-// WIDE (P >= 64): a wave's 64 rows span at most 2 ROIs and a tile's 128 at most 3, so
-// the ROI-sum epilogue keeps 2 slots per wave instead of 3 (a third fewer reductions).
-// WMV: waves along M.  2 = the 128 x 256 tile above (4 waves, two workgroups per CU); 4 =
-// a 256 x 256 tile on 8 waves, one workgroup per CU (transition only, P >= 86 so the tile
-// spans <= 4 ROIs): the same wave tiles and MFMAs, the B tile streamed once per 256 rows
-// instead of per 128 -- 32 instead of 48 KB of L2 -> LDS per K step for the same work
-template <int EPI, bool WIDE, int HSWM, int SMF, int WMV = 2>
+// HSWM: the DSC tile's activation (1 = Hardswish, the normal group), a compile-time constant
+template <int EPI, int HSWM>
 __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, unsigned char* smem) {
-  static_assert(WMV == 2 || (WMV == 4 && EPI == EPI_TRANS && SMF == 1), "wide-M gemm4: transition, MFMA sums");
+  constexpr int WMV = 2;                           // waves along M
   constexpr int NT = 128 * WMV, BM = 64 * WMV;   // threads, tile rows
   constexpr int ABUF = BM * 4, BUF = ABUF + 1024;  // uint4: A | B (256 rows) per ring stage
   constexpr int NB = 1024 / NT;                    // B DMA ops per thread per stage (A: 2)
@@ -694,7 +343,7 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
   // slot (0 where it has no rows) with plain stores -- no zeroing pass, no atomics; the
   // consumer adds llrintf(p0 * 2^24) + llrintf(p1 * 2^24) (the former int64 atomics' sum)
   float* part = reinterpret_cast<float*>(smem + (EPI == EPI_DSC ? G4_STAGE : (size_t)0));  // [WMV][SLOTS][256]
-  if constexpr (SMF != 0) {
+  {
     // the same partials on the MFMA: S[slot][col] = sum_rows mask[slot][row] * act[row][col]
     // as 16x16x32 bf16 MFMAs whose B operand is the accumulator fragments themselves --
     // lane (fr, fc) holds rows 4 fc + e of row tiles 2p and 2p + 1 for column fr, which
@@ -739,64 +388,6 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
         for (int ts = 0; ts < G4_SLOTS; ++ts) part[(wr * G4_SLOTS + ts) * 256 + colq + t * 16] = sacc[ts];
       }
     }
-  } else {
-    const int64_t r0w = m0 + wr * 64;
-    const int64_t roiw = r0w / a.P;
-    const int wslot0 = (int)(roiw - roi_base);
-    const int P = a.P;
-    const int nxt0 = P - (int)(r0w - roiw * P);
-    const bool full = r0w + 64 <= (int64_t)a.M;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      constexpr int WS = WIDE ? 2 : G4_WSLOTS, TS = WIDE ? 3 : G4_SLOTS;
-      float ssum[WS];
-#pragma unroll
-      for (int q = 0; q < WS; ++q) ssum[q] = 0.f;
-      int slot = 0, nxt = nxt0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const f4v v = acc[k][t];
-        if (full && nxt >= 16 * k + 16) {
-          const float x = (v[0] + v[1]) + (v[2] + v[3]);
-#pragma unroll
-          for (int q = 0; q < WS; ++q)
-            if (q == slot) ssum[q] += x;
-        } else {
-          float lo = 0.f, hi = 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int row = 16 * k + fc * 4 + e;
-            const float x = (r0w + row < a.M) ? v[e] : 0.f;
-            if (row < nxt) lo += x;
-            else hi += x;
-          }
-#pragma unroll
-          for (int q = 0; q < WS; ++q) {
-            if (q == slot) ssum[q] += lo;
-            if (q == slot + 1) ssum[q] += hi;
-          }
-        }
-        if (nxt <= 16 * k + 16) {
-          ++slot;
-          nxt += P;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < WS; ++q) {
-        ssum[q] = sum_xor16(ssum[q]);
-        ssum[q] = sum_xor32(ssum[q]);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int ts = 0; ts < TS; ++ts) {
-          float v = 0.f;
-#pragma unroll
-          for (int q = 0; q < WS; ++q)
-            if (q <= slot && wslot0 + q == ts) v = ssum[q];
-          part[(wr * G4_SLOTS + ts) * 256 + colq + t * 16] = v;
-        }
-      }
-    }
   }
   if (prof) pst[3] = eg_stamp();
   if (EPI == EPI_DSC) {
@@ -826,13 +417,10 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
       long long v = 0;
 #pragma unroll
       for (int w = 0; w < WMV; ++w) v += llrintf(part[(w * G4_SLOTS + slot) * 256 + c] * kFix);
-      // partial j = the ROI's 128-row block index; a 256-row tile covers two blocks: the sum
-      // goes to the first one inside the ROI, 0 to the second (every partial written once)
-      const int64_t rb0 = roi * a.P / kPartRows, rb1 = (roi * a.P + a.P - 1) / kPartRows;
+      // partial j = the ROI's 128-row block index (the tile's own block)
+      const int64_t rb0 = roi * a.P / kPartRows;
       const int64_t tb0 = max(m0 / kPartRows, rb0);
-      long long* o = a.sums + (roi * kPart + (tb0 - rb0)) * a.ld_sums + g * a.N + n0 + c;
-      o[0] = v;
-      if (WMV == 4 && tb0 + 1 <= rb1 && tb0 + 1 <= (m0 + BM - 1) / kPartRows) o[a.ld_sums] = 0;
+      a.sums[(roi * kPart + (tb0 - rb0)) * a.ld_sums + g * a.N + n0 + c] = v;
     }
   }
   if (prof) pst[5] = eg_stamp();
@@ -863,19 +451,13 @@ __device__ __forceinline__ void gemm4_tile(const EncGemmArgs& a, int64_t lb, uns
 // one workgroup per tile (XCD-remapped); a DSC tile's group (SiLU / Hardswish) is a
 // template argument of its body, so each body is straight-line (a per-element select
 // was compiled into 64 branches of nop-padded exp / rcp chains)
-template <int EPI, bool WIDE, int SMF>
+template <int EPI>
 __global__ void __launch_bounds__(256, 2) gemm4_kernel(EncGemmArgs a, int64_t ntiles) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t lb = xcd_remap(blockIdx.x, ntiles);
-  if (EPI == EPI_DSC && (lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, WIDE, 1, SMF>(a, lb, smem);
-  else gemm4_tile<EPI, WIDE, 0, SMF>(a, lb, smem);
+  if (EPI == EPI_DSC && (lb % (a.N / 256 * a.groups)) / (a.N / 256) == 1) gemm4_tile<EPI, 1>(a, lb, smem);
+  else gemm4_tile<EPI, 0>(a, lb, smem);
 }
-// the 256 x 256 transition tile (gemm4_tile WMV = 4): 8 waves, one workgroup per CU
-__global__ void __launch_bounds__(512, 1) gemm4w_trans_kernel(EncGemmArgs a, int64_t ntiles) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  gemm4_tile<EPI_TRANS, true, 0, 1, 4>(a, xcd_remap(blockIdx.x, ntiles), smem);
-}
-constexpr size_t G4W_RING = (size_t)3 * (256 * 4 + 1024) * 16;  // 96 KiB
 
 // ---------------------------------------------------------------------------
 // g1dw4 (g1dw_mode 7): g1dw_kernel's first 1x1 convs + depthwise 5x5 on 4-wave
@@ -966,7 +548,6 @@ __device__ __forceinline__ void dw5q_regs(const uint32_t* __restrict__ src, cons
 }
 
 
-template <bool PF>
 __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W1,
                                                         const float* __restrict__ wdw, uint16_t* __restrict__ Y2,
                                                         int M, int N) {
@@ -1095,12 +676,12 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
         }
   }
   __syncthreads();
-  // PF (g1dw 6, the default): L2 prefetch of the A rows of the tile this slot most likely
+  // L2 prefetch of the A rows of the tile this slot most likely
   // runs next (xcd_remap's order: logical tile lb + 64 runs on this XCD after lb), an eighth
   // of its M tile per N tile, issued now so the depthwise below covers its HBM latency
   // (28 us of 389 isolated); retired by the kernel's end, nothing waits on it before
   uint32_t pf = 0;
-  if (PF) {
+  {
     const int64_t tn = lb + 64;
     const int64_t xs = (int64_t)gridDim.x / 8;   // logical tiles per XCD range (remap: contiguous)
     if (tn / xs == lb / xs && tn < (int64_t)gridDim.x && tid < 208) {
@@ -1130,54 +711,36 @@ __global__ void __launch_bounds__(256, 2) g1dw4_kernel(const uint16_t* __restric
       default: dw5q_regs<1, 1, G1Q_YS>(src, wreg, dst, l); break;
     }
   }
-  if (PF) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
 }
 
 
 // ---------------------------------------------------------------------------
-// rmb_front: one DSC of the RMB end to end for one 10x10 ROI per workgroup
-// (card.py:28-57: the branch's first 1x1 convs, the depthwise 5x5, depth.2 +
-// point.2 with eval-BN folded, the activation, and the ROI's column sums).  Y1 and
-// Y2 live only in LDS, so the [M, 1024] Y2 that g1dw4 wrote (419 MB per 2048
-// ROIs) and gemm4<DSC> read back (530 MB) never reaches HBM; HBM sees X once and
-// XRN once.  Workgroup (roi, g): g = 0 reinforce (SiLU), 1 normal (Hardswish).
+// rmb_front3: one DSC of the RMB end to end for 10x10 ROIs (card.py:28-57: the
+// branch's first 1x1 convs, the depthwise 5x5, depth.2 + point.2 with eval-BN folded,
+// the activation, and the SE's squeeze means).  Y1 and Y2 live only in LDS; HBM sees X
+// and the [x_r | x_n] rows (XRN).  A workgroup runs one DSC group G (0 reinforce /
+// SiLU, 1 normal / Hardswish) for the ROIs roi0, roi0 + stride, ... (persistent grid).
 //
-// 8 waves, one workgroup per CU (126 KiB of LDS).  Wave w owns output columns
-// 64 w .. 64 w + 63 of the group's 512 in BOTH GEMMs and all 112 rows (7 row
-// tiles of 16; rows 100..111 are padding whose results are dropped): a 112 x 64
-// wave tile of 16x16x32 MFMAs, 112 accumulator registers.  No weight element is used
-// by two waves, so weights do not go through LDS: they are pre-packed on the host in
-// MFMA fragment order ([g][k step][16-col tile][lane] x 16 B), and a wave's four
-// fragments of a K step are one contiguous 4 KiB read straight into VGPRs, two steps
-// ahead.  The ROI's X rows (shared by the 8 waves) are staged by LDS-DMA into the same
-// LDS image Y1 and Y2 use later: 16 K blocks of 32 channels, 100 rows x 64 B per block
-// (row r's 16-B chunk c at slot r*4 + (c ^ sw(r)), sw(r) = (r >> 1) & 3: conflict-free
-// ds_read_b128 fragment reads, 2-way 8-B row writes), block stride 6464 B so the
-// depthwise's 4-B channel-pair reads of two blocks fall on different banks.  X arrives in
-// four groups of four blocks, each issued four K steps ahead: GEMM1 waits at 4 barriers
-// instead of one per K step (a per-step barrier kept the 8 waves' LDS reads in lockstep:
-// GEMM1 ran 2.3x GEMM2's time for the same MFMAs).  Both GEMMs are computed transposed
-// (weights = A operand), so a lane holds 4 consecutive channels of one pixel.  Same
-// MFMA shape, K order and roundings (Y1 and Y2 to bf16) as g1dw4 + gemm4<DSC>: XRN is
-// bit-identical to the two-kernel path; the column sums add the same f32 activations
-// in another order (f32 lane sums, one partial per ROI).
+// 8 waves, one workgroup per CU.  Wave w owns output columns 64 w .. 64 w + 63 of the
+// group's 512 in BOTH GEMMs and all 112 rows (7 row tiles of 16; rows 100..111 are
+// padding whose results are dropped): a 112 x 64 wave tile of 16x16x32 MFMAs, 112
+// accumulator registers.  No weight element is used by two waves, so weights do not go
+// through LDS: they are pre-packed on the host in MFMA fragment order ([g][k step][16-col
+// tile][lane] x 16 B), and a wave's four fragments of a K step are one contiguous 4 KiB
+// read straight into VGPRs, two steps ahead.  The ROI's X rows (shared by the 8 waves)
+// are staged by LDS-DMA into the LDS image Y1 and Y2 use later: K blocks of 32 channels,
+// 100 rows x 64 B per block (row r's 16-B chunk c at slot r*4 + (c ^ sw(r)), sw(r) =
+// (r >> 1) & 3: conflict-free ds_read_b128 fragment reads, 2-way 8-B row writes), block
+// stride 6464 B so the depthwise's 4-B channel-pair reads of two blocks fall on different
+// banks.  X arrives in four groups of four blocks, each issued four K steps ahead (a
+// per-step barrier kept the 8 waves' LDS reads in lockstep).  Both GEMMs are computed
+// transposed (weights = A operand), so a lane holds 4 consecutive channels of one pixel.
+// Same MFMA shape, K order and roundings (Y1 and Y2 to bf16) as g1dw4 + gemm4<DSC>: XRN is
+// bit-identical to the two-kernel path; the means add the same f32 activations in
+// another order.
 constexpr int RF_S = 100;                                      // rows per ROI
 constexpr int RF_KBS = 1616;                                   // block stride (dwords): 6400 B + 64
-constexpr size_t RF_Y = (size_t)15 * RF_KBS * 4 + 112 * 64;    // row tile 6 of block 15 reads rows ..111
-constexpr int RF_OS = 260;                                     // output staging row stride (dwords)
-constexpr size_t RF_LDS = RF_Y;
-static_assert((size_t)RF_S * RF_OS * 4 <= RF_Y, "output staging reuses the Y image");
-static_assert(RF_LDS <= 160 * 1024, "one rmb_front workgroup per CU");
-
-// GEMM1 issue order: X group 0 (blocks 0..3, one DMA op per block per wave), B(0), B(1);
-// step kt issues X group kt / 4 + 1 when kt % 4 == 0 (4 ops), then B(kt + 2).  Ops issued
-// after B(kt) when step kt starts = the vmcnt that retires B(kt) and every older X group
-constexpr int rf_vm_after_b(int kt) {
-  constexpr int NK = 16;
-  if (kt == 0) return 4;
-  if (kt == 1) return 4 + 4;
-  return ((kt - 1) % 4 == 0 && (kt - 1) / 4 + 1 < 4 ? 4 : 0) + (kt + 1 < NK ? 4 : 0);
-}
 
 // s_waitcnt vmcnt(n) for a (compile-time after unrolling) n, tied to the four fragment registers
 __device__ __forceinline__ void rf_vmwait(int n, u32x4 (&b)[4]) {
@@ -1199,36 +762,12 @@ struct RfArgs {
   const uint4* W2p;     // [2][16][32][64] fragments of the BN-folded DSC weights
   const float* bias;    // [1024] BN-folded bias
   uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
-  long long* sums;      // [R][kPart][1024] int64 x 2^24: partial 0 = the ROI's sum, the rest 0
+  float *m_r, *m_n;     // [R][512] the squeeze means of SiLU(x_r) / Hardswish(x_n) (trk_enc_se's)
   int64_t R;            // ROIs
-  int pf;               // trk_set_tuning("rf_pf"): L2 prefetch distance in ROIs (X rows of ROI + pf), 0 = none
-  unsigned long long* prof;  // trk_enc_set_prof: wave 0's phase cycles per workgroup (diagnostics)
-  int lag;              // trk_set_tuning("rf_lag"), rf2_body: half B starts GEMM1 once A is past K step lag
-  int sum_lanes;        // trk_set_tuning("rf_sumlanes"): rf2_body's ROI sums converted one channel per lane
-  int dwprio;           // trk_set_tuning("rf_dwprio"): rf2_body's depthwise at s_setprio 2 (1: half B, 2: both)
-  // fused mode (trk_enc_rmb_fused: SE and the transition inside the kernel)
-  const uint4* Wtp;     // [32 k steps][32 col tiles][64 lanes] 16-B fragments of Wt [512][1024]
-  const float* bt;      // [512] transition bias
-  const float *se_w1, *se_b1, *se_w2, *se_b2;  // [128][512], [128], [512][128], [512] (f32)
-  uint16_t* XN;         // [R * 100][512] hand-off: the normal group's bf16 Hardswish(x_n)
-  int* flags;           // [R] the epoch the normal group's XN rows were published with
-  int epoch;
-  float *m_r, *m_n, *s; // [R][512] squeeze means and SE scales (trk_enc_se's outputs)
-  long long* tsums;     // [R][kPart][512] sums of SiLU(T) (partial 0; the others 0)
-  // front + SE (trk_enc_rmb_front_se, rf_v 3): each workgroup writes its ROIs' squeeze means
-  // (group 0 m_r, group 1 m_n) and group 0 then runs the SE over its ROIs in batches of 16;
-  // sums may be null (then not written)
-  int se_front, se_H;  // se_front 2 (trk_enc_rmb_front_means): the means only, no SE
+  unsigned long long* prof;  // trk_enc_set_prof: every wave's phase cycles per ROI (diagnostics)
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
-// Y dword of (pixel s, channel pair at column col of the group): block col / 32,
-// chunk (col % 32) / 8 swizzled by rf_sw(s), dword (col % 8) / 2
-__device__ __forceinline__ int rf_yaddr(int s, int col) {
-  const int kb = col >> 5, c = (col & 31) >> 3, d = (col & 7) >> 1;
-  return kb * RF_KBS + s * 16 + ((c ^ rf_sw(s)) << 2) + d;
-}
-
 // depthwise 5x5 of output quadrant (QY, QX) for the lane's channel pair, results
 // held as packed bf16 pairs (the caller writes them back in place after a barrier);
 // same per-output FMA order as dw5q_regs.  Pixel s sits at dword b[rf_sw(s)] + 16 s (s is
@@ -1290,11 +829,6 @@ __device__ __forceinline__ void rf_dw5q_store(uint32_t* y, const int (&b)[4], co
     }
 }
 
-__device__ __forceinline__ void rf_lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  g4_barrier();
-}
-
 // the wave's four B fragments of k step kt (4 KiB contiguous): asm loads, so the issue order
 // is the program order and the caller's counted vmcnt waits are exact
 __device__ __forceinline__ void rf_loadB(const uint4* bp, int kt, u32x4 (&d)[4]) {
@@ -1338,277 +872,21 @@ __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f
   }
 }
 
-template <int G>
-__device__ __forceinline__ void rf_body(const RfArgs& a, int64_t lb, unsigned char* smem) {
-  const int64_t roi = lb >> 1;
-  unsigned long long pst[8];
-  const bool prof = a.prof != nullptr;
-  if (prof) pst[0] = eg_stamp();
-  uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fc = lane >> 4;
-  const int64_t r0 = roi * RF_S;
-  constexpr int NK = 512 / BK;
-
-  // X -> the LDS image: wave w's lanes < 50 move pieces 50 w + lane (row p >> 2, slot p & 3)
-  // of every block, one DMA op per block
-  const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
-  const uint16_t* xsrc = a.X + (r0 + xr) * 512 + (((xp & 3) ^ rf_sw(xr)) * 8);
-  auto issueX = [&](int grp) {
-    if (lane < 50) {
-      const uint16_t* xs = xsrc;
-      asm volatile("" : "+v"(xs));  // per group: the 16 block addresses are not all hoisted
-#pragma unroll
-      for (int kb = 4 * grp; kb < 4 * grp + 4; ++kb)
-        __builtin_amdgcn_global_load_lds(GPTR(xs + kb * BK), LPTR(Y + kb * RF_KBS + 200 * wave), 16, 0, 0);
-    }
-  };
-  // fragment (k step kt, col tile t) of the wave at [(g * 16 + kt) * 32 + 4 wave + t][lane]
-  const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
-  const uint4* b2p = a.W2p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
-  u32x4 bq[3][4];
-  const int lterm = fr * 4 + (fc ^ rf_sw(fr));
-  const uint32_t y_a = lds_addr(Y) + lterm * 16;
-
-  f4v acc[7][4];
-#pragma unroll
-  for (int i = 0; i < 7; ++i)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
-
-  // ---- GEMM1: Y1^T[64 x 112 per wave] = W1 . X^T, K = 512.  Every load of the K loops is
-  // an asm statement or the DMA builtin in program order (no compiler waits)
-  issueX(0);
-  rf_loadB(b1p, 0, bq[0]);
-  rf_loadB(b1p, 1, bq[1]);
-#pragma unroll
-  for (int kt = 0; kt < NK; ++kt) {
-    u32x4(&b)[4] = bq[kt % 3];
-    // at an X group's first step: vmcnt(0), not a count -- an LDS-DMA is not guaranteed to
-    // retire in issue order with the VGPR loads behind it, so only an empty counter proves
-    // the group landed
-    rf_vmwait(kt % 4 == 0 ? 0 : rf_vm_after_b(kt), b);
-    if (kt % 4 == 0) {
-      g4_barrier();  // X group kt / 4 landed for every wave
-      if (kt / 4 + 1 < 4) issueX(kt / 4 + 1);
-    }
-    if (kt + 2 < NK) rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
-    rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
-  }
-  if (prof) {
-    asm volatile("" ::"v"(acc[6][3][3]));
-    pst[1] = eg_stamp();
-  }
-  // the compiler puts an s_waitcnt vmcnt(0) before the first LDS access after an LDS-DMA
-  // (alias safety): nothing but retired GEMM1 loads may be in flight there, so every load
-  // below is issued after the Y1 writes, and the L2 prefetch after the depthwise's reads
-  rf_lds_barrier();  // every wave's GEMM1 reads of X are done: Y1 overwrites the image
-  // ---- Y1 -> LDS: each lane stores its 4 channels of a pixel as one 8-B write
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int px = i * 16 + fr;
-    if (px < RF_S) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const f4v v = acc[i][t];
-        *reinterpret_cast<uint2*>(Y + rf_yaddr(px, wave * 64 + t * 16 + fc * 4)) =
-            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      }
-    }
-  }
-  // depthwise taps of the lane's channel pair (asm loads, waited for below with a count that
-  // leaves GEMM2's first two B steps in flight)
-  const int cg = wave >> 1;  // the wave's 128 depthwise channels
-  dw_pair_t wreg[25];
-  {
-    const float* wp = a.wdw + G * 512 + cg * 128 + 2 * lane;
-#pragma unroll
-    for (int k = 0; k < 25; ++k)
-      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(wreg[k]) : "v"(wp + k * 1024) : "memory");
-  }
-  rf_loadB(b2p, 0, bq[0]);
-  rf_loadB(b2p, 1, bq[1]);
-  rf_lds_barrier();
-  if (prof) pst[2] = eg_stamp();
-  asm volatile("s_waitcnt vmcnt(8)" : "+v"(wreg[0]), "+v"(wreg[1]), "+v"(wreg[2]), "+v"(wreg[3]), "+v"(wreg[4]),
-               "+v"(wreg[5]), "+v"(wreg[6]), "+v"(wreg[7]), "+v"(wreg[8]), "+v"(wreg[9]), "+v"(wreg[10]),
-               "+v"(wreg[11]), "+v"(wreg[12])::"memory");
-  asm volatile("" : "+v"(wreg[13]), "+v"(wreg[14]), "+v"(wreg[15]), "+v"(wreg[16]), "+v"(wreg[17]), "+v"(wreg[18]),
-               "+v"(wreg[19]), "+v"(wreg[20]), "+v"(wreg[21]), "+v"(wreg[22]), "+v"(wreg[23]), "+v"(wreg[24]));
-  if (prof) pst[2] = eg_stamp();
-
-  // ---- depthwise 5x5 in place: wave = (128-channel group, output half); both quadrants
-  // of the half are computed before anyone overwrites Y1
-  const int NPF = (G == 0 && a.pf) ? 2 : 0;
-  uint32_t pf0 = 0, pf1 = 0;
-  {
-    const int kb0 = cg * 4 + (lane >> 4), c0 = (lane & 15) >> 2, d0 = lane & 3;
-    const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
-                       kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
-    uint32_t o0[25], o1[25];
-    // L2 prefetch (reinforce workgroups) of the X rows of ROI + a.pf (default 8): the XCD's
-    // 32 CUs run 16 ROIs at a time, so that ROI starts about half a workgroup lifetime after
-    // this point, early enough for its first DMA group to find the rows near (16 ahead: the
-    // rows leave L2 first, 701 vs 662 MB fetched per launch, pipeline 0.6-0.9 % slower).
-    // Two 4-B loads per thread = the ROI's 800 128-B lines; retired by GEMM2's third wait
-    auto prefetch = [&]() {
-      if (G == 0 && a.pf) {
-        const int64_t rn = min(roi + a.pf, a.R - 1);
-        const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
-        const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
-        asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
-        asm volatile("global_load_dword %0, %1, off" : "+v"(pf1) : "v"(pb) : "memory");
-      }
-    };
-    if ((wave & 1) == 0) {
-      rf_dw5q<0, 0>(Y, yb, wreg, o0);
-      rf_dw5q<0, 1>(Y, yb, wreg, o1);
-      prefetch();
-      rf_lds_barrier();
-      rf_dw5q_store<0, 0>(Y, yb, o0);
-      rf_dw5q_store<0, 1>(Y, yb, o1);
-    } else {
-      rf_dw5q<1, 0>(Y, yb, wreg, o0);
-      rf_dw5q<1, 1>(Y, yb, wreg, o1);
-      prefetch();
-      rf_lds_barrier();
-      rf_dw5q_store<1, 0>(Y, yb, o0);
-      rf_dw5q_store<1, 1>(Y, yb, o1);
-    }
-  }
-  rf_lds_barrier();
-  if (prof) pst[3] = eg_stamp();
-
-  // ---- GEMM2: x = Y2 . W2^T (K = 512), A fragments from the resident Y image
-  float4 bias4[4];
-#pragma unroll
-  for (int i = 0; i < 7; ++i)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kt = 0; kt < NK; ++kt) {
-    u32x4(&b)[4] = bq[kt % 3];
-    rf_vmwait(kt + 1 < NK ? 4 + (kt < 2 ? NPF : 0) : 0, b);
-    if (kt == 2 && G == 0) asm volatile("" : "+v"(pf0), "+v"(pf1));  // retired by the wait above
-    if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
-    if (kt == NK - 3) {  // the epilogue's bias, three steps before it is needed (L2 latency)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
-    }
-    rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
-  }
-
-  if (prof) {
-    asm volatile("" ::"v"(acc[6][3][3]));
-    pst[4] = eg_stamp();
-  }
-  // ---- epilogue: BN-folded bias + activation (lane: channels 16 t + 4 fc + e)
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
-        v = G == 1 ? hswish2(v) : silu2(v);
-        acc[i][t][2 * h] = v.x;
-        acc[i][t][2 * h + 1] = v.y;
-      }
-  }
-  // column sums over the ROI's 100 pixels: per lane over its pixel tiles (tile 6 holds
-  // pixels 96..111: fr < 4 only), then over the 16 pixel lanes fr of each channel group
-  {
-    const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float sv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) x += acc[i][t][e];
-        if (fr < 4) x += acc[6][t][e];
-        sv[e] = x;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sv[e] += lane_xor1(sv[e]);
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
-      }
-      if (fr == 0) {
-        long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[e] * kFix);
-        for (int j = 1; j < cnt; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[j * 1024 + e] = 0;
-      }
-    }
-  }
-  if (prof) pst[5] = eg_stamp();
-  {
-    rf_lds_barrier();  // every wave's GEMM2 reads of Y are done: stage the output over it
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int px = i * 16 + fr;
-      if (px < RF_S) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f4v v = acc[i][t];
-          *reinterpret_cast<uint2*>(Y + px * RF_OS + ((wave * 64 + t * 16 + fc * 4) >> 1)) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
-      }
-    }
-    rf_lds_barrier();
-    if (prof) pst[6] = eg_stamp();
-    const uint32_t* stg = Y;
-    uint16_t* dst = a.XRN + r0 * 1024 + G * 512;
-#pragma unroll 4
-    for (int q = tid; q < RF_S * 64; q += 512) {
-      const int row = q >> 6, c = q & 63;
-      *reinterpret_cast<uint4*>(dst + (int64_t)row * 1024 + c * 8) =
-          *reinterpret_cast<const uint4*>(stg + row * RF_OS + c * 4);
-    }
-  }
-  if (prof) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pst[7] = eg_stamp();
-    if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
-      unsigned long long* o = a.prof + (lb * 8 + wave) * 8;
-      for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
-      o[7] = pst[7] - pst[0];
-    }
-  }
-}
-
-// ---- rmb_front with decoupled halves (round 4, rf_v = 2, the default).  The same
-// phases, math and per-wave tiles as rf_body, but the 8 waves no longer pass full
-// workgroup barriers between phases.  Half A (waves 0..3, one per SIMD) produces Y1 / Y2
-// channels 0..255 and half B (waves 4..7) channels 256..511; the depthwise of a half only
-// reads its own half's Y1, so the only cross-half dependencies left are GEMM2's K steps
-// 8..15 (Y2(B)) and the LDS regions the halves reuse.  Those are tracked by LDS counters
-// (a wave adds 1 after its LDS writes or DMA have landed; a waiter polls with s_sleep).
-// A runs ahead (older waves, and MFMA phases at s_setprio 1), so on every SIMD one
-// wave's depthwise / activation VALU runs beside its partner's MFMAs instead of after
-// them (rf_body: 68K cycles per workgroup, of which 27K MFMA).
-// LDS (blocks of RF_KBS dwords, the rf_body image): blocks 0..15 = X for GEMM1 (both
-// halves), blocks 16..23 = Y(A); once both halves finished GEMM1, blocks 8..15 = Y(B)
-// and blocks 0..7 = A's output staging; B stages over Y(A) after both halves' GEMM2.
+// Decoupled halves: half A (waves 0..3, one per SIMD) produces Y1 / Y2 channels 0..255 and
+// half B (waves 4..7) channels 256..511; the depthwise of a half only reads its own half's Y1,
+// so the only cross-half dependencies are GEMM2's K steps 8..15 (Y2(B)) and the LDS regions
+// the halves reuse.  Those are tracked by LDS counters (a wave adds 1 after its LDS writes or
+// DMA have landed; a waiter polls with s_sleep) that count on across the workgroup's ROIs
+// (targets 4 (it + 1)).  B starts GEMM1 behind A's (they share every SIMD's matrix pipe), so
+// on every SIMD one wave's depthwise / activation VALU runs beside its partner's MFMAs.
+// LDS (blocks of RF_KBS dwords): blocks 0..15 = X for GEMM1 (both halves), blocks 16..23 =
+// Y(A); once both halves finished GEMM1, blocks 8..15 = Y(B) and blocks 0..7 = A's output
+// staging; B stages over Y(A) after both halves' GEMM2.
 constexpr int RF2_NB = 24;
 constexpr size_t RF2_CTR = (size_t)(RF2_NB - 1) * RF_KBS * 4 + 112 * 64;  // past block 23's row-111 reads
-enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16,
-       RF3_CPUB = 18, RF3_CYF = 19, RF3_CH = 20, RF3_CS = 21, RF3_CYS = 22, RF2_CSD = 24, RF2_NCTR = 32 };
+enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16, RF2_CSD = 18,
+       RF2_NCTR = 20 };
 constexpr size_t RF2_LDS = RF2_CTR + RF2_NCTR * 4;
-// fused mode: the SE vectors after the counters (m_r, relu(W1 m_r + b1), s)
-constexpr size_t RF3_M = RF2_LDS, RF3_H = RF3_M + 512 * 4, RF3_S = RF3_H + 128 * 4;
-constexpr size_t RF3_LDS = RF3_S + 512 * 4;
-static_assert(RF3_LDS <= 160 * 1024, "one fused rmb workgroup per CU");
 constexpr int RF2_SROW = 128;  // output staging row (dwords): 256 channels, 16-B chunks XOR-swizzled by row
 static_assert(RF2_LDS <= 160 * 1024, "one rmb_front workgroup per CU");
 static_assert((size_t)RF_S * RF2_SROW * 4 <= (size_t)8 * RF_KBS * 4, "a half's staging fits 8 blocks");
@@ -1673,56 +951,15 @@ __device__ __forceinline__ void rf_dma16_lanes36(const void* g, uint32_t base) {
       : "memory");
 }
 
-// ---- fused tail (trk_enc_rmb_fused): what trk_enc_se and trk_enc_transition_gemm did for
-// the ROI, inside the ROI's two workgroups.  acc holds the group's activated 64 x 112 tile.
-//   normal group (G = 1): m_n, then its bf16 Hardswish(x_n) rows -> XN with sc1 stores,
-//     each wave's stores retired, then the ROI's flag = epoch (one sc1 store).
-//   reinforce group (G = 0): m_r; bf16 SiLU(x_r) -> the LDS K-block image (blocks 0..15);
-//     SE (FC1: 4 threads per hidden unit, FC2: one thread per channel, f32 FMA chains);
-//     the image scaled in place, y = bf16(x_f * s) as gemm4<TRANS> stages it; then
-//     GEMM3 T = Wt . [y ; x_n] (K = 1024: the image, then the partner's XN rows polled
-//     for and loaded with sc1 loads into an 8-block LDS ring, blocks 16..23), + bias,
-//     SiLU, per-channel sums -> tsums.  The pair runs on one XCD (the grid is padded to a
-//     multiple of 16 workgroups), so the hand-off is an L2 round trip.
-// sc1 (agent-coherent) global access: stores drop their line from the writer's L2 and
-// loads bypass the reader's L1 (MI355X_MICROARCH.md, inter-workgroup hand-off table)
-__device__ __forceinline__ void rf3_store_sc1(uint16_t* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void rf3_load_sc1(const uint16_t* p, u32x4& v) {
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-}
-// poll the ROI's flag (sc1 loads) until it holds epoch; bounded like rf2_wait
-__device__ __forceinline__ void rf3_wait_flag(const int* flag, int epoch) {
-  uint32_t v, sv, n;
-  asm volatile(
-      "s_mov_b32 %[n], 0\n"
-      "1:\n\t"
-      "global_load_dword %[v], %[p], off sc1\n\t"
-      "s_waitcnt vmcnt(0)\n\t"
-      "v_readfirstlane_b32 %[s], %[v]\n\t"
-      "s_cmp_eq_u32 %[s], %[t]\n\t"
-      "s_cbranch_scc1 2f\n\t"
-      "s_add_u32 %[n], %[n], 1\n\t"
-      "s_cmp_gt_u32 %[n], %[lim]\n\t"
-      "s_cbranch_scc1 2f\n\t"
-      "s_sleep 2\n\t"
-      "s_branch 1b\n"
-      "2:"
-      : [v] "=&v"(v), [s] "=&s"(sv), [n] "=&s"(n)
-      : [p] "v"(flag), [t] "s"(epoch), [lim] "s"(kRf2Spin)
-      : "memory", "scc");
-}
-
-// per-channel sums of the wave's activated tile (rf_body's lane / DPP order): xor 1, xor 2,
+// per-channel sums of the wave's activated tile: xor 1, xor 2,
 // row_ror 8, row_ror 4 is a butterfly (row_ror 4 before 8 is not: lanes 0 and 4 would add
 // the quads in different orders), so every lane of a 16-lane row holds the same 16 sums;
-// lane fr returns the one of channel 16 (fr >> 2) + 4 fc + (fr & 3) (rf3_lane_ch), so the
+// lane fr returns the one of channel 16 (fr >> 2) + 4 fc + (fr & 3) (rf_lane_ch), so the
 // fixed-point conversions run once per channel instead of 16 times on lanes fr == 0
-__device__ __forceinline__ int rf3_lane_ch(int wave, int fr, int fc) {
+__device__ __forceinline__ int rf_lane_ch(int wave, int fr, int fc) {
   return wave * 64 + (fr >> 2) * 16 + fc * 4 + (fr & 3);
 }
-__device__ __forceinline__ float rf3_colsum(const f4v (&acc)[7][4], int fr) {
+__device__ __forceinline__ float rf_colsum(const f4v (&acc)[7][4], int fr) {
   float mine = 0.f;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -1742,352 +979,14 @@ __device__ __forceinline__ float rf3_colsum(const f4v (&acc)[7][4], int fr) {
   return mine;
 }
 // the squeeze mean of a sum as trk_enc_se takes it: (float)(llrint(sum * 2^24) * 2^-24) / 100
-__device__ __forceinline__ float rf3_mean(float sum) {
+__device__ __forceinline__ float rf_mean(float sum) {
   return (float)((double)llrintf(sum * kFix) * (1.0 / 16777216.0)) / (float)RF_S;
 }
-__device__ __forceinline__ void rf3_store_f32_sc1(float* p, float v) {
-  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-// 8 consecutive floats (32-B aligned) with two sc1 loads and one wait
-__device__ __forceinline__ void rf3_load8_sc1(const float* p, float (&v)[8]) {
-  u32x4 x, y;
-  asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
-               "global_load_dwordx4 %1, %2, off offset:16 sc1\n\t"
-               "s_waitcnt vmcnt(0)"
-               : "=&v"(x), "=&v"(y)
-               : "v"(p)
-               : "memory");
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    v[e] = __uint_as_float(x[e]);
-    v[4 + e] = __uint_as_float(y[e]);
-  }
-}
-__device__ __forceinline__ float rf3_load_f32_sc1(const float* p) {
-  float v;
-  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
-// the fused tail's hand-off flags per ROI (RF3_NFL ints): x_n rows, m_r, s published
-enum { RF3_FXN = 0, RF3_FMR = 1, RF3_FS = 2, RF3_NFL = 4 };
-
-template <int G>
-__device__ __forceinline__ void rf3_tail(const RfArgs& a, int64_t roi, unsigned char* smem, f4v (&acc)[7][4],
-                                         int64_t lb, unsigned long long t_start) {
-  // diagnostics (trk_enc_set_prof): per wave [start -> tail, then the tail's phases] (8 x u64)
-  const bool prof = a.prof != nullptr;
-  unsigned long long ps[9];
-  if (prof) ps[0] = eg_stamp();
-  auto stamp = [&](int k) {
-    if (prof) ps[k] = eg_stamp();
-  };
-  auto flush = [&](int last) {
-    if (prof && (threadIdx.x & 63) == 0) {
-      unsigned long long* o = a.prof + (lb * 8 + (threadIdx.x >> 6)) * 8;
-      o[0] = ps[0] - t_start;
-      for (int q = 1; q < 8; ++q) o[q] = q <= last ? ps[q] - ps[q - 1] : 0;
-    }
-  };
-  uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
-  float* Ms = reinterpret_cast<float*>(smem + RF3_M);
-  float* Hs = reinterpret_cast<float*>(smem + RF3_H);
-  int* fl = a.flags + roi * RF3_NFL;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int half = wave >> 2, hw = wave & 3;
-  const int fr = lane & 15, fc = lane >> 4;
-  const int64_t r0 = roi * RF_S;
-  const int ch = rf3_lane_ch(wave, fr, fc);
-  const float mean = rf3_mean(rf3_colsum(acc, fr));
-  // one lane of wave 0 publishes flag k once every wave has counted its retired stores
-  auto publish = [&](int cnt, int k) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    rf2_signal(ctr + cnt, lane);
-    if (wave == 0) {
-      rf2_wait(ctr + cnt, 8);
-      if (lane == 0) __hip_atomic_store(fl + k, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  if constexpr (G == 1) {
-    // ---- normal group: m_n; bf16 x_n rows -> XN (sc1), flag; then the ROI's SE (the
-    // reinforce group's m_r, published early, in; s out), off the reinforce group's path
-    a.m_n[roi * 512 + ch] = mean;
-    if (half == 0) {
-      rf2_wait(ctr + RF2_CG1 + 1, 4);
-    } else {
-      rf2_wait(ctr + RF2_CG2 + 0, 4);
-      rf2_wait(ctr + RF2_CG2 + 1, 4);
-    }
-    uint32_t* stg = Y + (half ? 16 * RF_KBS : 0);
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int px = i * 16 + fr;
-      if (px < RF_S) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f4v v = acc[i][t];
-          const int c = hw * 64 + t * 16 + fc * 4;
-          *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((c >> 3) ^ (px & 15)) << 2) + ((c & 7) >> 1)) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
-      }
-    }
-    rf2_signal(ctr + RF2_CST + half, lane);
-    rf2_wait(ctr + RF2_CST + half, 4);
-    stamp(1);
-    {
-      uint16_t* dst = a.XN + r0 * 512 + half * 256;
-      const int ht = tid & 255;
-      for (int q = ht; q < RF_S * 32; q += 256) {
-        const int row = q >> 5, c = q & 31;
-        rf3_store_sc1(dst + (int64_t)row * 512 + c * 8,
-                      *reinterpret_cast<const u32x4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2)));
-      }
-    }
-    publish(RF3_CPUB, RF3_FXN);
-    stamp(2);
-    // SE: m_r -> LDS, FC1, FC2 (one row group of 8 lanes per output, as trk_enc_se's sums in
-    // another order), s -> global (sc1) + flag
-    rf3_wait_flag(fl + RF3_FMR, a.epoch);
-    Ms[tid] = rf3_load_f32_sc1(a.m_r + roi * 512 + tid);
-    rf2_signal(ctr + RF3_CYF, lane);
-    rf2_wait(ctr + RF3_CYF, 8);
-    stamp(3);
-    const int l8 = lane & 7, g8 = lane >> 3;
-    auto sum8 = [&](float x) {
-      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));  // quad [1,0,3,2]
-      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));  // quad [2,3,0,1]
-      return x + __shfl_xor(x, 4);
-    };
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {  // FC1: h[j] = relu(b1[j] + W1[j] . m_r), j = 16 wave + 8 p + g8
-      const int j = 16 * wave + 8 * p + g8;
-      const float* w = a.se_w1 + j * 512 + 4 * l8;
-      float h = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
-        const float4 mv = *reinterpret_cast<const float4*>(Ms + 32 * kk + 4 * l8);
-        h = __builtin_fmaf(wv.x, mv.x, h);
-        h = __builtin_fmaf(wv.y, mv.y, h);
-        h = __builtin_fmaf(wv.z, mv.z, h);
-        h = __builtin_fmaf(wv.w, mv.w, h);
-      }
-      h = sum8(h);
-      if (l8 == 0) Hs[j] = fmaxf(h + a.se_b1[j], 0.f);
-    }
-    rf2_signal(ctr + RF3_CH, lane);
-    rf2_wait(ctr + RF3_CH, 8);
-    stamp(4);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {  // FC2: s[c] = hardsigmoid(b2[c] + W2[c] . h), c = 64 wave + 8 p + g8
-      const int c = 64 * wave + 8 * p + g8;
-      const float* w = a.se_w2 + c * 128 + 4 * l8;
-      float x = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const float4 wv = *reinterpret_cast<const float4*>(w + 32 * kk);
-        const float4 hv = *reinterpret_cast<const float4*>(Hs + 32 * kk + 4 * l8);
-        x = __builtin_fmaf(wv.x, hv.x, x);
-        x = __builtin_fmaf(wv.y, hv.y, x);
-        x = __builtin_fmaf(wv.z, hv.z, x);
-        x = __builtin_fmaf(wv.w, hv.w, x);
-      }
-      x = sum8(x);
-      if (l8 == 0) rf3_store_f32_sc1(a.s + roi * 512 + c, fminf(fmaxf(x + a.se_b2[c] + 3.0f, 0.f), 6.0f) / 6.0f);
-    }
-    publish(RF3_CS, RF3_FS);
-    stamp(5);
-    flush(5);
-    return;
-  } else {
-    // ---- reinforce group: m_r out first (the normal group's SE waits for it), bf16 x_f ->
-    // the K-block image (unscaled); GEMM3's x_n half over the ring, then -- once s has
-    // arrived -- the image scaled in place and GEMM3's x_f half
-    rf3_store_f32_sc1(a.m_r + roi * 512 + ch, mean);
-    publish(RF3_CYS, RF3_FMR);
-    // A's channels go to blocks 0..7 (X: dead once B is past GEMM1), B's to 8..15 (Y(B): dead
-    // once both halves are past GEMM2; the ring, blocks 16..23 = Y(A), likewise)
-    if (half == 0) {
-      rf2_wait(ctr + RF2_CG1 + 1, 4);
-    } else {
-      rf2_wait(ctr + RF2_CG2 + 0, 4);
-      rf2_wait(ctr + RF2_CG2 + 1, 4);
-    }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int px = i * 16 + fr;
-      if (px < RF_S) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f4v v = acc[i][t];
-          *reinterpret_cast<uint2*>(Y + rf_yaddr(px, wave * 64 + t * 16 + fc * 4)) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
-      }
-    }
-    rf2_signal(ctr + RF3_CYF, lane);
-    stamp(1);
-    // the partner's x_n (flag, then LDS-DMA with sc1 into the ring once every wave is past
-    // GEMM2): 4 K blocks per group, one op per block per wave, lanes < 50 moving pieces
-    // 50 wave + lane (row p >> 2, slot p & 3), as rf_body's X
-    rf3_wait_flag(fl + RF3_FXN, a.epoch);
-    const int xp = 50 * wave + lane, xr = min(xp >> 2, RF_S - 1);
-    const uint16_t* xsrc = a.XN + (r0 + xr) * 512 + (((xp & 3) ^ rf_sw(xr)) * 8);
-    auto ring_dma = [&](int grp) {  // x_n blocks 4 grp .. 4 grp + 3 -> slots (4 grp) & 7 ..
-      if (lane < 50) {
-        const uint16_t* xs = xsrc;
-        asm volatile("" : "+v"(xs));
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          __builtin_amdgcn_global_load_lds(GPTR(xs + (4 * grp + q) * BK),
-                                           LPTR(Y + (16 + ((4 * grp + q) & 7)) * RF_KBS + 200 * wave), 16, 0,
-                                           16 /* sc1 */);
-      }
-    };
-    rf2_wait(ctr + RF3_CYF, 8);  // the x_f image complete, every wave past GEMM2
-    ring_dma(0);
-    ring_dma(1);
-    stamp(2);
-    // ---- GEMM3 (K = 1024): steps 0..15 = x_n (ring; Wt k steps 16..31), 16..31 = x_f * s
-    // (image; Wt k steps 0..15).  Ring: groups 0, 1 (slots 0..7) issued above, 2 (slots 0..3)
-    // at step 4 and 3 (4..7) at step 8, each behind the barrier that ends the reads of the
-    // slots' previous group; barriers at 4, 8, 12 publish groups 1 (at 0: vmcnt(0) before the
-    // first barrier), 2, 3.  Before step 16: s from the normal group, the image scaled in place
-    constexpr int NK3 = 32;
-    const uint4* b3p = a.Wtp + (size_t)(wave * 4) * 64 + lane;
-    auto wstep = [](int kt) { return (kt + 16) & 31; };
-    u32x4 bq[3][4];
-    const int lterm = fr * 4 + (fc ^ rf_sw(fr));
-    const uint32_t y_a = lds_addr(Y) + lterm * 16;
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
-    float4 bias4[4];
-    rf_loadB(b3p, wstep(0), bq[0]);
-    rf_loadB(b3p, wstep(1), bq[1]);
-    __builtin_amdgcn_s_setprio(1);
-    auto step = [&](int kt) {
-      u32x4(&b)[4] = bq[kt % 3];
-      // vmcnt(0): this wave's ring DMA retired before the barrier that publishes it (groups
-      // 0-1 at step 0, 2 at 8, 3 at 12); steps 5 / 9 count the group issued one step before;
-      // step 16 follows the scaling, whose sc1 loads waited for everything
-      const bool rs = kt == 0 || kt == 8 || kt == 12;
-      rf_vmwait(rs ? 0 : (kt + 1 < NK3 ? 4 + ((kt == 5 || kt == 9) ? 4 : 0) : 0), b);
-      if (kt == 0 || kt == 4 || kt == 8 || kt == 12) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        g4_barrier();
-      }
-      if (kt == 4) ring_dma(2);  // slots 0..3: group 0 was read in steps 0..3
-      if (kt == 8) ring_dma(3);  // slots 4..7: group 1, steps 4..7
-      if (kt + 2 < NK3) rf_loadB(b3p, wstep(kt + 2), bq[(kt + 2) % 3]);
-      if (kt == NK3 - 3) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          bias4[t] = *reinterpret_cast<const float4*>(a.bt + wave * 64 + t * 16 + fc * 4);
-      }
-      const int blk = kt < 16 ? 16 + (kt & 7) : kt - 16;
-      rf_mfma_step(y_a + blk * RF_KBS * 4, b, acc);
-    };
-#pragma unroll
-    for (int kt = 0; kt < 16; ++kt) step(kt);
-    __builtin_amdgcn_s_setprio(0);
-    if (prof) ps[3] = eg_stamp();
-    rf3_wait_flag(fl + RF3_FS, a.epoch);
-    if (prof) ps[4] = eg_stamp();
-    {
-      // y = bf16(float(bf16 x_f) * s) in place: thread t takes channel chunk t & 63 (8
-      // channels, block (t & 63) >> 2, chunk t & 3) of rows wave + 8 i
-      const int cc = tid & 63, kb = cc >> 2, c4 = cc & 3;
-      float sc[8];
-      rf3_load8_sc1(a.s + roi * 512 + cc * 8, sc);
-      auto scale_row = [&](int px) {
-        u32x4* pp = reinterpret_cast<u32x4*>(Y + kb * RF_KBS + px * 16 + ((c4 ^ rf_sw(px)) << 2));
-        const u32x4 v = *pp;
-        u32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          o[e] = pack_bf16x2(__uint_as_float(v[e] << 16) * sc[2 * e], __uint_as_float(v[e] & 0xffff0000u) * sc[2 * e + 1]);
-        *pp = o;
-      };
-#pragma unroll
-      for (int i = 0; i < 12; ++i) scale_row(wave + 8 * i);  // rows 0..95
-      if (wave < 4) scale_row(96 + wave);                      // rows 96..99 (wave-uniform)
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    g4_barrier();  // the whole image scaled
-    if (prof) ps[5] = eg_stamp();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kt = 16; kt < NK3; ++kt) step(kt);
-    __builtin_amdgcn_s_setprio(0);
-    if (prof) ps[6] = eg_stamp();
-    // ---- SiLU(T + bias) and its per-channel sums over the ROI -> tsums
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
-          v = silu2(v);
-          acc[i][t][2 * h] = v.x;
-          acc[i][t][2 * h + 1] = v.y;
-        }
-    }
-    const float ts = rf3_colsum(acc, fr);
-    {
-      const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
-      long long* o = a.tsums + roi * kPart * 512 + ch;
-      o[0] = llrintf(ts * kFix);
-      for (int j = 1; j < cnt; ++j) o[j * 512] = 0;
-    }
-    if (prof) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(7);
-    flush(7);
-  }
-}
-
-// front + SE: the SE of the workgroup's ROIs roi0, roi0 + stride, ... in batches of 16 rows --
-// enc_se_kernel's arithmetic (rb_linear, the same tiles and K order, 8 waves), so s is
-// bit-identical to trk_enc_se on the means this kernel wrote
-__device__ __forceinline__ void rf_se_batches(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride) {
-  constexpr int C = 512;
-  const int H = a.se_H, ldx = ld_rows(C), ldh = ld_rows(H);
-  float* Xs = reinterpret_cast<float*>(smem);
-  float* Hs = Xs + RB * ldx;
-  for (int64_t b0 = roi0; b0 < a.R; b0 += RB * stride) {
-    const int nrow = (int)min<int64_t>(RB, (a.R - b0 + stride - 1) / stride);
-    for (int q = threadIdx.x; q < RB * (C / 4); q += blockDim.x) {
-      const int rr = q / (C / 4), c = (q % (C / 4)) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rr < nrow) v = *reinterpret_cast<const float4*>(a.m_r + (b0 + rr * stride) * C + c);
-      *reinterpret_cast<float4*>(Xs + swz_at(rr, c, ldx)) = v;
-    }
-    __syncthreads();
-    rb_linear<8>(Xs, ldx, a.se_w1, a.se_b1, H, C,
-                 [&](int row, int col, float v) { Hs[swz_at(row, col, ldh)] = fmaxf(v, 0.f); });
-    __syncthreads();
-    float* __restrict__ sout = a.s;
-    rb_linear<8>(Hs, ldh, a.se_w2, a.se_b2, C, H, [&](int row, int col, float v) {
-      if (row < nrow) sout[(b0 + row * stride) * C + col] = fminf(fmaxf(v + 3.0f, 0.f), 6.0f) / 6.0f;
-    });
-    __syncthreads();
-  }
-}
-
-// MODE 0: one ROI (lb >> 1) per workgroup; 1: rmb_fused (one ROI + the fused tail); 2: persistent
-// (rmb_front3): the workgroup runs ROIs roi0, roi0 + stride, ... of its group G, the LDS counters
-// count on across ROIs (targets 4 (it + 1)), and ROI it + 1's X DMA and GEMM1 start as soon as
-// the blocks they need are free -- half A's GEMM1 of the next ROI runs under half B's epilogue
+// The workgroup's ROIs roi0, roi0 + stride, ...: ROI it + 1's X DMA and GEMM1 start as soon as
+// the blocks they need are free, so half A's GEMM1 of the next ROI runs under half B's epilogue
 // of this one instead of behind a workgroup boundary
-template <int G, int MODE>
-__device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned char* smem, int64_t roi0 = -1,
-                                         int64_t stride = 0) {
+template <int G>
+__device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride) {
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2097,7 +996,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   if (threadIdx.x < RF2_NCTR) ctr[threadIdx.x] = 0;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   g4_barrier();  // the only full barrier: counters zeroed
-  int64_t roi = MODE == 2 ? roi0 : (lb >> 1);
+  int64_t roi = roi0;
   for (uint32_t it = 0; roi < a.R; ++it, roi += stride) {
   const uint32_t t4 = 4u * (it + 1), p4 = 4u * it;  // counter targets: this ROI's / the previous one's
   // lane-dependent values re-derived per ROI through an opaque copy: hoisted out of the ROI
@@ -2144,10 +1043,9 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
 
   // ---- GEMM1 (K = 512 over X blocks 0..15); A: 8 DMA ops per group, B: none.  One
   // loop per half (HALF a template constant): a half test inside the unrolled loop costs
-  // spills
-  // (persistent mode, targets 0 on the first ROI: before the previous ROI's blocks are
-  // overwritten, half A's staging reads (X blocks 0..7) and both halves' GEMM2 (blocks 8..15
-  // held Y2(B)) are done)
+  // spills.  Before the previous ROI's blocks are overwritten (targets 0 on the first ROI),
+  // half A's staging reads (X blocks 0..7) and both halves' GEMM2 (blocks 8..15 held Y2(B))
+  // are done
   auto gemm1 = [&](auto half_c) {
     constexpr int HALF = decltype(half_c)::value;
     if (HALF == 0) {
@@ -2184,10 +1082,10 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
   if (half == 0) {
     gemm1(std::integral_constant<int, 0>{});
   } else {
-    // B starts behind A (rf_lag K steps; 16 = after A's whole GEMM1): run together, the
-    // two halves share every SIMD's matrix pipe and reach their VALU phases together
-    if (a.lag >= 16) rf2_wait(ctr + RF2_CG1 + 0, t4);
-    else if (a.lag > 0) rf2_wait(ctr + RF2_CX + a.lag / 4, t4);
+    // B starts after A's whole GEMM1: run together, the two halves share every SIMD's
+    // matrix pipe and reach their VALU phases together (measured: lag 0 / 8 / 12 K steps tie
+    // or lose)
+    rf2_wait(ctr + RF2_CG1 + 0, t4);
     gemm1(std::integral_constant<int, 1>{});
   }
   __builtin_amdgcn_s_setprio(0);
@@ -2238,31 +1136,14 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
 
   // ---- depthwise 5x5 in place: waves 2 cg and 2 cg + 1 own the two output halves of the
   // same 128 channels, so the read-before-overwrite hand-off is between those two only
-  const int NPF = (G == 0 && a.pf) ? 2 : 0;
-  uint32_t pf0 = 0, pf1 = 0;
-  // the depthwise of half B is on the workgroup's critical path (half A's GEMM2 waits for it at
-  // K step 8) and shares each SIMD with half A's GEMM2: rf_dwprio 1 issues it at priority 2
-  // over those MFMAs (2: both halves' depthwise)
-  const bool dwp = a.dwprio == 2 || (a.dwprio == 1 && half == 1);
-  if (dwp) __builtin_amdgcn_s_setprio(2);
   {
     const int kb0 = rf2_yblk(cg * 4 + (lane >> 4)), c0 = (lane & 15) >> 2, d0 = lane & 3;
     const int yb[4] = {kb0 * RF_KBS + (c0 << 2) + d0, kb0 * RF_KBS + ((c0 ^ 1) << 2) + d0,
                        kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
     uint32_t o0[25], o1[25];
-    auto prefetch = [&]() {  // rf_body's L2 prefetch of ROI + a.pf's X rows (reinforce workgroups)
-      if (G == 0 && a.pf) {
-        const int64_t rn = min(MODE == 2 ? roi + stride : roi + a.pf, a.R - 1);
-        const uint16_t* pa = a.X + rn * RF_S * 512 + (int64_t)tid * 64;
-        const uint16_t* pb = a.X + rn * RF_S * 512 + (int64_t)min(tid + 512, 799) * 64;
-        asm volatile("global_load_dword %0, %1, off" : "+v"(pf0) : "v"(pa) : "memory");
-        asm volatile("global_load_dword %0, %1, off" : "+v"(pf1) : "v"(pb) : "memory");
-      }
-    };
     if ((wave & 1) == 0) {
       rf_dw5q<0, 0>(Y, yb, wreg, o0);
       rf_dw5q<0, 1>(Y, yb, wreg, o1);
-      prefetch();
       rf2_signal(ctr + RF2_CDW + cg, lane);
       rf2_wait(ctr + RF2_CDW + cg, 2 * (it + 1));
       rf_dw5q_store<0, 0>(Y, yb, o0);
@@ -2270,14 +1151,12 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     } else {
       rf_dw5q<1, 0>(Y, yb, wreg, o0);
       rf_dw5q<1, 1>(Y, yb, wreg, o1);
-      prefetch();
       rf2_signal(ctr + RF2_CDW + cg, lane);
       rf2_wait(ctr + RF2_CDW + cg, 2 * (it + 1));
       rf_dw5q_store<1, 0>(Y, yb, o0);
       rf_dw5q_store<1, 1>(Y, yb, o1);
     }
   }
-  if (dwp) __builtin_amdgcn_s_setprio(0);
   rf2_signal(ctr + RF2_CY2 + half, lane);
   if (prof) pst[3] = eg_stamp();
 
@@ -2291,8 +1170,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
     u32x4(&b)[4] = bq[kt % 3];
-    rf_vmwait(kt + 1 < NK ? 4 + (kt < 2 ? NPF : 0) : 0, b);
-    if (kt == 2 && G == 0) asm volatile("" : "+v"(pf0), "+v"(pf1));  // retired by the wait above
+    rf_vmwait(kt + 1 < NK ? 4 : 0, b);
     if (kt == 0) rf2_wait(ctr + RF2_CY2 + 0, t4);
     if (kt == 8) rf2_wait(ctr + RF2_CY2 + 1, t4);
     if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
@@ -2323,59 +1201,11 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
         acc[i][t][2 * h + 1] = v.y;
       }
   }
-  if constexpr (MODE == 1) {
-    rf3_tail<G>(a, roi, smem, acc, lb, prof ? pst[0] : 0ull);
-    return;
-  } else {
-  if (a.sum_lanes) {
-    // every lane converts and stores one channel's sum (the butterfly leaves all 16 sums
-    // of a row group in every lane of it): one fixed-point conversion per lane instead of
-    // 16 on the lanes fr == 0; the same bits
-    const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
-    const float x = rf3_colsum(acc, fr);
-    if (a.sums) {
-      long long* o = a.sums + roi * kPart * 1024 + G * 512 + rf3_lane_ch(wave, fr, fc);
-      o[0] = llrintf(x * kFix);
-      for (int j = 1; j < cnt; ++j) o[j * 1024] = 0;
-    }
-    if (MODE == 2 && a.se_front) (G == 0 ? a.m_r : a.m_n)[roi * 512 + rf3_lane_ch(wave, fr, fc)] = rf3_mean(x);
-  } else
   {
-    const int cnt = (int)((r0 + RF_S - 1) / kPartRows - r0 / kPartRows) + 1;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float sv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) x += acc[i][t][e];
-        if (fr < 4) x += acc[6][t][e];
-        sv[e] = x;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        sv[e] += lane_xor1(sv[e]);
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x4E, 0xF, 0xF, true));  // ^2
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x128, 0xF, 0xF, true));  // row_ror 8
-        sv[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sv[e]), 0x124, 0xF, 0xF, true));  // row_ror 4
-      }
-      if (fr == 0) {
-        if (a.sums) {
-          long long* o = a.sums + roi * kPart * 1024 + G * 512 + wave * 64 + t * 16 + fc * 4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = llrintf(sv[e] * kFix);
-          for (int j = 1; j < cnt; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[j * 1024 + e] = 0;
-        }
-        if (MODE == 2 && a.se_front) {
-          float* m = (G == 0 ? a.m_r : a.m_n) + roi * 512 + wave * 64 + t * 16 + fc * 4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) m[e] = rf3_mean(sv[e]);
-        }
-      }
-    }
+    // every lane converts and stores one channel's squeeze mean (the butterfly leaves all 16
+    // sums of a row group in every lane of it)
+    const float x = rf_colsum(acc, fr);
+    (G == 0 ? a.m_r : a.m_n)[roi * 512 + rf_lane_ch(wave, fr, fc)] = rf_mean(x);
   }
   if (prof) pst[5] = eg_stamp();
   // ---- output staging: A over blocks 0..7 (X, dead once B is past GEMM1), B over Y(A)
@@ -2418,58 +1248,26 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, int64_t lb, unsigned c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pst[7] = eg_stamp();
     if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
-      unsigned long long* o = a.prof + ((roi * 2 + G) * 8 + wave) * 8;
+      unsigned long long* o = a.prof + ((roi * 2 + G) * 8 + wave) * 8;  // [ROI][group][wave][8]
       for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
       o[7] = pst[7] - pst[0];
     }
   }
-  }  // MODE != 1
-  if constexpr (MODE != 2) break;
   }  // ROI loop
-  if constexpr (MODE == 2 && G == 0) {
-    if (a.se_front == 1) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's m_r rows are in
-      g4_barrier();                                      // ... from every wave; LDS is free
-      rf_se_batches(a, smem, roi0, stride);
-    }
-  }
 }
 
-// workgroup (roi, g) = logical id 2 roi + g, XCD-remapped: a ROI's two groups run on one
-// XCD, so the second reads the ROI's X rows from L2
-__global__ void __launch_bounds__(512, 1) rmb_front_kernel(RfArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  if (lb & 1) rf_body<1>(a, lb, smem);
-  else rf_body<0>(a, lb, smem);
-}
-__global__ void __launch_bounds__(512, 1) rmb_front2_kernel(RfArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  if (lb & 1) rf2_body<1, 0>(a, lb, smem);
-  else rf2_body<0, 0>(a, lb, smem);
-}
-// fused: rmb_front + SE + transition; the grid is padded to a multiple of 16 workgroups so
-// xcd_remap never splits a ROI's pair across XCDs (the pair hands x_n over through L2)
-// persistent front (rf_v 3): 16 k workgroups; workgroup w sits on XCD w % 8, runs group
-// G = (w / 8) & 1 and the ROIs xcd + 8 (p + P k), p = w / 16, P = gridDim / 16 -- both groups of
-// a ROI on one XCD (its X rows read from HBM once), every ROI once
+// 16 k workgroups; workgroup w sits on XCD w % 8 (the dispatcher's round robin; for speed only,
+// nothing depends on it), runs group G = (w / 8) & 1 and the ROIs xcd + 8 (p + P k), p = w / 16,
+// P = gridDim / 16 -- both groups of a ROI on one XCD, every ROI once
 __global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int w = blockIdx.x, xcd = w & 7, slot = w >> 3;
   const int64_t P = gridDim.x / 16;
   const int64_t roi0 = xcd + 8 * (int64_t)(slot >> 1), stride = 8 * P;
-  if (slot & 1) rf2_body<1, 2>(a, 0, smem, roi0, stride);
-  else rf2_body<0, 2>(a, 0, smem, roi0, stride);
+  if (slot & 1) rf2_body<1>(a, smem, roi0, stride);
+  else rf2_body<0>(a, smem, roi0, stride);
 }
 
-__global__ void __launch_bounds__(512, 1) rmb_fused_kernel(RfArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  if ((lb >> 1) >= a.R) return;
-  if (lb & 1) rf2_body<1, 1>(a, lb, smem);
-  else rf2_body<0, 1>(a, lb, smem);
-}
 
 // ---------------------------------------------------------------------------
 // trans4 (trk_set_tuning("enc_trans", 1)): the transition (K = 1024, x_f = the first 512
@@ -2526,10 +1324,10 @@ __device__ __forceinline__ void seq_for(F&& f, std::integer_sequence<int, K...>)
   (f(std::integral_constant<int, K>{}), ...);
 }
 
-// OPT bit 0: s_setprio(1) over each step's MFMAs; bit 1: the step's B loads and A DMA issued
-// between its MFMAs (after row tiles 1 and 3) instead of after them; bit 2: the A fragments
-// read by asm with counted waits per row tile
-template <int SPS, int BD, int OPT = 0>
+// The step's B loads and A DMA are issued between its MFMAs (after row tiles 1 and 3), not
+// after them (235.4 vs 244.1 us isolated; measured and dropped: s_setprio(1) over the MFMAs,
+// 248.7; the A fragments read by asm with counted waits per row tile, a tie)
+template <int SPS, int BD>
 __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uint4* Wtp, int64_t ntiles) {
   static_assert(t4_vm_ok<SPS, BD>(), "trans4 vmcnt out of the rf_vmwait range");
   constexpr int NS = T4_NK / SPS, NSLOT = 3 * SPS;
@@ -2650,63 +1448,26 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
     constexpr int kt = decltype(ktc)::value;
     const uint4* buf = ring + (kt % NSLOT) * T4_BUF;
     bf8v afr[8];
-    if constexpr (OPT & 4) {
-      // the 8 fragment reads issued up front as asm; each row tile's MFMAs wait (counted
-      // lgkmcnt) for their own fragment only, as rf_mfma_step (the compiler's schedule read two,
-      // waited for everything, read six, waited again)
-      const uint32_t ab = lds_addr(buf + lterm);
-      u32x4 aq[8];
-      asm volatile("ds_read_b128 %0, %1" : "=v"(aq[0]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(aq[1]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(aq[2]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(aq[3]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(aq[4]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(aq[5]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(aq[6]) : "v"(ab) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:7168" : "=v"(aq[7]) : "v"(ab) : "memory");
 #pragma unroll
-      for (int i = 0; i < 8; ++i) afr[i] = __builtin_bit_cast(bf8v, aq[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + lterm + i * 64);
-    }
-    if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
+    for (int i = 0; i < 8; ++i) afr[i] = *reinterpret_cast<const bf8v*>(buf + lterm + i * 64);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if constexpr (OPT & 4) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (i == 0) asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(afr[0]));
-        else if (i == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(afr[1]));
-        else if (i == 2) asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(afr[2]));
-        else if (i == 3) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(afr[3]));
-        else if (i == 4) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(afr[4]));
-        else if (i == 5) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(afr[5]));
-        else if (i == 6) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(afr[6]));
-        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(afr[7]));
-      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], __builtin_bit_cast(bf8v, bq[kt % (BD + 1)][t]),
                                                             acc[i][t], 0, 0, 0);
-      if constexpr (OPT & 2) {
-        if (i == 1) {
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (kt + BD < T4_NK) loadB(kt + BD);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (i == 3) {
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      if (i == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kt + BD < T4_NK) loadB(kt + BD);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (i == 3) {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(OPT & 2)) {
-      if constexpr (kt + BD < T4_NK) loadB(kt + BD);
-      if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
-    }
     if constexpr (kt + 1 < T4_NK) {
       rf_vmwait(t4_vm<SPS, BD>(kt), bq[(kt + 1) % (BD + 1)]);
       if constexpr ((kt + 1) % SPS == 0) {
@@ -2807,13 +1568,8 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_gemm4: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, false, 0>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, true, 0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4_kernel<EPI, true, 1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS);
-
     attr = true;
   }
   EncGemmArgs b = a;
@@ -2823,15 +1579,9 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
   // to retire (DSC: ring or staging + partials, 74 KiB; transition: ring + the SE scales
   // of the slots a 128-row tile can span, 78 KiB at P = 100)
   const int tslots = std::min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
-  const size_t lds = !g_enc_lds_tight ? G4_LDS
-                    : EPI == EPI_DSC  ? std::max(G4_RING, G4_STAGE + G4_RED)
-                                      : std::max(G4_RING + (size_t)tslots * a.kscale * 4, (size_t)G4_RED);
-  if (g_enc_sums == 1)  // ROI sums on the MFMA (any P >= 43)
-    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 1>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
-  else if (a.P >= 64)
-    hipLaunchKernelGGL((gemm4_kernel<EPI, true, 0>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
-  else
-    hipLaunchKernelGGL((gemm4_kernel<EPI, false, 0>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
+  const size_t lds = EPI == EPI_DSC ? std::max(G4_RING, G4_STAGE + G4_RED)
+                                    : std::max(G4_RING + (size_t)tslots * a.kscale * 4, (size_t)G4_RED);
+  hipLaunchKernelGGL((gemm4_kernel<EPI>), dim3((unsigned)nwg), dim3(256), lds, st, b, nwg);
   return trk::check_launch("gemm4_kernel");
 }
 
@@ -2860,37 +1610,20 @@ extern "C" int trk_enc_sums_reduce(const long long* part, int64_t R, int64_t P, 
   return trk::check_launch("sums_reduce_kernel");
 }
 
-extern "C" int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
-                            int64_t ldc, void* stream) {
-  TRK_REQUIRE(M >= 0 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 && lda >= K && ldc >= N && lda % 8 == 0 &&
-                  ldc % 8 == 0,
-              "enc_gemm: need K %% 32 == 0, N %% 256 == 0, lda/ldc multiples of 8");
-  if (M == 0) return TRK_OK;
-  TRK_REQUIRE(A && B && C && aligned16(A) && aligned16(B) && aligned16(C), "enc_gemm: null or unaligned pointer");
-  EncGemmArgs a{};
-  a.A = (const uint16_t*)A; a.lda = lda;
-  a.B = (const uint16_t*)B; a.bias = nullptr;
-  a.C = (uint16_t*)C; a.ldc = ldc;
-  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = 1; a.groups = 1;
-  return launch<EPI_PLAIN, 256, 256>(a, reinterpret_cast<hipStream_t>(stream));
-}
-
 extern "C" int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2,
                                 const float* bias, int64_t Ng, void* XRN, long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && P <= 256 && Kg % BK == 0 && Kg > 0 && Ng % 128 == 0 && Ng > 0,
-              "enc_dsc_gemm: need 32 <= P <= 256, K %% 32 == 0, N %% 128 == 0");
+  TRK_REQUIRE(M >= 0 && P >= 43 && P <= 256 && Kg % BK == 0 && Kg > 0 && Ng % 256 == 0 && Ng > 0,
+              "enc_dsc_gemm: need 43 <= P <= 256, K %% 32 == 0, N %% 256 == 0");
   if (M == 0) return TRK_OK;
   TRK_REQUIRE(Y2 && W2 && bias && XRN && sums && aligned16(Y2) && aligned16(W2) && aligned16(XRN),
               "enc_dsc_gemm: null or unaligned pointer");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   EncGemmArgs a{};
   a.A = (const uint16_t*)Y2; a.lda = 2 * Kg;
   a.B = (const uint16_t*)W2; a.bias = bias;
   a.C = (uint16_t*)XRN; a.ldc = 2 * Ng;
   a.sums = sums; a.ld_sums = (int)(2 * Ng);
   a.M = (int)M; a.N = (int)Ng; a.K = (int)Kg; a.P = (int)P; a.groups = 2; a.kscale = 0;
-  if (g_enc_gemm == 1 && P >= 43 && Ng % 256 == 0) return launch4<EPI_DSC>(a, st);
-  return launch<EPI_DSC, 128, 128>(a, st);
+  return launch4<EPI_DSC>(a, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
@@ -2902,12 +1635,17 @@ extern "C" int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, in
 extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s,
                                         int64_t kscale, const void* Wt, const void* Wtp, const float* bias,
                                         int64_t N, long long* sums, void* stream) {
-  TRK_REQUIRE(M >= 0 && P >= 32 && P <= 256 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 &&
-                  kscale % BK == 0 && kscale <= K,
-              "enc_transition_gemm: need 32 <= P <= 256, K %% 32 == 0, N %% 256 == 0, kscale %% 32 == 0");
+  TRK_REQUIRE(M >= 0 && P >= 43 && P <= 256 && K % BK == 0 && K > 0 && N % 256 == 0 && N > 0 &&
+                  kscale % BK == 0 && kscale <= K && kscale * G4_SLOTS <= G4_SQ * 256 * 4,
+              "enc_transition_gemm: need 43 <= P <= 256, K %% 32 == 0, N %% 256 == 0, kscale %% 32 == 0, "
+              "kscale <= 512");
   if (M == 0) return TRK_OK;
   TRK_REQUIRE(XRN && s && Wt && bias && sums && aligned16(XRN) && aligned16(Wt) && aligned16(s),
               "enc_transition_gemm: null or unaligned pointer");
+  // the packed fragments (ops.enc_pack_fragments_k of Wt [N][K]) are trans4's operand image
+  // for exactly K = 1024, N = 512 (rf_loadB steps one K step as 32 column tiles)
+  TRK_REQUIRE(!Wtp || (K == 1024 && N == 512 && kscale == 512 && aligned16(Wtp)),
+              "enc_transition_gemm: packed Wt needs K = 1024, N = 512, kscale = 512 (16-byte aligned)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   EncGemmArgs a{};
   a.A = (const uint16_t*)XRN; a.lda = K;
@@ -2915,51 +1653,16 @@ extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, i
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  if (g_enc_gemm >= 1 && g_enc_trans == 1 && P >= 43 && K == 1024 && kscale == 512 && Wtp) {
+  if (g_enc_trans == 1 && Wtp) {
     const int64_t nwg = ((int64_t)M + 127) / 128 * (N / 256);
     TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
     a.prof = g_enc_prof;
     const size_t slds = (size_t)G4_SLOTS * 512 * 4;
-    const uint4* wp = reinterpret_cast<const uint4*>(Wtp);
-    if (g_t4_mode == 1)
-      hipLaunchKernelGGL((trans4_kernel<2, 2>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 2)
-      hipLaunchKernelGGL((trans4_kernel<1, 3>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 3)
-      hipLaunchKernelGGL((trans4_kernel<2, 3>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 4)
-      hipLaunchKernelGGL((trans4_kernel<1, 2, 1>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 5)
-      hipLaunchKernelGGL((trans4_kernel<1, 2, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 6)
-      hipLaunchKernelGGL((trans4_kernel<1, 2, 3>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 7)
-      hipLaunchKernelGGL((trans4_kernel<2, 3, 3>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 8)
-      hipLaunchKernelGGL((trans4_kernel<1, 2, 6>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else if (g_t4_mode == 9)
-      hipLaunchKernelGGL((trans4_kernel<2, 3, 6>), dim3((unsigned)nwg), dim3(256), 6 * T4_BUF * 16 + slds, st, a, wp, nwg);
-    else
-      hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a, wp, nwg);
+    hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a,
+                       reinterpret_cast<const uint4*>(Wtp), nwg);
     return trk::check_launch("trans4_kernel");
   }
-  if (g_enc_gemm >= 1 && g_enc_trans_wide && P >= 86 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) {
-    const int64_t nwg = ((int64_t)M + 255) / 256 * (N / 256);
-    TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm4w_trans_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
-    a.prof = g_enc_prof;
-    const int tslots = std::min(G4_SLOTS, (255 + (int)P - 1) / (int)P + 1);
-    const size_t lds = G4W_RING + (size_t)tslots * kscale * 4;
-    hipLaunchKernelGGL(gemm4w_trans_kernel, dim3((unsigned)nwg), dim3(512), lds, st, a, nwg);
-    return trk::check_launch("gemm4w_trans_kernel");
-  }
-  if (g_enc_gemm >= 1 && P >= 43 && kscale * G4_SLOTS <= G4_SQ * 256 * 4) return launch4<EPI_TRANS>(a, st);
-  return launch<EPI_TRANS, 128, 256>(a, st);
+  return launch4<EPI_TRANS>(a, st);
 }
 
 extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64_t N, const float* wdw, void* Y2,
@@ -2973,116 +1676,29 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
   TRK_REQUIRE(nwg < 0x7fffffff, "enc_g1_dwconv: too many workgroups");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel<true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(g1dw4_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G1Q_LDS);
     attr = true;
   }
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (g_g1dw == 6)
-    hipLaunchKernelGGL(g1dw4_kernel<true>, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
-                       (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
-  else
-    hipLaunchKernelGGL(g1dw4_kernel<false>, dim3((unsigned)nwg), dim3(256), G1Q_LDS, st,
-                       (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
+  hipLaunchKernelGGL(g1dw4_kernel, dim3((unsigned)nwg), dim3(256), G1Q_LDS, reinterpret_cast<hipStream_t>(stream),
+                     (const uint16_t*)X, (const uint16_t*)W1, wdw, (uint16_t*)Y2, (int)M, (int)N);
   return trk::check_launch("g1dw4_kernel");
-}
-
-namespace {
-struct FrontSe {  // trk_enc_rmb_front_se's SE operands (null: the plain front; w1 null: the means only)
-  const float *w1, *b1, *w2, *b2;
-  int64_t H;
-  float *m_r, *m_n, *s;
-};
-// grow-only device workspace of the two-launch fallbacks (rf_v 1 / 2)
-void* front_ws(size_t bytes) {
-  static void* ws = nullptr;
-  static size_t ws_n = 0;
-  if (bytes > ws_n) {
-    if (ws) (void)hipFree(ws);
-    ws = nullptr;
-    ws_n = 0;
-    if (hipMalloc(&ws, bytes) != hipSuccess) return nullptr;
-    ws_n = bytes;
-  }
-  return ws;
-}
-int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p, const float* bias,
-                     void* XRN, long long* sums, const FrontSe* se, void* stream);
-}  // namespace
-
-extern "C" int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                                 const float* bias, void* XRN, long long* sums, void* stream) {
-  return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sums, nullptr, stream);
-}
-
-extern "C" int trk_enc_rmb_front_se(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                                    const float* bias, void* XRN, long long* sums, const float* se_w1,
-                                    const float* se_b1, int64_t H, const float* se_w2, const float* se_b2, float* m_r,
-                                    float* m_n, float* s, void* stream) {
-  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front_se: 10x10 ROIs (M %% 100 == 0)");
-  if (M == 0) return TRK_OK;
-  TRK_REQUIRE(H > 0 && H % 16 == 0 && H <= 512, "enc_rmb_front_se: SE hidden size H a multiple of 16 in [16, 512]");
-  TRK_REQUIRE(se_w1 && se_b1 && se_w2 && se_b2 && m_r && m_n && s && aligned16(se_w1) && aligned16(se_w2) &&
-                  aligned16(m_r) && aligned16(m_n) && aligned16(s),
-              "enc_rmb_front_se: null or unaligned SE pointer");
-  if (g_rf_v == 3) {
-    const FrontSe se{se_w1, se_b1, se_w2, se_b2, H, m_r, m_n, s};
-    return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sums, &se, stream);
-  }
-  // the one-ROI-per-workgroup fronts: the front, then trk_enc_se on its sums (a grow-only
-  // workspace when the caller passes none)
-  long long* sp = sums;
-  if (!sp) {
-    sp = static_cast<long long*>(front_ws((size_t)(M / RF_S) * kPart * 1024 * sizeof(long long)));
-    TRK_REQUIRE(sp, "enc_rmb_front_se: workspace allocation");
-  }
-  if (int e = rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sp, nullptr, stream)) return e;
-  return trk_enc_se(sp, M / RF_S, 1024, RF_S, 512, se_w1, se_b1, H, se_w2, se_b2, m_r, m_n, s, stream);
 }
 
 extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                                        const float* bias, void* XRN, float* m_r, float* m_n, void* stream) {
-  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front_means: 10x10 ROIs (M %% 100 == 0)");
+  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front_means: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
   if (M == 0) return TRK_OK;
-  TRK_REQUIRE(m_r && m_n && aligned16(m_r) && aligned16(m_n), "enc_rmb_front_means: null or unaligned m_r / m_n");
-  if (g_rf_v == 3) {
-    const FrontSe se{nullptr, nullptr, nullptr, nullptr, 0, m_r, m_n, nullptr};
-    return rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, nullptr, &se, stream);
-  }
-  // the one-ROI-per-workgroup fronts: the front, then trk_enc_se's means phase on its sums (its
-  // s, into the workspace, is discarded)
-  const size_t nsum = (size_t)(M / RF_S) * kPart * 1024 * sizeof(long long);
-  char* ws = static_cast<char*>(front_ws(nsum + (size_t)(M / RF_S) * 512 * sizeof(float)));
-  TRK_REQUIRE(ws, "enc_rmb_front_means: workspace allocation");
-  long long* sp = reinterpret_cast<long long*>(ws);
-  if (int e = rmb_front_launch(X, M, W1p, wdw, W2p, bias, XRN, sp, nullptr, stream)) return e;
-  static float* zw = nullptr;  // a zero 16 x 512 SE (only the means are wanted)
-  if (!zw) {
-    TRK_REQUIRE(hipMalloc(&zw, (16 * 512 * 2 + 16 + 512) * sizeof(float)) == hipSuccess, "enc_rmb_front_means: alloc");
-    TRK_REQUIRE(hipMemset(zw, 0, (16 * 512 * 2 + 16 + 512) * sizeof(float)) == hipSuccess, "enc_rmb_front_means: alloc");
-  }
-  return trk_enc_se(sp, M / RF_S, 1024, RF_S, 512, zw, zw + 16 * 512 * 2, 16, zw + 16 * 512, zw + 16 * 512 * 2 + 16,
-                    m_r, m_n, reinterpret_cast<float*>(ws + nsum), stream);
-}
-
-namespace {
-int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p, const float* bias,
-                     void* XRN, long long* sums, const FrontSe* se, void* stream) {
-  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
-  if (M == 0) return TRK_OK;
-  TRK_REQUIRE(X && W1p && wdw && W2p && bias && XRN && (sums || se) && aligned16(X) && aligned16(W1p) &&
-                  aligned16(W2p) && aligned16(XRN) && aligned16(wdw),
-              "enc_rmb_front: null or unaligned pointer");
-  const int64_t nwg = M / RF_S * 2;
-  TRK_REQUIRE(nwg < 0x7fffffff, "enc_rmb_front: too many workgroups");
+  TRK_REQUIRE(X && W1p && wdw && W2p && bias && XRN && m_r && m_n && aligned16(X) && aligned16(W1p) &&
+                  aligned16(W2p) && aligned16(XRN) && aligned16(wdw) && aligned16(m_r) && aligned16(m_n),
+              "enc_rmb_front_means: null or unaligned pointer");
+  TRK_REQUIRE(M / RF_S < 0x7fffffff, "enc_rmb_front_means: too many ROIs");
+  // the CU count of the device the launch goes to (queried per call: a process may drive several)
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16) ncu = 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front2_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
     attr = true;
@@ -3095,98 +1711,19 @@ int rmb_front_launch(const void* X, int64_t M, const void* W1p, const float* wdw
   a.W2p = (const uint4*)W2p;
   a.bias = bias;
   a.XRN = (uint16_t*)XRN;
-  a.sums = sums;
+  a.m_r = m_r;
+  a.m_n = m_n;
   a.R = M / RF_S;
-  a.pf = g_rf_v == 3 ? g_rf3_pf : g_rf_pf;
   a.prof = g_enc_prof;
-  a.lag = g_rf_lag;
-  a.sum_lanes = g_rf_sumlanes;
-  a.dwprio = g_rf_dwprio;
-  if (se) {
-    a.se_front = se->w1 ? 1 : 2;
-    a.se_H = (int)se->H;
-    a.se_w1 = se->w1; a.se_b1 = se->b1; a.se_w2 = se->w2; a.se_b2 = se->b2;
-    a.m_r = se->m_r; a.m_n = se->m_n; a.s = se->s;
-  }
-  if (g_rf_v == 3) {
-    // persistent: 16 workgroups per 8 ROIs up to one per CU (a multiple of 16, so both groups
-    // of a ROI share an XCD)
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16) ncu = 16;
-    }
-    // (0: two CUs per XCD left free -- the tracker's and the ROI stream's kernels start there
-    // instead of waiting for a persistent workgroup to end: 2.03-2.05 vs 1.96-1.98M ROIs/s
-    // over four interleaved pairs against rf_v 2, where all 16 pairs measured a tie)
-    const int64_t groups =
-        std::min<int64_t>((a.R + 7) / 8, g_rf3_groups > 0 ? g_rf3_groups : std::max(1, ncu / 16 - 2));
-    hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups)), dim3(512), RF2_LDS,
-                       reinterpret_cast<hipStream_t>(stream), a);
-    return trk::check_launch("rmb_front3_kernel");
-  }
-  if (g_rf_v == 2) {
-    hipLaunchKernelGGL(rmb_front2_kernel, dim3((unsigned)nwg), dim3(512), RF2_LDS,
-                       reinterpret_cast<hipStream_t>(stream), a);
-    return trk::check_launch("rmb_front2_kernel");
-  }
-  hipLaunchKernelGGL(rmb_front_kernel, dim3((unsigned)nwg), dim3(512), RF_LDS, reinterpret_cast<hipStream_t>(stream),
-                     a);
-  return trk::check_launch("rmb_front_kernel");
-}
-}  // namespace
-
-extern "C" int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                                 const float* bias, const void* Wtp, const float* bt, const float* se_w1,
-                                 const float* se_b1, const float* se_w2, const float* se_b2, void* xn_work,
-                                 int* flags, int epoch, float* m_r, float* m_n, float* s, long long* tsums,
-                                 void* stream) {
-  TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_fused: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
-  if (M == 0) return TRK_OK;
-  TRK_REQUIRE(X && W1p && wdw && W2p && bias && Wtp && bt && se_w1 && se_b1 && se_w2 && se_b2 && xn_work && flags &&
-                  m_r && m_n && s && tsums,
-              "enc_rmb_fused: null pointer");
-  TRK_REQUIRE(aligned16(X) && aligned16(W1p) && aligned16(W2p) && aligned16(Wtp) && aligned16(wdw) &&
-                  aligned16(bt) && aligned16(se_w1) && aligned16(se_w2) && aligned16(xn_work) && aligned16(m_r) &&
-                  aligned16(m_n) && aligned16(s) && aligned16(tsums),
-              "enc_rmb_fused: operands must be 16-byte aligned");
-  TRK_REQUIRE(epoch != 0, "enc_rmb_fused: epoch must differ from the flags' initial 0");
-  const int64_t R = M / RF_S;
-  // pairs (2 roi, 2 roi + 1) stay on one XCD under xcd_remap when every XCD's range starts
-  // at an even id: a grid that is a multiple of 16 (the padding workgroups exit at once)
-  const int64_t nwg = (2 * R + 15) / 16 * 16;
-  TRK_REQUIRE(nwg < 0x7fffffff, "enc_rmb_fused: too many workgroups");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_fused_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF3_LDS);
-    attr = true;
-  }
-  RfArgs a;
-  memset(&a, 0, sizeof a);
-  a.X = (const uint16_t*)X;
-  a.W1p = (const uint4*)W1p;
-  a.wdw = wdw;
-  a.W2p = (const uint4*)W2p;
-  a.bias = bias;
-  a.R = R;
-  a.pf = g_rf_pf;
-  a.lag = g_rf_lag;
-  a.sum_lanes = g_rf_sumlanes;
-  a.dwprio = g_rf_dwprio;
-  a.Wtp = (const uint4*)Wtp;
-  a.bt = bt;
-  a.se_w1 = se_w1; a.se_b1 = se_b1; a.se_w2 = se_w2; a.se_b2 = se_b2;
-  a.XN = (uint16_t*)xn_work;
-  a.flags = flags;
-  a.epoch = epoch;
-  a.m_r = m_r; a.m_n = m_n; a.s = s;
-  a.tsums = tsums;
-  a.prof = g_enc_prof;
-  hipLaunchKernelGGL(rmb_fused_kernel, dim3((unsigned)nwg), dim3(512), RF3_LDS, reinterpret_cast<hipStream_t>(stream),
-                     a);
-  return trk::check_launch("rmb_fused_kernel");
+  // persistent: 16 workgroups per 8 ROIs up to one per CU (a multiple of 16, so both groups of a
+  // ROI share an XCD); rf3_groups 0 = two CUs per XCD left free -- the tracker's and the ROI
+  // stream's kernels start there instead of waiting for a persistent workgroup to end
+  // (2.03-2.05 vs 1.96-1.98M ROIs/s over four interleaved pairs against one ROI per workgroup)
+  const int64_t groups =
+      std::min<int64_t>((a.R + 7) / 8, g_rf3_groups > 0 ? g_rf3_groups : std::max(1, ncu / 16 - 2));
+  hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups)), dim3(512), RF2_LDS,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return trk::check_launch("rmb_front3_kernel");
 }
 
 // diagnostics: gemm4 per-workgroup phase stamps (8 u64 per workgroup); nullptr

@@ -36,10 +36,6 @@
 #include <type_traits>
 
 unsigned long long* g_lsap_prof = nullptr;  // trk_lsap_set_prof (diagnostics)
-int g_lsap_split = 0;  // trk_set_tuning("lsap_split"): trk_lsap_dev narrow + wide launches (see there;
-                       // measured r04: live stage-1 LSAP 95-100 vs 79-83 us, the pipeline 2.025-2.055 vs
-                       // 2.039-2.065M ROIs/s -- the wide launch's wait for a CU costs more than the
-                       // narrow kernel's 126 instead of 237 VGPRs saves)
 int g_lsap_dev_lds_kb = 24;  // trk_set_tuning("lsap_dev_lds_kb"): LDS budget of trk_lsap_dev workgroups.  Small
                              // enough to be placed beside the encoder's workgroups (a CU's whole LDS would wait for
                              // a CU free of them); the leading-row shortcut needs no ring, the sequential rows re-read
@@ -66,10 +62,6 @@ struct LsapArgs {
   const int32_t* dev_nr;  // trk_lsap_dev: shapes in device memory, bounded by nr_bound / nc_bound
   const int32_t* dev_nc;
   int nr_bound, nc_bound;
-  // trk_lsap_dev split launches: this launch solves the matrices whose column slots
-  // ks = ceil(max(nr, nc) / 64) satisfy ks_lo < ks <= ks_hi, the other launch the rest (the
-  // narrow launch, ks_lo == 0, also owns the empty and out-of-bound matrices)
-  int ks_lo, ks_hi;
   int nr[kMaxBatch];
   int nc[kMaxBatch];
 };
@@ -624,8 +616,6 @@ lsap_kernel(const LsapArgs A) {
     nr0 = A.dev_nr[f];
     nc0 = A.dev_nc[f];
     const bool out = nr0 < 0 || nc0 < 0 || nr0 > A.nr_bound || nc0 > A.nc_bound;
-    const int ks = out || nr0 == 0 || nc0 == 0 ? 0 : (max(nr0, nc0) + 63) >> 6;
-    if (A.ks_lo > 0 ? ks <= A.ks_lo : ks > A.ks_hi) return;  // the other launch's matrix
     if (out) {  // outside the launch's sizing
       if (assign)
         for (int r = threadIdx.x; r < A.nr_bound; r += blockDim.x) assign[r] = -1;
@@ -715,7 +705,6 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
     a.prof = g_lsap_prof ? g_lsap_prof + f0 * 16 : nullptr;
-    a.ks_hi = 1 << 20;
     int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                              : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
@@ -771,23 +760,8 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
     a.prof = g_lsap_prof ? g_lsap_prof + f0 * 16 : nullptr;
-    // split (lsap_split 1, off by default): the bound's kernel is sized for its widest matrix (at
-    // c3, 16 column slots: 237 VGPRs) while the frames' matrices fit 4 (126 VGPRs); the
-    // narrow kernel solves those and the wide launch only the wider ones (it exits at once
-    // when there are none)
-    const bool split = g_lsap_split && wc_max > 256;
-    a.ks_lo = 0;
-    a.ks_hi = split ? 4 : 1 << 20;
-    int e = 0;
-    if (split) {
-      e = dtype == TRK_F32 ? launch_ks<float>(256, dim3(nf), lds, st, a) : launch_ks<double>(256, dim3(nf), lds, st, a);
-      if (e) return e;
-      a.ks_lo = 4;
-      a.ks_hi = 1 << 20;
-      a.prof = nullptr;
-    }
-    e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
-                         : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
+    const int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
+                                   : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
   }
   return TRK_OK;

@@ -931,22 +931,9 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "roi_fma")) { TRK_REQUIRE(value == 0 || value == 1, "roi_fma in {0, 1}"); g_roi_fma = value; return TRK_OK; }
   if (!strcmp(key, "roi_wlds")) { TRK_REQUIRE(value == 0 || value == 1, "roi_wlds in {0, 1}"); g_roi_wlds = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
-  if (!strcmp(key, "rf_pf")) { extern int g_rf_pf; TRK_REQUIRE(value >= 0 && value <= 64, "rf_pf in [0, 64]"); g_rf_pf = value; return TRK_OK; }
-  if (!strcmp(key, "t4_mode")) { extern int g_t4_mode; TRK_REQUIRE(value >= 0 && value <= 9, "t4_mode in [0, 9]"); g_t4_mode = value; return TRK_OK; }
   if (!strcmp(key, "enc_trans")) { extern int g_enc_trans; TRK_REQUIRE(value == 0 || value == 1, "enc_trans in {0, 1}"); g_enc_trans = value; return TRK_OK; }
-  if (!strcmp(key, "enc_trans_wide")) { extern int g_enc_trans_wide; TRK_REQUIRE(value == 0 || value == 1, "enc_trans_wide in {0, 1}"); g_enc_trans_wide = value; return TRK_OK; }
-  if (!strcmp(key, "rf_sumlanes")) { extern int g_rf_sumlanes; TRK_REQUIRE(value == 0 || value == 1, "rf_sumlanes in {0, 1}"); g_rf_sumlanes = value; return TRK_OK; }
-  if (!strcmp(key, "rf_dwprio")) { extern int g_rf_dwprio; TRK_REQUIRE(value >= 0 && value <= 2, "rf_dwprio in {0, 1, 2}"); g_rf_dwprio = value; return TRK_OK; }
-  if (!strcmp(key, "rf_lag")) { extern int g_rf_lag; TRK_REQUIRE(value >= 0 && value <= 16 && value % 4 == 0, "rf_lag in {0, 4, 8, 12, 16}"); g_rf_lag = value; return TRK_OK; }
-  if (!strcmp(key, "rf3_pf")) { extern int g_rf3_pf; TRK_REQUIRE(value == 0 || value == 1, "rf3_pf in {0, 1}"); g_rf3_pf = value; return TRK_OK; }
   if (!strcmp(key, "rf3_groups")) { extern int g_rf3_groups; TRK_REQUIRE(value >= 0 && value <= 64, "rf3_groups in 0..64"); g_rf3_groups = value; return TRK_OK; }
-  if (!strcmp(key, "rf_v")) { extern int g_rf_v; TRK_REQUIRE(value >= 1 && value <= 3, "rf_v in {1, 2, 3}"); g_rf_v = value; return TRK_OK; }
-  if (!strcmp(key, "g1dw")) { extern int g_g1dw; TRK_REQUIRE(value == 4 || value == 6, "g1dw in {4, 6}"); g_g1dw = value; return TRK_OK; }
-  if (!strcmp(key, "enc_lds_tight")) { extern int g_enc_lds_tight; TRK_REQUIRE(value == 0 || value == 1, "enc_lds_tight in {0, 1}"); g_enc_lds_tight = value; return TRK_OK; }
-  if (!strcmp(key, "enc_sums")) { extern int g_enc_sums; TRK_REQUIRE(value == 0 || value == 1, "enc_sums in {0, 1}"); g_enc_sums = value; return TRK_OK; }
-  if (!strcmp(key, "enc_gemm")) { extern int g_enc_gemm; TRK_REQUIRE(value == 0 || value == 1, "enc_gemm in {0, 1}"); g_enc_gemm = value; return TRK_OK; }
   if (!strcmp(key, "dw_fast")) { extern int g_dw_fast; TRK_REQUIRE(value == 0 || value == 1, "dw_fast in {0,1}"); g_dw_fast = value; return TRK_OK; }
-  if (!strcmp(key, "lsap_split")) { extern int g_lsap_split; TRK_REQUIRE(value == 0 || value == 1, "lsap_split in {0, 1}"); g_lsap_split = value; return TRK_OK; }
   if (!strcmp(key, "lsap_dev_lds_kb")) { extern int g_lsap_dev_lds_kb; TRK_REQUIRE(value >= 8 && value <= 156, "lsap_dev_lds_kb in [8, 156]"); g_lsap_dev_lds_kb = value; return TRK_OK; }
   if (!strcmp(key, "roi_vec")) { TRK_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "roi_vec in {0,1,2,4}"); g_roi_vec = value; return TRK_OK; }
   trk::set_error("set_tuning: unknown key '%s'", key);

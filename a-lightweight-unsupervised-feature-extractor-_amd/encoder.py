@@ -109,20 +109,6 @@ class DeferredHead:
             return self._fn()
 
 
-class DeferredTail:
-    """The fused path after the front kernel, not yet enqueued on the producing stream:
-    the SE already runs on `Model.se_stream` (behind the front); `finish()` enqueues the
-    transition GEMM on the current stream (after the SE's event) and returns what the
-    forward would have (a DeferredHead, or the embeddings).  A caller that runs the next
-    frame's front before `finish()` takes the SE off the embedding stream's critical path."""
-
-    def __init__(self, fn):
-        self._fn = fn
-
-    def finish(self):
-        return self._fn()
-
-
 class Model(nn.Module):
     """encoderAndHead.Model(in_channels, out_channels, warmup_epochs, proj_dim)."""
 
@@ -186,7 +172,7 @@ class Model(nn.Module):
             w["b2"] = torch.cat([w["br"].float(), w["bn"].float()]).to(device, torch.float32)
             w["wt_nk"] = wt.contiguous().to(device, torch.bfloat16)                  # [C, 2C]
             if tuple(w["wt_nk"].shape) == (512, 1024):
-                from .ops import enc_pack_fragments_k                                # rmb_fused's GEMM3
+                from .ops import enc_pack_fragments_k                                # trans4's operand
                 w["wt_pk"] = enc_pack_fragments_k(w["wt_nk"])
             w["bt_f"] = r.transition[0].bias.float().to(device)
             w["bt"] = r.transition[0].bias.to(device, dtype)
@@ -234,31 +220,18 @@ class Model(nn.Module):
     # fp32 (the parity path) keeps hipBLASLt GEMMs + the separate act/mean passes
     fused_gemm = True
     fused_dwconv = True  # 10x10 bf16: depthwise 5x5 fused into the first GEMM (enc_g1_dwconv)
-    fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel
-                         # (enc_rmb_front; Y2 never reaches HBM); False: enc_g1_dwconv + enc_dsc_gemm
-    fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se / enc_head)
-    front_se = False     # with fused_front and fused_tail: the SE inside the front kernel (enc_rmb_front_se:
-                         # the persistent front's reinforce workgroups run it over their ROIs; no sums
-                         # round trip, no enc_se launch).  Measured r04: the front grows by the SE's
-                         # 36 us (two 16-row batches per workgroup) and the transition by 25 (the ROI
-                         # stage gated behind the front now lands on it alone): 2.011-2.021 vs
-                         # 2.029-2.058M ROIs/s, so off
-    front_means = True   # with fused_front and fused_tail (front_se off): the front writes the squeeze means
-                         # (enc_rmb_front_means) and the SE reads them (enc_se_means) -- no int64 sums
-                         # round trip, no means phase in the SE
-    fused_full = False   # with fused_front and fused_tail: the SE and the transition GEMM inside the
-                         # front kernel too (enc_rmb_fused; the [M, 1024] XRN never reaches HBM)
+    fused_front = True   # 10x10 bf16, C = 512: first GEMMs + depthwise + DSC GEMMs in one kernel that also
+                         # writes the SE's squeeze means (enc_rmb_front_means; Y2 never reaches HBM);
+                         # False: enc_g1_dwconv + enc_dsc_gemm (Y2 in HBM)
+    fused_tail = True    # bf16: SE + Shake2 mix + projection head as two trk kernels (enc_se(_means) / enc_head)
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
-    defer_tail = False   # fused front + tail: return a DeferredTail after the front; the SE runs on
-    se_stream = None     # se_stream behind the front, the transition only when the caller finishes it
     stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
                          # enqueued (a caller can record an event there to place other streams' work)
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
-        from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_gemm, enc_g1_dwconv, enc_dsc_gemm,
-                          enc_rmb_front, enc_rmb_front_se, enc_rmb_front_means, enc_rmb_fused, enc_transition_gemm,
-                          enc_se, enc_se_means, enc_head, enc_sums_reduce)
+        from .ops import (act_mean, dwconv5_nhwc, scale_rows, enc_g1_dwconv, enc_dsc_gemm, enc_rmb_front_means,
+                          enc_transition_gemm, enc_se, enc_se_means, enc_head, enc_sums_reduce)
         N, C, S1, S2 = x.shape
         dt, dev = x.dtype, x.device
         W = self._fused_weights(dt, dev)
@@ -267,47 +240,22 @@ class Model(nn.Module):
         ss = S1 * S2
         X = x.permute(0, 2, 3, 1).reshape(N * ss, C)                 # view when channels_last
         Co = W["w2r"].shape[1]
-        fused = (self.fused_gemm and dt == torch.bfloat16 and ss >= 32 and C % 32 == 0 and h4 % 256 == 0 and
+        # the trk GEMMs' tiles: a 128-row tile spans at most 4 ROIs (ss >= 43), N % 256 == 0
+        fused = (self.fused_gemm and dt == torch.bfloat16 and ss >= 43 and C % 32 == 0 and h4 % 256 == 0 and
                  h2 % 32 == 0 and Co % 256 == 0)
-        front = (fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_front and
-                 "w1_pk" in W and Co == 512)
-        if front and self.fused_tail and self.fused_full and "wt_pk" in W:
-            m_r, m_n, s, tsums = enc_rmb_fused(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"], W["wt_pk"], W["bt_f"],
-                                               W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
-            if self.stage_hook is not None:
-                self.stage_hook("g1")
-                self.stage_hook("dsc")
-            head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
-                                    self.head.net[1].eps, W["h4"], W["h4b"])
-            return DeferredHead(head, (tsums, s, m_r, m_n)) if self.defer_head else head()
-        se_out = None
-        if front and self.fused_tail and self.front_se and not (self.defer_tail and self.se_stream is not None):
-            XRN, _, m_r, m_n, s = enc_rmb_front_se(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"], W["se_w1"],
-                                                  W["se_b1"], W["se_w2"], W["se_b2"])
-            se_out = (m_r, m_n, s)
-            if self.stage_hook is not None:
-                self.stage_hook("g1")
-                self.stage_hook("dsc")
-        elif front and self.fused_tail and self.front_means and not (self.defer_tail and self.se_stream is not None):
+        ten = fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous()
+        front = ten and self.fused_front and "w1_pk" in W and Co == 512
+        if front:
             XRN, m_r, m_n = enc_rmb_front_means(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
             if self.stage_hook is not None:
                 self.stage_hook("g1")
                 self.stage_hook("dsc")
-            se_out = (m_r, m_n, enc_se_means(m_r, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"]))
-        elif front:
-            XRN, sums = enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
-            if self.stage_hook is not None:
-                self.stage_hook("g1")
-                self.stage_hook("dsc")
-        elif fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous() and self.fused_dwconv:
+        elif ten and self.fused_dwconv:
             Y2 = enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])               # first 1x1 convs + depthwise 5x5, one kernel
             if self.stage_hook is not None:
                 self.stage_hook("g1")
         else:
-            if fused:
-                Y1 = enc_gemm(X, W["w1_nk"]).view(N, S1, S2, h4)     # 4 first 1x1 convs, one GEMM
-            else:
-                Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)
+            Y1 = (X @ W["w1t"]).view(N, S1, S2, h4)                    # 4 first 1x1 convs, one GEMM (hipBLASLt)
             Y2 = dwconv5_nhwc(Y1, W["dw_t"]).view(N * ss, h4)         # 4 depthwise 5x5, one kernel
         if fused:
             # DSC pair + SE squeeze + GAP(x_n) in one GEMM; SE excitation + transition
@@ -316,33 +264,13 @@ class Model(nn.Module):
                 XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
                 if self.stage_hook is not None:
                     self.stage_hook("dsc")
-            if self.fused_tail and front and self.defer_tail and self.se_stream is not None:
-                e_front = torch.cuda.Event()
-                e_front.record()
-                se_st = self.se_stream
-                with torch.cuda.stream(se_st):
-                    se_st.wait_event(e_front)
-                    sums.record_stream(se_st)
-                    m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
-                    e_se = torch.cuda.Event()
-                    e_se.record(se_st)
-                defer_head = self.defer_head
-
-                def finish():
-                    st = torch.cuda.current_stream()
-                    st.wait_event(e_se)
-                    for t in (m_r, m_n, s):
-                        t.record_stream(st)
-                    tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True, Wtp=W.get("wt_pk"))
-                    head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
-                                            self.head.net[1].eps, W["h4"], W["h4b"])
-                    return DeferredHead(head, (tsums, s, m_r, m_n)) if defer_head else head()
-                return DeferredTail(finish)
             if self.fused_tail:
-                # squeeze means + SE MLP (unless the front ran them), then Shake2 mix + projection
-                # head: one kernel each
-                m_r, m_n, s = se_out if se_out is not None else enc_se(sums, ss, W["se_w1"], W["se_b1"],
-                                                                      W["se_w2"], W["se_b2"])
+                # SE MLP (+ the squeeze means unless the front wrote them), then Shake2 mix +
+                # projection head: one kernel each
+                if front:
+                    s = enc_se_means(m_r, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+                else:
+                    m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
                 tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True, Wtp=W.get("wt_pk"))
                 head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
                                         self.head.net[1].eps, W["h4"], W["h4b"])
@@ -353,8 +281,9 @@ class Model(nn.Module):
                 # this stream (the next frame's ROI Align / first GEMM) then fill the rest of
                 # the GPU beside it
                 return DeferredHead(head, (tsums, s, m_r, m_n))
-            f = enc_sums_reduce(sums, ss)
-            m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
+            if not front:  # (the front wrote m_r / m_n)
+                f = enc_sums_reduce(sums, ss)
+                m_r, m_n = f[:, :Co] / ss, f[:, Co:] / ss
             s = self._se(m_r)
             m_cat = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], Wtp=W.get("wt_pk")) / ss
             a = self._alpha()

@@ -126,26 +126,10 @@ def scale_rows(x: torch.Tensor, s: torch.Tensor, act: Optional[str] = None) -> t
 _FIX = 2.0 ** -24
 
 
-def enc_gemm(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
-    """bf16 C[M, N] = A[M, K] . B[N, K]^T (A rows may be strided; B = [out, in] weights)."""
-    _need_gpu(A, "enc_gemm")
-    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16:
-        raise TypeError("enc_gemm: bf16 operands required")
-    if A.dim() != 2 or A.stride(1) != 1:
-        raise ValueError("enc_gemm: A must be [M, K] with unit column stride")
-    M, K = A.shape
-    N, K2 = B.shape
-    if K2 != K:
-        raise ValueError("enc_gemm: shape mismatch")
-    B = B.contiguous()
-    C = torch.empty((M, N), device=A.device, dtype=torch.bfloat16)
-    check(lib().trk_enc_gemm(_ptr(A), M, K, A.stride(0), _ptr(B), N, _ptr(C), N, _stream(A.device)), "enc_gemm")
-    return C
-
-
 def enc_g1_dwconv(X: torch.Tensor, W1: torch.Tensor, wdw: torch.Tensor) -> torch.Tensor:
     """bf16: dwconv5(X . W1^T) for 10x10 ROIs: X [R*100, 512] rows, W1 [N, 512],
-    wdw tap-major [25, N] f32 -> Y2 [R*100, N] (== enc_gemm then dwconv5_nhwc)."""
+    wdw tap-major [25, N] f32 -> Y2 [R*100, N] (the four first 1x1 convs of the RMB as one
+    GEMM, Y1 rounded to bf16, then the 1024-channel depthwise 5x5)."""
     _need_gpu(X, "enc_g1_dwconv")
     if X.dtype != torch.bfloat16 or W1.dtype != torch.bfloat16:
         raise TypeError("enc_g1_dwconv: bf16 operands required")
@@ -186,8 +170,8 @@ def enc_dsc_gemm(Y2: torch.Tensor, P: int, W2: torch.Tensor, bias: torch.Tensor,
 
 
 def enc_pack_fragments_k(W: torch.Tensor) -> torch.Tensor:
-    """[N, K] bf16 weights -> the 16x16x32 MFMA A-fragment order of trk_enc_rmb_fused's
-    transition: [K/32 k steps][N/16 col tiles][64 lanes][8], element (s, n, l, j) =
+    """[N, K] bf16 weights -> the 16x16x32 MFMA A-fragment order the trans4 transition reads:
+    [K/32 k steps][N/16 col tiles][64 lanes][8], element (s, n, l, j) =
     W[16n + l%16][32s + 8(l//16) + j]."""
     N, K = W.shape
     W = W.reshape(N // 16, 16, K // 32, 4, 8)                 # n, fr, s, fc, j
@@ -196,72 +180,10 @@ def enc_pack_fragments_k(W: torch.Tensor) -> torch.Tensor:
 
 def enc_pack_fragments(W: torch.Tensor) -> torch.Tensor:
     """[2*512, 512] (or [2, 512, 512]) bf16 weights [N][K] -> the 16x16x32 MFMA
-    fragment order trk_enc_rmb_front reads: [2][16 k steps][32 col tiles][64 lanes][8],
+    fragment order trk_enc_rmb_front_means reads: [2][16 k steps][32 col tiles][64 lanes][8],
     element (g, s, n, l, j) = W[g*512 + 16n + l%16][32s + 8(l//16) + j]."""
     W = W.reshape(2, 32, 16, 16, 4, 8)                 # g, n, fr, s, fc, j
     return W.permute(0, 3, 1, 4, 2, 5).contiguous()    # g, s, n, fc, fr, j  (lane = 16 fc + fr)
-
-
-def enc_rmb_front(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
-                  bias: torch.Tensor):
-    """bf16, 10x10 ROIs of 512 channels: enc_g1_dwconv + enc_dsc_gemm in one kernel
-    (Y2 stays in LDS).  X [R*100, 512], W1p / W2p from enc_pack_fragments, wdw [25, 1024]
-    f32, bias [1024] f32 -> (XRN [R*100, 1024], raw sums [R, TRK_ENC_PARTS, 1024])."""
-    _need_gpu(X, "enc_rmb_front")
-    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
-        raise TypeError("enc_rmb_front: bf16 operands required")
-    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
-        raise ValueError("enc_rmb_front: X must be contiguous [R*100, 512]")
-    pk = (2, 16, 32, 4, 16, 8)  # enc_pack_fragments' layout (an unpacked [1024, 512] has the same numel)
-    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or not (W1p.is_contiguous() and W2p.is_contiguous()):
-        raise ValueError("enc_rmb_front: W1p / W2p must be enc_pack_fragments output [2, 16, 32, 4, 16, 8]")
-    if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
-        raise ValueError("enc_rmb_front: wdw [25, 1024] f32 and bias [1024] required")
-    M = X.shape[0]
-    XRN = torch.empty((M, 1024), device=X.device, dtype=torch.bfloat16)
-    sums = torch.empty((M // 100, _lib.TRK_ENC_PARTS, 1024), device=X.device, dtype=torch.int64)
-    check(lib().trk_enc_rmb_front(_ptr(X), M, _ptr(W1p), _ptr(wdw.contiguous()), _ptr(W2p),
-                                  _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(sums),
-                                  _stream(X.device)), "enc_rmb_front")
-    return XRN, sums
-
-
-def enc_rmb_fused(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor, bias: torch.Tensor,
-                  Wtp: torch.Tensor, bt: torch.Tensor, se_w1: torch.Tensor, se_b1: torch.Tensor,
-                  se_w2: torch.Tensor, se_b2: torch.Tensor):
-    """enc_rmb_front + enc_se + enc_transition_gemm in one kernel (bf16, 10x10 ROIs of 512
-    channels): X [R*100, 512]; W1p / W2p from enc_pack_fragments, Wtp = enc_pack_fragments_k(Wt
-    [512, 1024]); wdw [25, 1024], bias [1024], bt [512], SE weights f32 -> (m_r, m_n, s [R, 512]
-    f32, tsums [R, TRK_ENC_PARTS, 512] int64): enc_se's and enc_transition_gemm(raw=True)'s
-    outputs, for enc_head."""
-    _need_gpu(X, "enc_rmb_fused")
-    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16 or \
-            Wtp.dtype != torch.bfloat16:
-        raise TypeError("enc_rmb_fused: bf16 operands required")
-    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
-        raise ValueError("enc_rmb_fused: X must be contiguous [R*100, 512]")
-    pk = (2, 16, 32, 4, 16, 8)
-    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or tuple(Wtp.shape) != (32, 32, 4, 16, 8):
-        raise ValueError("enc_rmb_fused: W1p / W2p [2, 16, 32, 4, 16, 8] (enc_pack_fragments), "
-                         "Wtp [32, 32, 4, 16, 8] (enc_pack_fragments_k)")
-    if wdw.shape != (25, 1024) or bias.numel() != 1024 or bt.numel() != 512 or tuple(se_w1.shape) != (128, 512) \
-            or tuple(se_w2.shape) != (512, 128) or se_b1.numel() != 128 or se_b2.numel() != 512:
-        raise ValueError("enc_rmb_fused: shape mismatch")
-    M = X.shape[0]
-    R = M // 100
-    dev = X.device
-    # per call: the hand-off workspace and flags (zeroed: epoch 1 is then fresh), so launches
-    # on different streams never share them
-    xn = torch.empty((M, 512), device=dev, dtype=torch.bfloat16)
-    flags = torch.zeros(max(R, 1) * 4, device=dev, dtype=torch.int32)  # [R][4]: x_n, m_r, s published
-    out = torch.empty((3, R, 512), device=dev, dtype=torch.float32)
-    tsums = torch.empty((R, _lib.TRK_ENC_PARTS, 512), device=dev, dtype=torch.int64)
-    c = lambda t: _f32c(t)
-    check(lib().trk_enc_rmb_fused(_ptr(X), M, _ptr(W1p), _ptr(c(wdw)), _ptr(W2p), _ptr(c(bias)), _ptr(Wtp),
-                                  _ptr(c(bt)), _ptr(c(se_w1)), _ptr(c(se_b1)), _ptr(c(se_w2)), _ptr(c(se_b2)),
-                                  _ptr(xn), _ptr(flags), 1, _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _ptr(tsums),
-                                  _stream(dev)), "enc_rmb_fused")
-    return out[0], out[1], out[2], tsums
 
 
 def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Tensor,
@@ -279,8 +201,9 @@ def enc_transition_gemm(XRN: torch.Tensor, P: int, s: torch.Tensor, Wt: torch.Te
     R = (M + P - 1) // P
     if K2 != K or s.shape[0] != R or bias.numel() != N:
         raise ValueError("enc_transition_gemm: shape mismatch")
-    if Wtp is not None and (Wtp.dtype != torch.bfloat16 or Wtp.numel() != Wt.numel() or not Wtp.is_contiguous()):
-        raise ValueError("enc_transition_gemm: Wtp must be enc_pack_fragments_k(Wt)")
+    if Wtp is not None and (Wtp.dtype != torch.bfloat16 or not Wtp.is_contiguous() or
+                            tuple(Wtp.shape) != (K // 32, N // 16, 4, 16, 8) or (N, K) != (512, 1024)):
+        raise ValueError("enc_transition_gemm: Wtp must be enc_pack_fragments_k(Wt) of a [512, 1024] Wt")
     XRN, Wt = XRN.contiguous(), Wt.contiguous()
     s, bias = s.to(torch.float32).contiguous(), bias.to(torch.float32).contiguous()
     sums = torch.empty((R, _lib.TRK_ENC_PARTS, N), device=XRN.device, dtype=torch.int64)  # partials
@@ -305,43 +228,13 @@ def enc_sums_reduce(part: torch.Tensor, P: int) -> torch.Tensor:
     return out
 
 
-def enc_rmb_front_se(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
-                     bias: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
-                     b2: torch.Tensor, want_sums: bool = False):
-    """enc_rmb_front + enc_se in one launch (trk_enc_rmb_front_se): returns (XRN, sums or
-    None, m_r, m_n, s) -- XRN as enc_rmb_front's, m_r / m_n / s bit-identical to enc_se on
-    its sums (card.py:59-78).  want_sums: also write the raw partial sums."""
-    _need_gpu(X, "enc_rmb_front_se")
-    if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
-        raise TypeError("enc_rmb_front_se: bf16 operands required")
-    if X.dim() != 2 or not X.is_contiguous() or X.shape[1] != 512 or X.shape[0] % 100:
-        raise ValueError("enc_rmb_front_se: X must be contiguous [R*100, 512]")
-    pk = (2, 16, 32, 4, 16, 8)
-    if tuple(W1p.shape) != pk or tuple(W2p.shape) != pk or not (W1p.is_contiguous() and W2p.is_contiguous()):
-        raise ValueError("enc_rmb_front_se: W1p / W2p must be enc_pack_fragments output [2, 16, 32, 4, 16, 8]")
-    if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
-        raise ValueError("enc_rmb_front_se: wdw [25, 1024] f32 and bias [1024] required")
-    H, C = w1.shape
-    if C != 512 or w2.shape != (512, H) or b1.numel() != H or b2.numel() != 512:
-        raise ValueError("enc_rmb_front_se: SE weights w1 [H, 512], b1 [H], w2 [512, H], b2 [512]")
-    M = X.shape[0]
-    R = M // 100
-    XRN = torch.empty((M, 1024), device=X.device, dtype=torch.bfloat16)
-    sums = (torch.empty((R, _lib.TRK_ENC_PARTS, 1024), device=X.device, dtype=torch.int64) if want_sums else None)
-    out = torch.empty((3, R, 512), device=X.device, dtype=torch.float32)
-    w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
-    check(lib().trk_enc_rmb_front_se(_ptr(X), M, _ptr(W1p), _ptr(wdw.contiguous()), _ptr(W2p),
-                                     _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(sums),
-                                     _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2), _ptr(out[0]), _ptr(out[1]),
-                                     _ptr(out[2]), _stream(X.device)), "enc_rmb_front_se")
-    return XRN, sums, out[0], out[1], out[2]
-
-
 def enc_rmb_front_means(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
                         bias: torch.Tensor):
-    """enc_rmb_front writing the squeeze means instead of the raw sums
-    (trk_enc_rmb_front_means): returns (XRN, m_r, m_n) -- m_r / m_n bit-identical to
-    enc_se's on enc_rmb_front's sums."""
+    """bf16, 10x10 ROIs of 512 channels: enc_g1_dwconv + enc_dsc_gemm in one kernel
+    (trk_enc_rmb_front_means; Y2 stays in LDS).  X [R*100, 512], W1p / W2p from
+    enc_pack_fragments, wdw [25, 1024] f32, bias [1024] f32 -> (XRN [R*100, 1024], m_r, m_n
+    [R, 512] f32): XRN bit-identical to the two-kernel path, m_r / m_n the squeeze means
+    enc_se takes (of the kernel's own f32 column sums)."""
     _need_gpu(X, "enc_rmb_front_means")
     if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
         raise TypeError("enc_rmb_front_means: bf16 operands required")

@@ -211,12 +211,6 @@ class Pipeline:
         self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
                            if os.environ.get("TRK_ROI_STREAM", "1") == "1" else None)
         self.roi_pending = {}
-        # TRK_SE_DEFER=1: the encoder stops after the front kernel; the SE runs on a stream of its
-        # own behind it and frame f's transition is enqueued after frame f+1's front, so the SE
-        # is off the embedding stream (which then runs front(f+1), transition(f), front(f+2), ...)
-        self.defer_tail = (os.environ.get("TRK_SE_DEFER", "0") == "1" and self.defer_head and n_side == 1)
-        self.se_stream = torch.cuda.Stream(device=sc["feat"].device) if self.defer_tail else None
-        self.tails = {}  # frame -> DeferredTail (front enqueued, transition not yet)
         # TRK_ROI_AFTER=g1|dsc: frame f+1's ROI Align waits for frame f's first GEMM / DSC GEMM
         # (an event recorded through encoder.Model.stage_hook), so it runs beside the
         # encoder's later kernels instead of as soon as it is enqueued
@@ -290,9 +284,8 @@ class Pipeline:
             return self.model(roi).view(self.sc["streams"], self.sc["N"], 128)
 
     def embed_async(self, f):
-        """enqueue frame f's roi_align + encoder on the side stream (deferred tail: frame f's
-        front, then frame f-1's transition)"""
-        if f in self.pending or f in self.tails or f >= len(self.sc["rois"]):
+        """enqueue frame f's roi_align + encoder on the side stream"""
+        if f in self.pending or f >= len(self.sc["rois"]):
             return
         main = torch.cuda.current_stream()
         side = self.sides[f % len(self.sides)]
@@ -309,7 +302,6 @@ class Pipeline:
             else:
                 roi = self._roi_for(f, side)
                 self.model.defer_head = self.defer_head
-                self.model.defer_tail, self.model.se_stream = self.defer_tail, self.se_stream
                 try:
                     if self.defer_head:
                         with torch.no_grad():
@@ -318,13 +310,7 @@ class Pipeline:
                         emb = self.stage_embed(roi)
                 finally:
                     self.model.defer_head = False
-                    self.model.defer_tail, self.model.se_stream = False, None
                 self._roi_ahead(f + 1)
-                if hasattr(emb, "finish"):  # deferred tail: the previous frame's transition now
-                    self.tails[f] = emb
-                    if f - 1 in self.tails:
-                        self._finish_tail(f - 1)
-                    return
                 if hasattr(emb, "launch"):  # deferred head: launched by _step on the tracker's stream
                     self.pending[f] = (emb, None)
                     return
@@ -333,12 +319,6 @@ class Pipeline:
             ev.record(side)
         emb.record_stream(main)
         self.pending[f] = (emb, ev)
-
-    def _finish_tail(self, f):
-        """enqueue frame f's transition (and leave its head deferred) on its embedding stream"""
-        side = self.sides[f % len(self.sides)]
-        with torch.cuda.stream(side), torch.no_grad():
-            self.pending[f] = (self.tails.pop(f).finish(), None)
 
     def _roi_ahead(self, f):
         """ROI Align of frame f on its own stream, now: it runs beside the encoder
@@ -373,10 +353,6 @@ class Pipeline:
     def _step(self, f):
         sc = self.sc
         self.embed_async(f)
-        if self.defer_tail:
-            self.embed_async(f + 1)  # frame f+1's front, then frame f's transition
-            if f in self.tails:  # no frame after f: its transition now
-                self._finish_tail(f)
         emb, ev = self.pending.pop(f)
         if ev is None:  # deferred head: launched here, on the tracker's stream, before the step
             with torch.no_grad():
@@ -414,6 +390,32 @@ class Pipeline:
 
 
 # ----------------------------------------------------------- measurement --
+class ProfRegion:
+    """rocprofv3 --selected-regions support: the profiler collects only between
+    roctxProfilerResume(0) and roctxProfilerPause(0).  TRK_PROF_REGION picks the region this
+    run opens: "timed" (default: exactly the timed region's launches, after its opening
+    barrier + sync, closed after its closing sync) or "isolated" (kernel_pass, the
+    back-to-back launches after it).  Without rocprofv3's selected-regions mode (its
+    ROCPROF_SELECTED_REGIONS in the environment) every call is a no-op."""
+
+    def __init__(self):
+        self.which = os.environ.get("TRK_PROF_REGION", "timed")
+        self._lib = None
+        if os.environ.get("ROCPROF_SELECTED_REGIONS", "").lower() in ("1", "true", "yes", "on"):
+            lib = ctypes.CDLL("librocprofiler-sdk-roctx.so")
+            lib.roctxProfilerResume.argtypes = lib.roctxProfilerPause.argtypes = [ctypes.c_uint64]
+            self._lib = lib
+            self.pause()  # the preload starts collecting: nothing before the chosen region
+
+    def resume(self, which):
+        if self._lib is not None and which == self.which:
+            self._lib.roctxProfilerResume(0)
+
+    def pause(self):
+        if self._lib is not None:
+            self._lib.roctxProfilerPause(0)
+
+
 def _ev():
     return torch.cuda.Event(enable_timing=True)
 
@@ -429,9 +431,7 @@ class LiveProbe:
     NAMES = {"trk_roi_align_fwd": "roi_stage", "trk_nchw_to_nhwc": "map_nhwc", "trk_enc_g1_dwconv": "enc_g1_dwconv",
              "trk_enc_dsc_gemm": "enc_gemm_dsc", "trk_enc_transition_gemm": "enc_gemm_trans",
              "trk_enc_transition_gemm2": "enc_gemm_trans",
-             "trk_enc_rmb_front": "enc_rmb_front", "trk_enc_rmb_front_se": "enc_rmb_front",
              "trk_enc_rmb_front_means": "enc_rmb_front", "trk_enc_se_means": "enc_se",
-             "trk_enc_rmb_fused": "enc_rmb_fused",
              "trk_enc_se": "enc_se", "trk_enc_head": "enc_head", "trk_build_cost": "cost_live",
              "trk_lsap": "lsap_live", "trk_build_cost_dev": "cost_live", "trk_lsap_dev": "lsap_live",
              "trk_step_begin": "step_begin", "trk_step_mid": "step_mid", "trk_step_end": "step_end",
@@ -505,12 +505,10 @@ class LiveProbe:
         on purpose)"""
         if n_side != 1:
             return None
-        fused = bool(self.ev.get("enc_rmb_fused"))
-        ends = self.ev[("enc_rmb_fused" if fused else "enc_gemm_trans") if head_deferred else "enc_head"]
+        ends = self.ev["enc_gemm_trans" if head_deferred else "enc_head"]
         first = "roi_stage"
         if roi_own_stream:
-            first = ("enc_rmb_fused" if fused else
-                     "enc_rmb_front" if self.ev.get("enc_rmb_front") else "enc_g1_dwconv")
+            first = "enc_rmb_front" if self.ev.get("enc_rmb_front") else "enc_g1_dwconv"
         starts = self.ev[first]
         gaps = [e1.elapsed_time(s0) * 1e3 for (_, e1), (s0, _) in zip(ends, starts[1:])]
         return float(np.mean(gaps)) if gaps else None
@@ -544,10 +542,7 @@ def kernel_pass(pipe, f, reps=10):
     K = roi.shape[0]
     X = roi.permute(0, 2, 3, 1).reshape(K * 100, 512)
     if "w1_pk" in W:
-        timed("enc_rmb_front", lambda: ops.enc_rmb_front(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"]))
-    if "wt_pk" in W:
-        timed("enc_rmb_fused", lambda: ops.enc_rmb_fused(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"], W["wt_pk"],
-                                                         W["bt_f"], W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"]))
+        timed("enc_rmb_front", lambda: ops.enc_rmb_front_means(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"]))
     timed("enc_g1_dwconv", lambda: ops.enc_g1_dwconv(X, W["w1_nk"], W["dw_t"]))
     Y2 = ops.enc_g1_dwconv(X, W["w1_nk"], W["dw_t"])
     timed("enc_gemm_dsc", lambda: ops.enc_dsc_gemm(Y2, 100, W["w2_nk"], W["b2"]))
@@ -594,58 +589,35 @@ def _cpu_info():
     return model, cores
 
 
-def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
-    """The reference's CPU path on this box's host cores, two modes (SURVEY.md
-    8(d)), same inputs, 3 warm-up frames, per-frame medians:
-      vectorised        oracle roi_align (C restatement of torchvision's CPU
-                        kernel, 1 thread) + the fp32 encoder in plain torch
-                        (all torch threads) + the oracle's vectorised cost incl.
-                        gate (C, 1 thread) + scipy.optimize.linear_sum_assignment
-      reference_literal the same roi_align / encoder / LSAP with the cost as the
-                        reference's Python computes it: the per-track top-k loop
-                        (mainTracking.py:173-210) and the per-pair 4x4-inverse
-                        gating loop (:327-336) -- oracle/literal.py
-    One stream at N=256 (tracks = the stream's objects, banks of 30).  The
-    literal mode's loops take seconds per frame, so its cost stage is sampled on
-    frames_lit frames (the stages are timed separately and the medians added).
-    Threads: every physical core, capped by OMP_NUM_THREADS where the box sets it
-    (16 on a one-GPU gpurun box: that GPU's CPU share); torch and the oracle's
-    OpenMP loops (roi_align over ROIs, cost over track rows) use the same count."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as O
-    import literal as LIT
-    from scipy.optimize import linear_sum_assignment
+def _cpu_leg(sc, sd, O, LIT, lsa, N, S, frames_vec, frames_lit, budget_s):
+    """One CPU leg: the first N detections of one stream per frame (tracks = those objects,
+    banks of 30), S x S ROIs; returns per-stage medians (s) and the frame counts."""
     npw = sc["np"]
-    N = sc["N"]
+    Ns = sc["N"]
     rng = np.random.default_rng(7)
     bank = rng.standard_normal((N, 30, 128)).astype(np.float32)
     bank /= np.linalg.norm(bank, axis=-1, keepdims=True)
     gm = np.zeros((N, 4)); gs = np.tile(np.eye(4).reshape(1, 16) / 11.0, (N, 1))
     kf_x = [np.zeros(8) for _ in range(N)]
     kf_P = [np.diag([10.0] * 4 + [1000.0] * 4) for _ in range(N)]
-    model, cores = _cpu_info()
-    cap = os.environ.get("OMP_NUM_THREADS")
-    thr = min(int(cap), cores or int(cap)) if cap else (cores or os.cpu_count() or 1)
-    torch.set_num_threads(thr)
-    os.environ.setdefault("OMP_NUM_THREADS", str(thr))  # the oracle's OpenMP (read at its first parallel loop)
     t_roi, t_enc, t_cost, t_lsap, t_lit = [], [], [], [], []
     t_start = time.perf_counter()
     for q in range(3 + frames_vec):
         f = (PREROLL + q) % len(npw["rois"])
-        s = q % sc["streams"]
-        rois = npw["rois"][f, s * N:(s + 1) * N].copy()
+        st = q % sc["streams"]
+        rois = npw["rois"][f, st * Ns:st * Ns + N].copy()
         rois[:, 0] = 0
-        fmap = frame_map(sc, f)[s:s + 1].cpu().numpy()
+        fmap = frame_map(sc, f)[st:st + 1].cpu().numpy()
         t0 = time.perf_counter()
-        roi = O.roi_align(fmap, rois, (10, 10), 40 / 1280.0, 2, True)
+        roi = O.roi_align(fmap, rois, (S, S), 40 / 1280.0, 2, True)
         t1 = time.perf_counter()
         with torch.no_grad():
             emb = O.encoder_forward(sd, torch.from_numpy(roi)).numpy()
         t2 = time.perf_counter()
-        b, c = npw["dbox"][f, s], npw["dconf"][f, s]
+        b, c = npw["dbox"][f, st, :N], npw["dconf"][f, st, :N]
         out = O.cost_build(bank, np.full(N, 30, np.int32), emb, b, b, c, c, gm, gs, np.ones(N, np.int32))
         t3 = time.perf_counter()
-        linear_sum_assignment(out["C_total"])
+        lsa(out["C_total"])
         t4 = time.perf_counter()
         if q < frames_lit + 1:  # literal cost: 1 warm-up + frames_lit timed
             capp = LIT.build_c_app_topk_literal([list(bank[i]) for i in range(N)], list(emb))
@@ -658,33 +630,84 @@ def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
         if time.perf_counter() - t_start > 3 * budget_s:
             break
     med = lambda v: float(np.median(v))
-    vec = med(t_roi) + med(t_enc) + med(t_cost) + med(t_lsap)
-    lit = med(t_roi) + med(t_enc) + med(t_lit) + med(t_lsap)
+    return dict(roi=med(t_roi), enc=med(t_enc), cost=med(t_cost), lsap=med(t_lsap), lit=med(t_lit),
+                n_vec=len(t_roi), n_lit=len(t_lit))
+
+
+def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
+    """The reference's CPU path on this box's host cores, two modes (SURVEY.md
+    8(d)), same inputs, 3 warm-up frames, per-frame medians:
+      vectorised        oracle roi_align (C restatement of torchvision's CPU
+                        kernel) + the fp32 encoder in plain torch + the oracle's
+                        vectorised cost incl. gate (C) + scipy.optimize.linear_sum_assignment
+      reference_literal the same roi_align / encoder / LSAP with the cost as the
+                        reference's Python computes it: the per-track top-k loop
+                        (mainTracking.py:173-210) and the per-pair 4x4-inverse
+                        gating loop (:327-336) -- oracle/literal.py
+    The headline (value) is c3's shape: one stream at N=256, 10x10 ROIs.  The literal
+    mode's loops take seconds per frame, so its cost stage is sampled on frames_lit frames
+    (the stages are timed separately and the medians added).  BASELINE.md §2's other CPU
+    legs follow in `legs`: c1 (B=1, N=16, S=7 -- the reference tracker's own ROI size,
+    tracking.py:304-309 -- and S=10) and c2 (N=64, S=10), on fewer frames.
+    Threads: every physical core, capped by OMP_NUM_THREADS where the box sets it
+    (16 on a one-GPU gpurun box: that GPU's CPU share); torch and the oracle's
+    OpenMP loops (roi_align over ROIs, cost over track rows) use the same count."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    import literal as LIT
+    from scipy.optimize import linear_sum_assignment
+    model, cores = _cpu_info()
+    cap = os.environ.get("OMP_NUM_THREADS")
+    thr = min(int(cap), cores or int(cap)) if cap else (cores or os.cpu_count() or 1)
+    torch.set_num_threads(thr)
+    os.environ.setdefault("OMP_NUM_THREADS", str(thr))  # the oracle's OpenMP (read at its first parallel loop)
+    N = sc["N"]
+    m = _cpu_leg(sc, sd, O, LIT, linear_sum_assignment, N, 10, frames_vec, frames_lit, budget_s)
+    vec = m["roi"] + m["enc"] + m["cost"] + m["lsap"]
+    lit = m["roi"] + m["enc"] + m["lit"] + m["lsap"]
+    legs = {}
+    for name, n, S in (("c1_n16_s7", 16, 7), ("c1_n16_s10", 16, 10), ("c2_n64_s10", 64, 10)):
+        if n > N:
+            continue
+        g = _cpu_leg(sc, sd, O, LIT, linear_sum_assignment, n, S, 10, 3, budget_s / 4)
+        gv = g["roi"] + g["enc"] + g["cost"] + g["lsap"]
+        gl = g["roi"] + g["enc"] + g["lit"] + g["lsap"]
+        legs[name] = {"N": n, "roi": S, "frames": g["n_vec"], "literal_cost_frames": g["n_lit"],
+                      "vectorised": {"ms_per_frame": round(gv * 1e3, 2), "rois_per_s": round(n / gv, 2)},
+                      "reference_literal": {"ms_per_frame": round(gl * 1e3, 2), "rois_per_s": round(n / gl, 2),
+                                            "cost_ms": round(g["lit"] * 1e3, 2)},
+                      "stages_ms": {k: round(g[k] * 1e3, 2) for k in ("roi", "enc", "cost", "lsap")}}
     return dict(value=round(N / vec, 2), unit="ROIs/s", cores=thr, kind="port",
-                sample=f"one stream, N={N}, 3 warm-up frames, medians over {len(t_roi)} frames "
-                       f"(literal cost stage: {len(t_lit)} frames): roi_align {med(t_roi) * 1e3:.0f} ms (C, {thr} "
-                       f"OpenMP threads) + fp32 encoder {med(t_enc) * 1e3:.0f} ms (torch CPU, {thr} threads) + cost "
-                       f"{med(t_cost) * 1e3:.1f} ms (C, {thr} OpenMP threads) + scipy LSAP {med(t_lsap) * 1e3:.1f} ms",
+                sample=f"one stream, N={N}, 3 warm-up frames, medians over {m['n_vec']} frames "
+                       f"(literal cost stage: {m['n_lit']} frames): roi_align {m['roi'] * 1e3:.0f} ms (C, {thr} "
+                       f"OpenMP threads) + fp32 encoder {m['enc'] * 1e3:.0f} ms (torch CPU, {thr} threads) + cost "
+                       f"{m['cost'] * 1e3:.1f} ms (C, {thr} OpenMP threads) + scipy LSAP {m['lsap'] * 1e3:.1f} ms",
                 cpu_model=model, physical_cores=cores,
                 core_cap=(f"OMP_NUM_THREADS={cap} (the box's CPU share for this GPU)" if cap else None),
                 modes={"vectorised": {"ms_per_frame": round(vec * 1e3, 1), "rois_per_s": round(N / vec, 2)},
                        "reference_literal": {"ms_per_frame": round(lit * 1e3, 1), "rois_per_s": round(N / lit, 2),
-                                             "cost_ms": round(med(t_lit) * 1e3, 1)}})
+                                             "cost_ms": round(m["lit"] * 1e3, 1)}},
+                legs=legs)
 
 
-def timed_region(step, steps, dist, sync, red_dev, finish=None, own=None):
+def timed_region(step, steps, dist, sync, red_dev, finish=None, own=None, region=None):
     """Run `steps` steps between a barrier + device sync on both sides; return
     the MAX elapsed time over ranks (one all_reduce) and the step outputs
-    (this rank's own elapsed time is appended to `own` if given)."""
+    (this rank's own elapsed time is appended to `own` if given).  region: a
+    ProfRegion opened right after the opening sync and closed after the closing one."""
     if dist is not None:
         dist.barrier()
     sync()
+    if region is not None:
+        region.resume("timed")
     t0 = time.perf_counter()
     out = [step(k) for k in range(steps)]
     if finish is not None:
         finish()  # every frame's assignment indices read on the host
     sync()
     el = time.perf_counter() - t0
+    if region is not None:
+        region.pause()
     if own is not None:
         own.append(el)
     if dist is not None:
@@ -708,6 +731,7 @@ def main():
                          "launches on the side stream, so off by default)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
+    region = ProfRegion()  # before any GPU work: a --selected-regions profile holds only the chosen region
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -747,18 +771,6 @@ def main():
     # TRK_FRONT=0: the two-kernel encoder front (g1dw4 -> Y2 in HBM -> gemm4<DSC>) instead of
     # rmb_front (one kernel, Y2 in LDS)
     model.fused_front = os.environ.get("TRK_FRONT", "1") == "1"
-    # TRK_FULL=1/0: the SE and transition inside the front kernel (enc_rmb_fused) or not; unset:
-    # encoder.Model's default
-    if "TRK_FULL" in os.environ:
-        model.fused_full = os.environ["TRK_FULL"] == "1"
-    # TRK_FRONT_SE=1/0: the SE inside the front kernel (enc_rmb_front_se) or its own enc_se
-    # launch; unset: encoder.Model's default
-    if "TRK_FRONT_SE" in os.environ:
-        model.front_se = os.environ["TRK_FRONT_SE"] == "1"
-    # TRK_FRONT_MEANS=1/0: the front writes the squeeze means for enc_se_means, or the int64
-    # sums for enc_se; unset: encoder.Model's default
-    if "TRK_FRONT_MEANS" in os.environ:
-        model.front_means = os.environ["TRK_FRONT_MEANS"] == "1"
 
     # +depth frames: each step enqueues the embedding `depth` frames ahead (pipelining);
     # the syncs around the timed region make it do exactly `steps` embeddings (those of
@@ -778,21 +790,24 @@ def main():
     pipe.tracker.sync_wait_s = 0.0
     own = []
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
-                               torch.cuda.synchronize, red_dev, finish=pipe.tracker.drain, own=own)
+                               torch.cuda.synchronize, red_dev, finish=pipe.tracker.drain, own=own, region=region)
     el_own = own[0]
     probe.on = False
     kernel_sum = probe.sum_per_step_us(args.steps)
     live = probe.means_us()
     live = {k: v for k, v in live.items() if not k.endswith("_live")}
     tracker_live = {"lsap": probe.stage_means_us("lsap_live"), "cost": probe.stage_means_us("cost_live")}
-    side_gap = (None if pipe.defer_tail else  # frames interleave on the embedding stream on purpose
-                probe.embed_gaps_us(len(pipe.sides), pipe.defer_head, pipe.roi_stream is not None))
+    side_gap = probe.embed_gaps_us(len(pipe.sides), pipe.defer_head, pipe.roi_stream is not None)
     f = PREROLL + args.warmup + args.steps
     rois_total = args.steps * sc["streams"] * sc["N"] * world
     value = rois_total / el
     ident = float(np.mean([pipe.check_identity(PREROLL + args.warmup + k, r) for k, r in enumerate(results)]))
 
+    torch.cuda.synchronize()
+    region.resume("isolated")
     iso, M = kernel_pass(pipe, f - 1)
+    torch.cuda.synchronize()
+    region.pause()
     # per-launch device time: live (timed region) where probed, else isolated
     kt = dict(iso)
     kt.update(live)
@@ -820,13 +835,10 @@ def main():
         "enc_gemm_dsc": (R * 1024 * 2 * 2 + 2 * 512 * 512 * 2 + K * 1024 * 8, 2.0 * R * 1024 * 512,
                          BF16_PEAK_TFLOPS),
         "enc_gemm_trans": (R * 1024 * 2 + 512 * 1024 * 2 + K * 512 * 12, 2.0 * R * 512 * 1024, BF16_PEAK_TFLOPS),
-        # first 1x1 convs + depthwise + both DSC GEMMs in one kernel: X in, XRN + sums out
-        "enc_rmb_front": (R * 512 * 2 + R * 1024 * 2 + 2 * 1024 * 512 * 2 + 25 * 1024 * 4 + K * 1024 * 8,
+        # first 1x1 convs + depthwise + both DSC GEMMs in one kernel: X in, XRN + the squeeze
+        # means out
+        "enc_rmb_front": (R * 512 * 2 + R * 1024 * 2 + 2 * 1024 * 512 * 2 + 25 * 1024 * 4 + K * 1024 * 4,
                           2.0 * R * 1024 * 512 * 2 + 2.0 * R * 1024 * 25, BF16_PEAK_TFLOPS),
-        # front + SE + transition in one kernel: X in, the x_n hand-off written and read once
-        # (bf16), the three weight sets, the means / scales / transition sums out
-        "enc_rmb_fused": (R * 512 * 2 + 2 * R * 512 * 2 + 3 * 1024 * 512 * 2 + 2 * 128 * 512 * 4 + K * 512 * (3 * 4 + 24),
-                          2.0 * R * 1024 * 512 * 3 + 2.0 * R * 1024 * 25 + 4.0 * K * 128 * 512, BF16_PEAK_TFLOPS),
         "cost": (Fs * (M * 30 * 128 * 4 + N * 128 * 4 + M * N * 4), 2.0 * Fs * M * 30 * N * 128,
                  F32_MFMA_PEAK_TFLOPS),
     }
@@ -864,8 +876,18 @@ def main():
             tsrc = pm.get("profile", "profiles/pmc_traffic.json")
     except (OSError, KeyError, ValueError):
         pass
+    t_iso = iso.get(dom)
     rf = {"kernel": dom, "bound": per[dom]["bound"], "achieved": per[dom]["achieved"],
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
+          "time_us": per[dom]["us"],
+          "time_source": ("live: mean of the HIP-event pairs around this kernel's launches inside the timed "
+                          "region, on the stream it is launched on (the same launches a rocprofv3 "
+                          "--selected-regions run profiles, TRK_PROF_REGION=timed)" if dom in live else
+                          "isolated: back-to-back launches after the timed region"),
+          "isolated_time_us": None if t_iso is None else round(t_iso, 2),
+          "isolated_frac": None if t_iso is None else round(per[dom]["work"] / (t_iso * 1e-6) /
+                                                            (per[dom]["peak"] * (1e12 if per[dom]["unit"] == "TFLOP/s"
+                                                                                 else 1e9)), 4),
           "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": algo[dom][0],
           "algorithmic_flops_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
           "kernel_us_source": {k: ("live: HIP events around each launch in the timed region (with two "
@@ -905,8 +927,6 @@ def main():
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
     rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
-                     "se_deferred": pipe.defer_tail, "se_in_front": bool(getattr(pipe.model, "front_se", False)),
-                     "front_means": bool(getattr(pipe.model, "front_means", False)) and not getattr(pipe.model, "front_se", False),
                      "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
                      "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,

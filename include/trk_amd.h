@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TRK_ABI_VERSION 1
+#define TRK_ABI_VERSION 2
 
 enum {
   TRK_OK = 0,
@@ -51,30 +51,14 @@ const char* trk_last_error(void);
  *                    products (NOT bit-identical: within a few f32 roundings before the
  *                    bf16 rounding; f32 output is always the exact torchvision arithmetic)
  *   "dw_fast"        1 (default): 7x7/10x10 depthwise fast path; 0: generic depthwise kernel
- *   "enc_gemm"       1 (default): pipelined 128x256 DSC / transition GEMMs (gemm4); 0: the
- *                    128x128 / 128x256 kernels (same math, another f32 summation order)
- *   "enc_sums"       1 (default): gemm4's per-ROI column sums (SE squeeze, GAP) as MFMAs of a
- *                    slot mask with the activations split bf16 hi + lo (sums within ~1e-6
- *                    relative of the lane-reduction sums, 0)
- *   "g1dw"           6 (default): fused first GEMM + depthwise with the next round's rows
- *                    prefetched into L2; 4: without the prefetch
- *   "rf_pf"          8 (default): trk_enc_rmb_front rf_v 1 / 2 prefetches the X rows of ROI + rf_pf
- *                    into L2 (0..64; 0: no prefetch)
- *   "rf_v"           3 (default): trk_enc_rmb_front as a persistent grid, each workgroup running
- *                    the ROIs of one channel group back to back; 2: one ROI per workgroup, the
- *                    wave halves handing off through LDS counters; 1: lockstep phases (all
- *                    bit-identical)
- *   "rf3_groups"     0 (default: CUs / 16 - 2): rf_v 3 workgroup pairs per XCD (1..64)
- *   "rf3_pf"         0 (default): rf_v 3 without the L2 prefetch of the workgroup's next ROI; 1: with
- *   "rf_lag"         16 (default): with rf_v 2 / 3 (and in trk_enc_rmb_fused), half B starts its
- *                    first GEMM once half A is past that K step (0, 4, 8, 12, 16)
+ *   "enc_trans"      1 (default): trk_enc_transition_gemm2 with packed weights runs trans4
+ *                    (weights straight into VGPRs); 0: gemm4 (weights through LDS), same sums
+ *   "rf3_groups"     0 (default: CUs / 16 - 2): trk_enc_rmb_front_means workgroup pairs per XCD
+ *                    (1..64; all bit-identical)
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
  *                    given (the device tracker), else the detection-tile kernel; 1: the
  *                    LDS bank-resident cost2 kernel (all bit-identical)
- *   "lsap_split"     0 (default): trk_lsap_dev launches the bound's kernel once; 1: a kernel sized
- *                    for 256 columns for the matrices that fit it, then the bound's kernel for the
- *                    wider ones (it exits at once when there are none)
  *   "lsap_dev_lds_kb" LDS budget of trk_lsap_dev workgroups (default 24: they fit beside the
  *                    encoder's workgroups instead of waiting for a whole CU) */
 int trk_set_tuning(const char* key, int value);
@@ -182,8 +166,8 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
  * argmin, dual updates, augmentation; iterations, total, nr, nc; then the workgroup's
  * shortcut pass, loaders + solver, outputs, total).  NULL = off. */
 int trk_lsap_set_prof(unsigned long long* buf);
-/* diagnostics: per-workgroup timestamps of the 256x256 encoder GEMM (enc_gemm=2);
- * buf >= 16 u64 per workgroup, NULL = off */
+/* diagnostics: per-workgroup (gemm4, trans4: 8 u64 each) or per-wave (rmb_front3: [ROI][group]
+ * [wave][8] u64) phase timestamps of the encoder GEMMs; NULL = off */
 int trk_enc_set_prof(unsigned long long* buf);
 /* diagnostics: per-wave timestamps of the bank-resident cost kernel; NULL = off */
 int trk_cost_set_prof(unsigned long long* buf);
@@ -221,11 +205,8 @@ int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C,
  * j-th 128-row M tile (j < 1 + (roi*P + P - 1)/128 - roi*P/128); entries past
  * that count are not written.  The total of a ROI is the integer sum of its
  * partials (trk_enc_sums_reduce, or inside trk_enc_se / trk_enc_head), so it
- * does not depend on tile order.  Requires 32 <= P <= 256, K % 32 == 0,
+ * does not depend on tile order.  Requires 43 <= P <= 256, K % 32 == 0,
  * N % 256 == 0, 16-B aligned operands.
- *
- * trk_enc_gemm: plain C[M, N] = A[M, K] . B[N, K]^T in bf16 (row strides lda,
- *   ldc): the four first 1x1 convs of the RMB as one GEMM (card.py:28,38). 
  *
  * trk_enc_dsc_gemm: both DSC 1x1 GEMMs (card.py:53-56, depth.2 + point.2 with
  *   eval-BN folded): Y2 [M, 2*Kg] (reinforce half | normal half), W2
@@ -238,74 +219,37 @@ int trk_act_scale_rows(void* x, const float* s, int64_t N, int64_t P, int64_t C,
  *   produced (partials [ROIs][TRK_ENC_PARTS][N]); T is never stored.
  * ---------------------------------------------------------------------- */
 #define TRK_ENC_PARTS 3
-int trk_enc_gemm(const void* A, int64_t M, int64_t K, int64_t lda, const void* B, int64_t N, void* C,
-                 int64_t ldc, void* stream);
 /* out[roi][c] = (float)(sum_j part[roi][j][c] * 2^-24) for the partial sums above. */
 int trk_enc_sums_reduce(const long long* part, int64_t R, int64_t P, int64_t ld, float* out, void* stream);
-/* trk_enc_g1_dwconv: trk_enc_gemm (K = 512) followed by the 1024-channel
- *   depthwise 5x5 (card.py:29,39) in one kernel for 10x10 ROIs (M = ROIs x 100):
+/* trk_enc_g1_dwconv: the four first 1x1 convs of the RMB as one GEMM (card.py:28,38;
+ *   X [M][512] . W1^T, W1 [N][512]) followed by the 1024-channel depthwise 5x5
+ *   (card.py:29,39) in one kernel for 10x10 ROIs (M = ROIs x 100):
  *   Y2 = dwconv5(bf16(X . W1^T)) with weights tap-major [25][N] f32; Y1 never
- *   reaches HBM.  Bit-identical to trk_enc_gemm + trk_dwconv5_nhwc. */
+ *   reaches HBM. */
 int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64_t N, const float* wdw, void* Y2,
                       void* stream);
 int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const void* W2, const float* bias,
                      int64_t Ng, void* XRN, long long* sums, void* stream);
-/* trk_enc_rmb_front: trk_enc_g1_dwconv followed by trk_enc_dsc_gemm in ONE kernel
+/* trk_enc_rmb_front_means: trk_enc_g1_dwconv followed by trk_enc_dsc_gemm in ONE kernel
  *   for 10x10 ROIs of C = 512 channels (M = ROIs x 100, 4h = 1024, Ng = Kg = 512;
- *   card.py:28-57): each workgroup runs one DSC (reinforce or normal) of one ROI with
- *   Y1 and Y2 kept in LDS, so Y2 never reaches HBM.  Weights in MFMA fragment
- *   order: W1p = W1 [1024][512] and W2p = W2 [2][512][512] each as
- *   [2 groups][16 k steps][32 col tiles][64 lanes][8] bf16, element (g, s, n, l, j)
- *   = W[g*512 + 16n + (l % 16)][32 s + 8 (l / 16) + j] (trk.ops.enc_pack_fragments);
- *   wdw [25][1024] f32, bias [1024] f32 (BN-folded).  XRN is bit-identical to the
- *   two-kernel path; sums (same layout as trk_enc_dsc_gemm's, ld 1024) hold the
- *   ROI's whole sum in partial 0 and 0 in its other partials. */
-int trk_enc_rmb_front(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                      const float* bias, void* XRN, long long* sums, void* stream);
-
-/* trk_enc_rmb_front + trk_enc_se in one launch (rf_v 3, the persistent front): every
- * workgroup also writes its ROIs' squeeze means (m_r = mean SiLU(x_r) from the reinforce
- * group, m_n = mean Hardswish(x_n) from the normal group, [R][512] f32, the bits trk_enc_se
- * computes from the sums) and the reinforce-group workgroups then run the SE excitation
- * s = hardsigmoid(W2 relu(W1 m_r + b1) + b2) over their ROIs in batches of 16 with
- * trk_enc_se's arithmetic (bit-identical s).  Replaces the reference's SEBlock call after the
- * DSC pair (model/utils/modules/card.py:59-78, 128-148).  sums may be NULL (not written);
- * with rf_v 1 / 2 the call is the front followed by trk_enc_se (on sums, or on an internal
- * workspace when NULL).  se_w1 [H][512], se_b1 [H], se_w2 [512][H], se_b2 [512] f32, H a
- * multiple of 16 in [16, 512]. */
-int trk_enc_rmb_front_se(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                         const float* bias, void* XRN, long long* sums, const float* se_w1, const float* se_b1,
-                         int64_t H, const float* se_w2, const float* se_b2, float* m_r, float* m_n, float* s,
-                         void* stream);
-
-/* trk_enc_rmb_front writing the ROI squeeze means instead of the int64 sums: m_r / m_n
- * [R][512] f32, the bits trk_enc_se derives from the sums (rf_v 3: from the kernel's own
- * column sums, no sums round trip; rf_v 1 / 2: the front, then trk_enc_se's means phase on
- * an internal workspace).  Pair with trk_enc_se_means. */
+ *   card.py:28-57), writing the SE squeeze means instead of the int64 sums: a persistent
+ *   grid whose workgroups each run one DSC (reinforce or normal) of their ROIs with Y1 and
+ *   Y2 kept in LDS, so Y2 never reaches HBM.  Weights in MFMA fragment order: W1p = W1
+ *   [1024][512] and W2p = W2 [2][512][512] each as [2 groups][16 k steps][32 col tiles]
+ *   [64 lanes][8] bf16, element (g, s, n, l, j) = W[g*512 + 16n + (l % 16)][32 s + 8 (l / 16)
+ *   + j] (trk.ops.enc_pack_fragments); wdw [25][1024] f32, bias [1024] f32 (BN-folded).
+ *   XRN [M][1024] is bit-identical to the two-kernel path; m_r = mean SiLU(x_r), m_n = mean
+ *   Hardswish(x_n) [R][512] f32 as trk_enc_se computes them from int64 sums, of the kernel's
+ *   own f32 column sums.  Pair with trk_enc_se_means. */
 int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
                             const float* bias, void* XRN, float* m_r, float* m_n, void* stream);
-/* trk_enc_rmb_fused: trk_enc_rmb_front + trk_enc_se + trk_enc_transition_gemm in ONE kernel
- *   (10x10 ROIs, C = 512; card.py:28-78, :138-146).  A ROI's two workgroups hand data over
- *   through global memory and flags[roi][4] (= epoch once published): the normal group its
- *   bf16 Hardswish(x_n) rows (xn_work, [M][512] bf16) and, from the reinforce group's m_r,
- *   the SE scales s (FC1, ReLU, FC2, hardsigmoid: f32); the reinforce group computes
- *   T = Wt . [x_f * s | x_n] + bt with its SiLU summed per channel.  Outputs are trk_enc_se's and trk_enc_transition_gemm's:
- *   m_r, m_n, s [R][512] f32 and tsums [R][TRK_ENC_PARTS][512] (partial 0 = the ROI's sum,
- *   the others 0) for trk_enc_head; XRN never reaches HBM.  Wtp = Wt [512][1024] in the
- *   fragment order of trk_enc_rmb_front with 32 k steps ([32][32][64][8] bf16); se_w1
- *   [128][512], se_b1 [128], se_w2 [512][128], se_b2 [512], bt [512] f32.  flags [R][4] int32
- *   must not hold epoch when the launch starts (zero them per launch and pass epoch 1), and
- *   xn_work / flags must not be shared with a concurrent launch. */
-int trk_enc_rmb_fused(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                      const float* bias, const void* Wtp, const float* bt, const float* se_w1, const float* se_b1,
-                      const float* se_w2, const float* se_b2, void* xn_work, int* flags, int epoch, float* m_r,
-                      float* m_n, float* s, long long* tsums, void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
-/* trk_enc_transition_gemm2: the same, also given Wtp = Wt in the fragment order of trk_enc_rmb_fused
- *   (may be NULL).  With Wtp, K = 1024, kscale = 512 and trk_set_tuning("enc_trans", 1) the
- *   weights are read straight into registers (trans4 kernel) instead of through LDS; the sums
- *   are bit-identical either way. */
+/* trk_enc_transition_gemm2: the same, also given Wtp = Wt [512][1024] in MFMA fragment order
+ *   ([32 k steps][32 col tiles][64 lanes][8] bf16, trk.ops.enc_pack_fragments_k; may be NULL).
+ *   Wtp requires K = 1024, N = 512, kscale = 512 (else TRK_EINVAL); with it and
+ *   trk_set_tuning("enc_trans", 1) the weights are read straight into registers (trans4
+ *   kernel) instead of through LDS; the sums are bit-identical either way. */
 int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                              const void* Wt, const void* Wtp, const float* bias, int64_t N, long long* sums,
                              void* stream);

@@ -2,6 +2,7 @@
 public header declares, and rejects bad arguments on the host before any
 launch (SURVEY.md 8(b) error conventions)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -13,7 +14,7 @@ def test_library_exports_header_symbols(trk):
     assert len(syms) >= 7
     for s in syms:
         assert hasattr(L, s), f"libtrk_amd.so does not export {s}"
-    assert L.trk_abi_version() == 1
+    assert L.trk_abi_version() == 2
 
 
 def test_host_side_argument_errors(trk):
@@ -72,7 +73,7 @@ def test_encoder_fused_graph_fp32_vs_reference_golden(trk, s):
 
 
 def test_rmb_front_fragment_packing_and_argument_errors(trk):
-    """enc_pack_fragments is the exact permutation trk_enc_rmb_front reads (element
+    """enc_pack_fragments is the exact permutation trk_enc_rmb_front_means reads (element
     (g, s, n, l, j) = W[g*512 + 16n + l%16][32s + 8(l//16) + j]); the entry point rejects
     M % 100 != 0 and null pointers on the host."""
     import torch
@@ -85,25 +86,31 @@ def test_rmb_front_fragment_packing_and_argument_errors(trk):
     assert torch.equal(P, ref)
     assert torch.equal(ops.enc_pack_fragments(W.view(2, 512, 512)), ops.enc_pack_fragments(W))
     L = trk.lib()
-    assert L.trk_enc_rmb_front(ctypes.c_void_p(16), 150, ctypes.c_void_p(16), ctypes.c_void_p(16),
-                               ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16),
-                               ctypes.c_void_p(16), None) == -1
-    assert b"M % 100" in L.trk_last_error()
-    assert L.trk_enc_rmb_front(None, 100, None, None, None, None, None, None, None) == -1
-    assert L.trk_enc_rmb_front(None, 0, None, None, None, None, None, None, None) == 0
-    # trk_enc_rmb_front_se: the same front checks plus its SE operands (host-side, no launch)
     v = ctypes.c_void_p(16)
-    assert L.trk_enc_rmb_front_se(None, 0, *([None] * 8), 128, *([None] * 6)) == 0
-    assert L.trk_enc_rmb_front_se(v, 150, *([v] * 8), 128, *([v] * 6)) == -1
-    assert b"M % 100" in L.trk_last_error()
-    assert L.trk_enc_rmb_front_se(v, 100, *([v] * 8), 120, *([v] * 6)) == -1
-    assert b"multiple of 16" in L.trk_last_error()
-    assert L.trk_enc_rmb_front_se(v, 100, *([v] * 8), 128, v, v, None, v, v, v, v) == -1
-    assert b"SE pointer" in L.trk_last_error()
     assert L.trk_enc_rmb_front_means(None, 0, *([None] * 8)) == 0
     assert L.trk_enc_rmb_front_means(v, 150, *([v] * 8)) == -1
     assert b"M % 100" in L.trk_last_error()
     assert L.trk_enc_rmb_front_means(v, 100, *([v] * 5), None, v, v) == -1
+    # trk_enc_transition_gemm2: packed weights only for K = 1024, N = 512, kscale = 512
+    assert L.trk_enc_transition_gemm2(v, 100, 100, 1024, v, 512, v, v, v, 768, v, None) == -1
+    assert b"N = 512" in L.trk_last_error()
+    assert L.trk_enc_transition_gemm2(v, 100, 100, 768, v, 512, v, v, v, 512, v, None) == -1
     assert L.trk_enc_se_means(None, 0, 512, None, None, 128, None, None, None, None) == 0
     assert L.trk_enc_se_means(v, 4, 512, v, v, 120, v, v, v, v) == -1
     assert b"multiples of 16" in L.trk_last_error()
+
+
+def test_no_device_allocation_in_the_library():
+    """include/trk_amd.h promises no malloc / free inside a call (calls never synchronise the
+    device and are hipGraph-capturable): no HIP allocation, free or memset anywhere in csrc/."""
+    import re
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "a-lightweight-unsupervised-feature-extractor-_amd", "csrc")
+    bad = []
+    for name in sorted(os.listdir(src)):
+        if name.endswith((".hip", ".cpp", ".h")):
+            with open(os.path.join(src, name)) as fh:
+                for i, line in enumerate(fh, 1):
+                    if re.search(r"\bhip(Malloc\w*|Free\w*|Memset\w*|HostAlloc|HostMalloc)\s*\(", line):
+                        bad.append(f"{name}:{i}: {line.strip()}")
+    assert not bad, bad

@@ -152,30 +152,6 @@ def test_c2_chain_fp32_vs_oracle(trk, oracle, gpu):
     assert np.array_equal(r, np.arange(N)) and np.mean(c == perm) >= 0.95
 
 
-def test_c3_fused_full_encoder_vs_front_path(trk, gpu):
-    """The bench's encoder at c3 size: rmb_fused (SE + transition inside the front kernel)
-    against rmb_front -> enc_se -> transition GEMM on the same ROI features: the two paths
-    differ only in the SE's f32 summation order and the per-channel sum order (|d| <= 2e-5
-    on unit embeddings)."""
-    rng = np.random.default_rng(4096)
-    F, N = 8, 256
-    feat = torch.from_numpy(G.silu_np(rng.standard_normal((F, 512, 40, 40)).astype(np.float32))
-                            .astype(np.float32)).to(gpu)
-    boxes = np.stack([_boxes(rng, N) for _ in range(F)])
-    rois = np.concatenate([np.repeat(np.arange(F), N).astype(np.float32)[:, None], boxes.reshape(-1, 4)], 1)
-    model, _ = _model(trk, gpu)
-    with torch.no_grad():
-        roib = trk.roi_align(feat, torch.from_numpy(rois).to(gpu), (10, 10), 40 / 1280.0, 2, True,
-                             out_dtype=torch.bfloat16, channels_last=True)
-        model.fused_full = True
-        z_full = model(roib)
-        model.fused_full = False
-        z_front = model(roib)
-    d = (z_full - z_front).abs().max().item()
-    print(f"\nc3 fused-full vs front path: max |d| {d:.3e}")
-    assert d <= 2e-5, d
-
-
 def test_reference_half_configuration(trk, gpu):
     """The reference's own GPU configuration (tracking.py:177-178 model.half();
     tracking.py:209-221 rois built in feat.dtype, so fp16 boxes; :313 normalize(z.float())):

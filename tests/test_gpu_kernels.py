@@ -7,6 +7,7 @@ the reference's golden vectors.  Tolerances are written in each test:
   lsap: indices bit-exact (scipy semantics)
   encoder fp32: <= 1e-4 (north star);  bf16: |d| <= 1.2e-3, cosine >= 1 - 5e-6 vs fp32 (2x measured)
 """
+import ctypes
 import os
 
 import numpy as np
@@ -653,87 +654,32 @@ def test_enc_fused_gemms_vs_torch_fp32(trk, gpu, P, R):
     A = torch.cat([xs, XRN[:, Ng:].float()], 1)
     ref_t = F.silu(A @ Wt.float().t() + bt).view(R, P, Ng).sum(1)
     assert (st - ref_t).abs().max().item() <= 2e-3 * ref_t.abs().max().item()
-    # the pipelined 128 x 256 kernels (default) vs the 128 x 128 / 128 x 256 kernels:
-    # same math, another f32 summation order
-    L = ops.lib()
-    try:
-        assert L.trk_set_tuning(b"enc_gemm", 0) == 0
-        XRN0, sr0, sn0 = ops.enc_dsc_gemm(Y2, P, W2, b2)
-        st0 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
-    finally:
-        assert L.trk_set_tuning(b"enc_gemm", 1) == 0
-    assert (XRN0.float() - XRN.float()).abs().max().item() <= 1e-2 * max(1.0, XRN.float().abs().max().item())
-    assert (sr0 - sr).abs().max().item() <= 1e-3 * sr.abs().max().item()
-    assert (sn0 - sn).abs().max().item() <= 1e-3 * sn.abs().max().item()
-    assert (st0 - st).abs().max().item() <= 1e-3 * st.abs().max().item()
     st2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
     assert torch.equal(st, st2)
-    # plain GEMM (the first 1x1 convs), strided A rows
-    W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
-    A = Y2[:, :512]
-    Y1 = ops.enc_gemm(A, W1)
-    ref1 = A.float() @ W1.float().t()
-    assert (Y1.float() - ref1).abs().max().item() <= 1e-2 * max(1.0, ref1.abs().max().item())
     if P == 100:
-        # first GEMM + depthwise 5x5 fused (g1dw4) against the two kernels (enc_gemm +
-        # dwconv5_nhwc), odd ROI count (a half-filled last tile): Y1 sums its products in
-        # another order, so a Y1 value can round to the neighbouring bf16 (2^-8 relative),
-        # which moves the Y2 outputs it feeds by |w| times that; deterministic run to run
-        X = A.contiguous()
+        # first GEMM + depthwise 5x5 fused (g1dw4) against the fp32 GEMM rounded to bf16 +
+        # dwconv5_nhwc, odd ROI count (a half-filled last tile): Y1 sums its products in another
+        # order, so a Y1 value can round to the neighbouring bf16 (2^-8 relative), which moves the
+        # Y2 outputs it feeds by |w| times that; deterministic run to run
+        W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
+        X = Y2[:, :512].contiguous()
         wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
-        Yu = ops.dwconv5_nhwc(ops.enc_gemm(X, W1).view(R, 10, 10, 1024), wdw).view(M, 1024)
-        Y7 = ops.enc_g1_dwconv(X, W1, wdw)   # g1dw 6 (the default): + next-round A prefetch
+        Y1 = (X.float() @ W1.float().t()).bfloat16()
+        Yu = ops.dwconv5_nhwc(Y1.view(R, 10, 10, 1024), wdw).view(M, 1024)
+        Y7 = ops.enc_g1_dwconv(X, W1, wdw)
         Y7b = ops.enc_g1_dwconv(X, W1, wdw)
         assert torch.equal(Y7, Y7b)
-        try:  # g1dw 4: without the prefetch, the same arithmetic -> the same bits
-            assert L.trk_set_tuning(b"g1dw", 4) == 0
-            Y4 = ops.enc_g1_dwconv(X, W1, wdw)
-        finally:
-            assert L.trk_set_tuning(b"g1dw", 6) == 0
-        assert torch.equal(Y4, Y7)
         d = (Y7.float() - Yu.float()).abs()
         assert d.max().item() <= 2e-2 * Yu.float().abs().max().item()
         assert (d == 0).float().mean().item() >= 0.9
 
 
-@pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (86, 61)])
-def test_enc_transition_wide_tile_vs_default(trk, gpu, P, R):
-    """The transition on 256 x 256 tiles (enc_trans_wide 1: 8 waves, one workgroup per CU)
-    vs the default 128 x 256 tiles: the same wave tiles (64 rows x 128 columns) on the same
-    64-row blocks, MFMA K order and SE-scaled bf16 operands, and the per-ROI sums are int64
-    sums of the same per-wave f32 partials -- so the reduced sums must be bit-identical.
-    A 256-row tile covers two 128-row partial slots: P = 100 / 200 put ROIs across both
-    (the second one must be written as 0), R = 1 and 37 leave the last tile ragged."""
-    from importlib import import_module
-    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
-    g = torch.Generator().manual_seed(1000 + R)
-    M, Ng = R * P, 512
-    XRN = torch.randn(M, 2 * Ng, generator=g).to(gpu).bfloat16()
-    s = torch.rand(R, Ng, generator=g).to(gpu)
-    Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
-    bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
-    ref = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
-    L = trk.lib()
-    try:
-        assert L.trk_set_tuning(b"enc_trans_wide", 1) == 0
-        raw = ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True)
-        raw.fill_(0x5A5A5A5A5A5A)  # stale partials must be overwritten, not added to
-        got = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
-        got2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
-    finally:
-        L.trk_set_tuning(b"enc_trans_wide", 0)
-    assert torch.equal(got, ref) and torch.equal(got2, ref)  # (no fragments given: gemm4 either way)
-
-
-@pytest.mark.parametrize("t4_mode", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (49, 29)])
-def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R, t4_mode):
+def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R):
     """trans4 (enc_trans 1: the weights straight into VGPRs from the packed fragments,
     4 waves x 64 columns x 128 rows) vs gemm4 (weights through LDS, 2 x 2 waves): the same
     MFMA operands and K order, the same SE-scaled bf16 rows and the same per-64-row-block
-    MFMA sums, so the reduced ROI sums must be bit-identical; deterministic run to run.
-    t4_mode: K steps per LDS stage x B prefetch distance (0: 1x2, 1: 2x2, 2: 1x3, 3: 2x3) and
-    4-7: setprio / mid-step issue (5, mid-step issue at 1x2, is the default)."""
+    MFMA sums, so the reduced ROI sums must be bit-identical; deterministic run to run."""
     from importlib import import_module
     ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
     g = torch.Generator().manual_seed(2000 + R + P)
@@ -743,223 +689,102 @@ def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R, t4_mode):
     Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
     bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
     Wtp = ops.enc_pack_fragments_k(Wt)
+    assert Wtp[3, 5, 2, 7, 4].item() == Wt[16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
     ref = ops.enc_transition_gemm(XRN, P, s, Wt, bt)  # no fragments: gemm4 whatever the knob
     L = trk.lib()
     try:
-        assert L.trk_set_tuning(b"enc_trans", 1) == 0 and L.trk_set_tuning(b"t4_mode", t4_mode) == 0
+        assert L.trk_set_tuning(b"enc_trans", 1) == 0
         got = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
         got2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
         assert L.trk_set_tuning(b"enc_trans", 0) == 0
         nopk = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)  # knob 0: gemm4 with the fragments given
     finally:
         L.trk_set_tuning(b"enc_trans", 1)
-        L.trk_set_tuning(b"t4_mode", 5)  # the default
     assert torch.equal(got, ref) and torch.equal(got2, ref) and torch.equal(nopk, ref)
     with pytest.raises(ValueError, match="enc_pack_fragments_k"):
         ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp[:-1])
 
 
-@pytest.mark.parametrize("rf_v,rf_lag,groups,pf", [(2, 16, 0, 0), (2, 8, 0, 0), (2, 0, 0, 0), (1, 16, 0, 0),
-                                                   (3, 16, 0, 0), (3, 0, 0, 0), (3, 16, 1, 0), (3, 16, 16, 1),
-                                                   (3, 16, 64, 0)])
-@pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, rf_v, rf_lag, groups, pf):
-    """trk_enc_rmb_front (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
-    LDS) vs enc_g1_dwconv -> enc_dsc_gemm: the same MFMA shape, K order and bf16
-    roundings, so XRN must be bit-identical; the ROI sums add the same f32 activations in
-    another order (tol 1e-5 of the largest sum).  R = 2048 is the bench's c3 launch.
-    rf_v 3 (default): the persistent grid (rf3_groups workgroup pairs per XCD, 0 = CUs / 16 - 2;
-    a workgroup runs ROIs of one group back to back, the next ROI's GEMM1 under this one's
-    epilogue; 1 pair: 256 ROIs per workgroup at R = 2048, the LDS counters counting on
-    across all of them; 64: more pairs than ROIs); 2: one ROI per workgroup, the two wave
-    halves handing off through LDS counters, half B starting GEMM1 rf_lag K steps behind
-    half A; 1: lockstep phases.  pf: rf3_pf, the persistent grid's L2 prefetch of the next ROI
-    (off by default)."""
-    L = trk.lib()
-    assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf_lag", rf_lag) == 0
-    assert L.trk_set_tuning(b"rf3_groups", groups) == 0 and L.trk_set_tuning(b"rf3_pf", pf) == 0
-    try:
-        _rmb_front_vs_two_kernel(gpu, R)
-    finally:
-        L.trk_set_tuning(b"rf_v", 3)
-        L.trk_set_tuning(b"rf_lag", 16)
-        L.trk_set_tuning(b"rf3_groups", 0)
-        L.trk_set_tuning(b"rf3_pf", 0)
-
-
-@pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_sum_lanes_identical(trk, gpu, R):
-    """rf_sumlanes 1 (each lane converts and stores one channel's ROI sum) vs 0 (16 sums per
-    lane fr == 0): the column-sum butterfly leaves the same bits in every lane of a row
-    group, so XRN and the int64 partials must be identical."""
+@pytest.mark.parametrize("N", [768, 1024])
+def test_enc_transition_packed_weights_need_n512(trk, gpu, N):
+    """trans4 steps one K step of its packed fragments as 32 column tiles (N = 512): packed
+    weights of another N are refused by the wrapper and by the C ABI (never read in the wrong
+    order); without them gemm4 handles any N % 256 == 0 and matches the fp32 reference."""
+    import torch.nn.functional as F
     from importlib import import_module
     ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
-    g = torch.Generator().manual_seed(300 + R)
+    g = torch.Generator().manual_seed(N)
+    P, R = 100, 5
+    M = R * P
+    XRN = torch.randn(M, 1024, generator=g).to(gpu).bfloat16()
+    s = torch.rand(R, 512, generator=g).to(gpu)
+    Wt = (torch.randn(N, 1024, generator=g) / 32).to(gpu).bfloat16()
+    bt = (torch.randn(N, generator=g) / 4).to(gpu)
+    Wtp = ops.enc_pack_fragments_k(Wt)
+    with pytest.raises(ValueError, match="enc_pack_fragments_k"):
+        ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+    sums = torch.empty((R, 3, N), device=gpu, dtype=torch.int64)
+    c = lambda t: ctypes.c_void_p(t.data_ptr())
+    L = trk.lib()
+    assert L.trk_enc_transition_gemm2(c(XRN), M, P, 1024, c(s), 512, c(Wt), c(Wtp), c(bt), N, c(sums), None) == -1
+    assert b"N = 512" in L.trk_last_error()
+    st = ops.enc_transition_gemm(XRN, P, s, Wt, bt)
+    xs = (XRN[:, :512].float().view(R, P, 512) * s[:, None, :]).bfloat16().float().view(M, 512)
+    ref = F.silu(torch.cat([xs, XRN[:, 512:].float()], 1) @ Wt.float().t() + bt).view(R, P, N).sum(1)
+    assert (st - ref).abs().max().item() <= 2e-3 * ref.abs().max().item()
+
+
+def _front_operands(gpu, R, seed):
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(seed)
     X = torch.randn(R * 100, 512, generator=g).to(gpu).bfloat16()
-    W1p = ops.enc_pack_fragments((torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16())
-    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
-    W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16())
-    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
-    L = trk.lib()
-    res = {}
-    try:
-        for v in (0, 1):
-            assert L.trk_set_tuning(b"rf_sumlanes", v) == 0
-            XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-            res[v] = (XRN, ops.enc_sums_reduce(s, 100))
-        for v in (1, 2):  # issue priority of the depthwise: scheduling only, the same bits
-            assert L.trk_set_tuning(b"rf_dwprio", v) == 0
-            XRN, s = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-            res[10 + v] = (XRN, ops.enc_sums_reduce(s, 100))
-    finally:
-        L.trk_set_tuning(b"rf_sumlanes", 1)  # the defaults
-        L.trk_set_tuning(b"rf_dwprio", 0)
-    for k in (0, 11, 12):
-        assert torch.equal(res[k][0], res[1][0]) and torch.equal(res[k][1], res[1][1]), k
-
-
-def _rmb_front_vs_two_kernel(gpu, R):
-    from importlib import import_module
-    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
-    g = torch.Generator().manual_seed(R)
-    M, P = R * 100, 100
-    X = torch.randn(M, 512, generator=g).to(gpu).bfloat16()
     W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
     wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
     W2 = (torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16()
     b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
+    se = [(torch.randn(128, 512, generator=g) / 20).to(gpu), (torch.randn(128, generator=g) / 10).to(gpu),
+          (torch.randn(512, 128, generator=g) / 10).to(gpu), (torch.randn(512, generator=g) / 10).to(gpu)]
+    return ops, X, W1, wdw, W2, b2, se
+
+
+@pytest.mark.parametrize("groups", [0, 1, 14, 16, 64])
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups):
+    """trk_enc_rmb_front_means (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
+    LDS, the squeeze means written by the kernel) vs enc_g1_dwconv -> enc_dsc_gemm -> enc_se:
+    the same MFMA shape, K order and bf16 roundings, so XRN must be bit-identical; the means add
+    the same f32 activations in another order (tol 1e-5 of the largest mean).  R = 2048 is the
+    bench's c3 launch.  groups: rf3_groups, the persistent grid's workgroup pairs per XCD (0 =
+    CUs / 16 - 2, the default; 1 pair: 256 ROIs per workgroup at R = 2048, the LDS counters
+    counting on across all of them; 64: more pairs than ROIs)."""
+    ops, X, W1, wdw, W2, b2, se = _front_operands(gpu, R, R)
+    L = trk.lib()
+    P = 100
     Y2 = ops.enc_g1_dwconv(X, W1, wdw)
-    XRN2, s2 = ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True)
+    XRN2, sums2 = ops.enc_dsc_gemm(Y2, P, W2, b2, raw=True)
+    m_r2, m_n2, s2 = ops.enc_se(sums2, P, *se)
     W1p, W2p = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2)
     # the packing is a permutation: fragment (g, s, n, lane) holds W[g*512+16n+lane%16][32s+8(lane//16)+j]
     assert W1p[1, 3, 5, 2, 7, 4].item() == W1[512 + 16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
-    XRN1, s1 = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    assert L.trk_set_tuning(b"rf3_groups", groups) == 0
+    try:
+        XRN1, m_r1, m_n1 = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        XRN1b, m_r1b, m_n1b = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)  # deterministic
+        torch.cuda.synchronize()
+    finally:
+        L.trk_set_tuning(b"rf3_groups", 0)
     assert torch.equal(XRN1, XRN2)
-    f1, f2 = ops.enc_sums_reduce(s1, P), ops.enc_sums_reduce(s2, P)
-    assert (f1 - f2).abs().max().item() <= 1e-5 * f2.abs().max().item()
-    XRN1b, s1b = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)  # deterministic
-    assert torch.equal(XRN1, XRN1b) and torch.equal(ops.enc_sums_reduce(s1b, P), f1)
+    for a, b in ((m_r1, m_r2), (m_n1, m_n2)):
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
+    assert torch.equal(XRN1, XRN1b) and torch.equal(m_r1, m_r1b) and torch.equal(m_n1, m_n1b)
+    # the SE from given means is enc_se's arithmetic: the same s for the same m_r
+    assert torch.equal(ops.enc_se_means(m_r2, *se), s2)
     # unpacked weights (same numel) are refused, not read in the wrong order
     with pytest.raises(ValueError, match="enc_pack_fragments"):
-        ops.enc_rmb_front(X, W1, wdw, W2p, b2)
+        ops.enc_rmb_front_means(X, W1, wdw, W2p, b2)
     with pytest.raises(ValueError, match="enc_pack_fragments"):
-        ops.enc_rmb_front(X, W1p, wdw, W2.reshape(1024, 512), b2)
-
-
-@pytest.mark.parametrize("rf_v,groups,want_sums", [(3, 0, False), (3, 0, True), (3, 1, False), (3, 64, False),
-                                                   (2, 0, False), (2, 0, True)])
-@pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_se_vs_front_then_se(trk, gpu, R, rf_v, groups, want_sums):
-    """trk_enc_rmb_front_se (the persistent front writing the squeeze means, its reinforce
-    workgroups then running the SE over their ROIs in batches of 16) vs trk_enc_rmb_front +
-    trk_enc_se: XRN, m_r, m_n and s bit-identical (the means are the bits enc_se takes from
-    the int64 sums; the SE runs enc_se's rb_linear tiles); the sums, when asked for, equal the
-    plain front's.  R = 1 / 37: batches of fewer than 16 rows; 1 pair per XCD: 256 ROIs and 16
-    SE batches per workgroup at R = 2048; rf_v 2: the two-launch path (own workspace when
-    want_sums is off)."""
-    from importlib import import_module
-    ops = import_module(trk.__name__ + ".ops")
-    L = trk.lib()
-    g = torch.Generator().manual_seed(100 + R)
-    X = torch.randn(R * 100, 512, generator=g).to(gpu).bfloat16()
-    W1p = ops.enc_pack_fragments((torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16())
-    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
-    W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16())
-    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
-    w1 = (torch.randn(128, 512, generator=g) / 20).to(gpu)
-    bb1 = (torch.randn(128, generator=g) / 10).to(gpu)
-    w2 = (torch.randn(512, 128, generator=g) / 10).to(gpu)
-    bb2 = (torch.randn(512, generator=g) / 10).to(gpu)
-    assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf3_groups", groups) == 0
-    try:
-        XRN0, sums0 = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-        m_r0, m_n0, s0 = ops.enc_se(sums0, 100, w1, bb1, w2, bb2)
-        XRN1, sums1, m_r1, m_n1, s1 = ops.enc_rmb_front_se(X, W1p, wdw, W2p, b2, w1, bb1, w2, bb2,
-                                                          want_sums=want_sums)
-        torch.cuda.synchronize()
-    finally:
-        L.trk_set_tuning(b"rf_v", 3)
-        L.trk_set_tuning(b"rf3_groups", 0)
-    assert torch.equal(XRN1, XRN0)
-    assert torch.equal(m_r1, m_r0) and torch.equal(m_n1, m_n0)
-    assert torch.equal(s1, s0)
-    if want_sums:  # (partials past a ROI's count are never written: compare what a reader reads)
-        assert torch.equal(ops.enc_sums_reduce(sums1, 100), ops.enc_sums_reduce(sums0, 100))
-    else:
-        assert sums1 is None
-
-
-@pytest.mark.parametrize("rf_v,groups", [(3, 0), (3, 1), (2, 0)])
-@pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_means_and_se_means(trk, gpu, R, rf_v, groups):
-    """trk_enc_rmb_front_means (the front writing the squeeze means instead of the int64 sums)
-    + trk_enc_se_means (the excitation from those means) vs trk_enc_rmb_front + trk_enc_se:
-    XRN, m_r, m_n and s bit-identical.  rf_v 2: the front + enc_se's means phase on a workspace."""
-    from importlib import import_module
-    ops = import_module(trk.__name__ + ".ops")
-    L = trk.lib()
-    g = torch.Generator().manual_seed(200 + R)
-    X = torch.randn(R * 100, 512, generator=g).to(gpu).bfloat16()
-    W1p = ops.enc_pack_fragments((torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16())
-    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
-    W2p = ops.enc_pack_fragments((torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16())
-    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
-    w1 = (torch.randn(128, 512, generator=g) / 20).to(gpu)
-    bb1 = (torch.randn(128, generator=g) / 10).to(gpu)
-    w2 = (torch.randn(512, 128, generator=g) / 10).to(gpu)
-    bb2 = (torch.randn(512, generator=g) / 10).to(gpu)
-    assert L.trk_set_tuning(b"rf_v", rf_v) == 0 and L.trk_set_tuning(b"rf3_groups", groups) == 0
-    try:
-        XRN0, sums0 = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-        m_r0, m_n0, s0 = ops.enc_se(sums0, 100, w1, bb1, w2, bb2)
-        XRN1, m_r1, m_n1 = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
-        s1 = ops.enc_se_means(m_r1, w1, bb1, w2, bb2)
-        torch.cuda.synchronize()
-    finally:
-        L.trk_set_tuning(b"rf_v", 3)
-        L.trk_set_tuning(b"rf3_groups", 0)
-    assert torch.equal(XRN1, XRN0)
-    assert torch.equal(m_r1, m_r0) and torch.equal(m_n1, m_n0)
-    assert torch.equal(s1, s0)
-
-
-@pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_fused_vs_separate_kernels(trk, gpu, R):
-    """trk_enc_rmb_fused (front + SE + transition in one kernel; the normal group hands its
-    x_n rows to the reinforce group through L2) vs enc_rmb_front -> enc_se ->
-    enc_transition_gemm on the same operands.  m_r / m_n: the same lane sums and fixed-point
-    means, bit-identical.  s: the SE's f32 dot products in another order, |ds| <= 1e-6.
-    tsums: the transition with the reference path fed the fused s (identical y = bf16(x_f
-    s)), the per-channel SiLU sums in another order: within 1e-5 of the largest sum.
-    R = 1 and 37 leave padding workgroups (the grid is a multiple of 16)."""
-    from importlib import import_module
-    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
-    g = torch.Generator().manual_seed(100 + R)
-    M, P = R * 100, 100
-    X = torch.randn(M, 512, generator=g).to(gpu).bfloat16()
-    W1 = (torch.randn(1024, 512, generator=g) / 24).to(gpu).bfloat16()
-    wdw = (torch.randn(25, 1024, generator=g) / 5).to(gpu)
-    W2 = (torch.randn(2, 512, 512, generator=g) / 24).to(gpu).bfloat16()
-    b2 = (torch.randn(1024, generator=g) / 10).to(gpu)
-    Wt = (torch.randn(512, 1024, generator=g) / 32).to(gpu).bfloat16()
-    bt = (torch.randn(512, generator=g) / 10).to(gpu)
-    sw1 = (torch.randn(128, 512, generator=g) / 22).to(gpu)
-    sb1 = (torch.randn(128, generator=g) / 10).to(gpu)
-    sw2 = (torch.randn(512, 128, generator=g) / 11).to(gpu)
-    sb2 = (torch.randn(512, generator=g) / 10).to(gpu)
-    W1p, W2p, Wtp = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2), ops.enc_pack_fragments_k(Wt)
-    assert Wtp[3, 5, 2, 7, 4].item() == Wt[16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
-    m_r, m_n, s, tsums = ops.enc_rmb_fused(X, W1p, wdw, W2p, b2, Wtp, bt, sw1, sb1, sw2, sb2)
-    XRN, sums = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
-    e_r, e_n, e_s = ops.enc_se(sums, P, sw1, sb1, sw2, sb2)
-    assert torch.equal(m_r, e_r) and torch.equal(m_n, e_n)
-    assert (s - e_s).abs().max().item() <= 1e-6
-    e_t = ops.enc_transition_gemm(XRN, P, s, Wt, bt, raw=True)
-    ft, et = ops.enc_sums_reduce(tsums, P), ops.enc_sums_reduce(e_t, P)
-    assert (ft - et).abs().max().item() <= 1e-5 * et.abs().max().item()
-    m_r2, m_n2, s2, tsums2 = ops.enc_rmb_fused(X, W1p, wdw, W2p, b2, Wtp, bt, sw1, sb1, sw2, sb2)  # deterministic
-    # (partials past a ROI's count are never read: compare the reduced sums)
-    assert torch.equal(m_r, m_r2) and torch.equal(s, s2) and torch.equal(ops.enc_sums_reduce(tsums2, P), ft)
+        ops.enc_rmb_front_means(X, W1p, wdw, W2.reshape(1024, 512), b2)
 
 
 def _partials(total, P, parts=3):
@@ -1225,13 +1050,11 @@ def test_roi_align_a1_boundary_branches_gpu(trk, oracle, gpu):
             assert torch.equal(nhwc.float().cpu(), torch.from_numpy(exp).to(od).float()), (S, od)
 
 
-@pytest.mark.parametrize("split", [1, 0])
-def test_lsap_dev_split_launch_vs_host_sizes(trk, gpu, split):
-    """trk_lsap_dev (shapes in device memory, one bound for the batch) vs trk_lsap (host
-    shapes, the kernel sized by the widest matrix): lsap_split 1 (off by default) solves the matrices of at
-    most 256 columns in the narrow kernel and the wider ones in the bound's kernel; the
-    narrow launch also owns the empty and the out-of-bound matrices (status -4, assign -1
-    over the bound's rows).  Every output is bit-identical to the host-sized launch."""
+def test_lsap_dev_vs_host_sizes(trk, gpu):
+    """trk_lsap_dev (shapes in device memory, one bound for the batch, each matrix solved by
+    the body its own width needs) vs trk_lsap (host shapes, the kernel sized by the widest
+    matrix), with empty and out-of-bound matrices (status -4, assign -1 over the bound's
+    rows).  Every output is bit-identical to the host-sized launch."""
     from importlib import import_module
     ops = import_module(trk.__name__ + ".ops")
     L = trk.lib()
@@ -1254,15 +1077,11 @@ def test_lsap_dev_split_launch_vs_host_sizes(trk, gpu, split):
     dnr = torch.tensor([r for r, _ in nr], dtype=torch.int32, device=gpu)
     dnc = torch.tensor([c for _, c in nr], dtype=torch.int32, device=gpu)
     out = {k: torch.full_like(v, -7) for k, v in ref.items()}
-    assert L.trk_set_tuning(b"lsap_split", split) == 0
-    try:
-        rc = L.trk_lsap_dev(F, ops._ptr(Cg), ops._lib.TRK_F32, B, (B + 8) * B, ops._ptr(dnr), ops._ptr(dnc), B, B,
-                            kmax, ops._ptr(out["rows"]), ops._ptr(out["cols"]), ops._ptr(out["count"]),
-                            ops._ptr(out["status"]), ops._ptr(out["assign"]), B + 8, 50.0, ops._stream(gpu))
-        assert rc == 0
-        torch.cuda.synchronize()
-    finally:
-        L.trk_set_tuning(b"lsap_split", 0)
+    rc = L.trk_lsap_dev(F, ops._ptr(Cg), ops._lib.TRK_F32, B, (B + 8) * B, ops._ptr(dnr), ops._ptr(dnc), B, B,
+                        kmax, ops._ptr(out["rows"]), ops._ptr(out["cols"]), ops._ptr(out["count"]),
+                        ops._ptr(out["status"]), ops._ptr(out["assign"]), B + 8, 50.0, ops._stream(gpu))
+    assert rc == 0
+    torch.cuda.synchronize()
     cnt = ref["count"].cpu().numpy()
     assert (out["status"][:-1].cpu() == ref["status"][:-1].cpu()).all() and int(out["status"][-1]) == -4
     assert int(out["count"][-1]) == 0 and (out["assign"][-1, :B].cpu() == -1).all()

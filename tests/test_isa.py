@@ -1,6 +1,6 @@
 """ISA check of the hand-counted vmcnt waits in the rmb kernels (csrc/enc_gemm.hip).
 
-rmb_front / rmb_fused / trans4 issue their K-loop loads (weight fragments, depthwise taps,
+rmb_front3 / trans4 issue their K-loop loads (weight fragments, depthwise taps,
 prefetches, LDS-DMA) as asm statements and retire them with counted s_waitcnt vmcnt(N).
 The compiler does not know those loads are in flight: if it moved or reused a
 destination register before the covering wait, the kernel would read (or clobber) a
@@ -54,8 +54,8 @@ def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
                     "enc_gemm.hip"], cwd=c, check=True, capture_output=True)
     lines = asm.read_text().splitlines()
     found = 0
-    for name, body in IC.kernels(lines, ["rmb_front_kernel", "rmb_front2_kernel", "rmb_front3_kernel", "rmb_fused_kernel", "trans4_kernel"]):
+    for name, body in IC.kernels(lines, ["rmb_front3_kernel", "trans4_kernel"]):
         found += 1
         bad = IC.scan(body)
         assert not bad, (name, bad[:5])
-    assert found == 4 + 10  # rmb_front, rmb_front2, rmb_front3, rmb_fused + the 10 trans4 variants
+    assert found == 2  # rmb_front3 + trans4
