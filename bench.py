@@ -571,7 +571,29 @@ def kernel_pass(pipe, f, reps=10):
     C = cost_out["C_total"]
     lo = trk.lsap_batched(C, Ms, [N] * S_, cost_max=50.0)
     timed("lsap", lambda: trk.lsap_batched(C, Ms, [N] * S_, cost_max=50.0, out=lo))
-    return out, M
+    # trk_lsap_dev (sizes in device memory, the tracker's launch) on the same matrices, its launch
+    # sized by the pipeline's row bound (last_Mb: live tracks + detections in flight) and by M:
+    # the kernel instantiation (column slots) is the bound's, the solve the matrix's own
+    L = ops.lib()
+    dnr = torch.tensor(Ms, dtype=torch.int32, device=emb.device)
+    dnc = torch.full((S_,), N, dtype=torch.int32, device=emb.device)
+    Mb = max(int(tr.last_Mb), M)
+    Cp = torch.full((S_, Mb, N), 1e3, device=emb.device)
+    Cp[:, :M] = C
+    kq = min(Mb, N)
+    dv = {"rows": torch.empty((S_, kq), dtype=torch.int64, device=emb.device),
+          "cols": torch.empty((S_, kq), dtype=torch.int64, device=emb.device),
+          "count": torch.empty((S_,), dtype=torch.int32, device=emb.device),
+          "status": torch.empty((S_,), dtype=torch.int32, device=emb.device),
+          "assign": torch.empty((S_, Mb), dtype=torch.int32, device=emb.device)}
+    for name, bound in (("lsap_dev_bound", Mb), ("lsap_dev_m", M)):
+        def run(bound=bound):
+            rc = L.trk_lsap_dev(S_, ops._ptr(Cp), 0, N, Mb * N, ops._ptr(dnr), ops._ptr(dnc), bound, N, kq,
+                                ops._ptr(dv["rows"]), ops._ptr(dv["cols"]), ops._ptr(dv["count"]),
+                                ops._ptr(dv["status"]), ops._ptr(dv["assign"]), Mb, 50.0, ops._stream(emb.device))
+            assert rc == 0, rc
+        timed(name, run)
+    return out, M, {"lsap_dev_bound_rows": Mb}
 
 
 def _cpu_info():
@@ -805,7 +827,7 @@ def main():
 
     torch.cuda.synchronize()
     region.resume("isolated")
-    iso, M = kernel_pass(pipe, f - 1)
+    iso, M, iso_info = kernel_pass(pipe, f - 1)
     torch.cuda.synchronize()
     region.pause()
     # per-launch device time: live (timed region) where probed, else isolated
@@ -895,6 +917,9 @@ def main():
                                    if k in live else "isolated: back-to-back launches after the timed region")
                                for k in kt},
           "isolated_us": {k: round(v, 2) for k, v in iso.items()},
+          "isolated_note": dict(iso_info, note="lsap_dev_bound / lsap_dev_m: trk_lsap_dev on the step's stage-1 "
+                                "matrices, its launch sized by the pipeline's row bound (live tracks + detections in "
+                                "flight) or by the matrices' rows"),
           "per_kernel": per, "lsap_us_per_frame_batch": round(kt["lsap"], 2),
           "tracker_live_us_per_launch": dict(tracker_live, note="live HIP events in the timed region, per "
                                              "launch of all streams' frames; stage 2 = ReID-only rows (none "

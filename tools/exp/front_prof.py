@@ -1,4 +1,4 @@
-"""rmb_front phase cycles (s_memtime stamps of wave 0 per workgroup, trk_enc_set_prof):
+"""rmb_front3 phase cycles (s_memtime stamps of wave 0 per workgroup, trk_enc_set_prof):
 GEMM1, Y1 -> LDS, depthwise, GEMM2, activation + sums, output staging, stores, total;
 medians per DSC group (wave 0) and per wave (0 reinforce / SiLU, 1 normal / Hardswish) and isolated launch time,
 for each tuning variant given ("k=v;k=v", "" = defaults).
@@ -22,7 +22,7 @@ buf = torch.zeros(2 * R * 8 * 8, dtype=torch.int64, device=dev)
 names = ["gemm1", "y1_store", "depthwise", "gemm2", "act_sums", "staging", "stores", "total"]
 
 
-DEFAULTS = {"rf_pf": 8, "rf_v": 3, "rf_lag": 16, "rf_sumlanes": 1, "rf_dwprio": 0}  # knobs whose default is not 0
+DEFAULTS = {}  # knobs whose default is not 0
 
 
 def apply(v, reset=False):
@@ -37,7 +37,7 @@ def launch_us(v):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for _ in range(5):
-        ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+        ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
     ev[1].record()
     torch.cuda.synchronize()
     apply(v, reset=True)
@@ -56,13 +56,13 @@ for _ in range(7):
 ref = None
 for v in variants:
     apply(v)
-    out = ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    out = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
     torch.cuda.synchronize()
     if ref is None:
         ref = out
     same = torch.equal(out[0], ref[0])
     L.trk_enc_set_prof(ctypes.c_void_p(buf.data_ptr()))
-    ops.enc_rmb_front(X, W1p, wdw, W2p, b2)
+    ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
     torch.cuda.synchronize()
     L.trk_enc_set_prof(None)
     p = buf.view(R, 2, 8, 8).double().cpu()   # [roi][group][wave][phase]

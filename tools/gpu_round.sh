@@ -27,7 +27,10 @@ if [ "$SKIP_TESTS" != 1 ]; then
   step pytest 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread || exit $?
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 fi
-step bench 600 python bench.py --steps 20 --warmup 5 || exit $?
+if [ "${SKIP_BENCH:-0}" != 1 ]; then
+  step bench 600 python bench.py --steps 20 --warmup 5 || exit $?
+fi
+[ "${SKIP_PROF:-0}" = 1 ] && { echo "== done (no profiles)"; exit 0; }
 cd /tmp
 step stats 600 rocprofv3 --kernel-trace --stats --selected-regions -d "$OUT/prof_$TAG" -o run --output-format csv \
   -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline || exit $?
