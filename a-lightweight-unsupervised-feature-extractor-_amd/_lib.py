@@ -11,7 +11,9 @@ import re
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrk_amd.so")
+# TRK_LIB_PATH: another in-tree build of the same library (A/B experiments of two builds); the
+# default is the package's own libtrk_amd.so
+LIB_PATH = os.environ.get("TRK_LIB_PATH") or os.path.join(_HERE, "libtrk_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "trk_amd.h")
 
 TRK_F32, TRK_BF16, TRK_F64 = 0, 1, 2
