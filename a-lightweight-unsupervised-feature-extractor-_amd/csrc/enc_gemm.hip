@@ -21,6 +21,8 @@
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: per-workgroup phase stamps)
 int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rmb_front3 workgroup pairs per XCD (0 = CUs / 16 - 2)
+int g_rf3_chunks = 1;  // trk_set_tuning("rf3_chunks"): rmb_front3 generations (each pair's ROIs in that many
+                       // chunks, one workgroup each; 1 = one persistent generation)
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
@@ -764,6 +766,7 @@ struct RfArgs {
   uint16_t* XRN;        // [R * 100][1024] = [SiLU(x_r) | Hardswish(x_n)]
   float *m_r, *m_n;     // [R][512] the squeeze means of SiLU(x_r) / Hardswish(x_n) (trk_enc_se's)
   int64_t R;            // ROIs
+  int pairs, chunks;    // rmb_front3's grid: workgroup pairs per XCD, generations (ROI chunks)
   unsigned long long* prof;  // trk_enc_set_prof: every wave's phase cycles per ROI (diagnostics)
 };
 
@@ -996,7 +999,8 @@ __device__ __forceinline__ float rf_mean(float sum) {
 // the blocks they need are free, so half A's GEMM1 of the next ROI runs under half B's epilogue
 // of this one instead of behind a workgroup boundary
 template <int G>
-__device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride) {
+__device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride,
+                                         int64_t roi_end) {
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + RF2_CTR);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1007,7 +1011,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   g4_barrier();  // the only full barrier: counters zeroed
   int64_t roi = roi0;
-  for (uint32_t it = 0; roi < a.R; ++it, roi += stride) {
+  for (uint32_t it = 0; roi < roi_end; ++it, roi += stride) {
   const uint32_t t4 = 4u * (it + 1), p4 = 4u * it;  // counter targets: this ROI's / the previous one's
   // lane-dependent values re-derived per ROI through an opaque copy: hoisted out of the ROI
   // loop, every address the body derives from them stayed live across it (268 VGPRs spilled)
@@ -1275,16 +1279,28 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   }  // ROI loop
 }
 
-// 16 k workgroups; workgroup w sits on XCD w % 8 (the dispatcher's round robin; for speed only,
-// nothing depends on it), runs group G = (w / 8) & 1 and the ROIs xcd + 8 (p + P k), p = w / 16,
-// P = gridDim / 16 -- both groups of a ROI on one XCD, every ROI once
+// The grid is C generations of 16 P workgroups (P pairs per XCD).  Workgroup w of generation c
+// sits on XCD w % 8 (the dispatcher's round robin; for speed only, nothing depends on it), runs
+// group G = (w / 8) & 1 and the ROIs xcd + 8 (p + P k), p = (w % 16 P) / 16, for k in chunk c of
+// the pair's k range -- both groups of a ROI on one XCD, every ROI once.  C = 1: one persistent
+// generation; C > 1: workgroups retire between chunks, so kernels of other streams (the tracker's,
+// at a higher priority) are dispatched there instead of waiting for the whole launch
 __global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int w = blockIdx.x, xcd = w & 7, slot = w >> 3;
-  const int64_t P = gridDim.x / 16;
-  const int64_t roi0 = xcd + 8 * (int64_t)(slot >> 1), stride = 8 * P;
-  if (slot & 1) rf2_body<1>(a, smem, roi0, stride);
-  else rf2_body<0>(a, smem, roi0, stride);
+  const int64_t per = 16 * (int64_t)a.pairs;
+  const int64_t c = blockIdx.x / per;
+  const int w = (int)(blockIdx.x % per), xcd = w & 7, slot = w >> 3;
+  const int64_t P = a.pairs;
+  const int64_t stride = 8 * P;
+  // k range of the pair: ROIs xcd + 8 (p + P k) < R
+  const int64_t p = slot >> 1;
+  const int64_t nk = (a.R - xcd - 8 * p + stride - 1) / stride;  // ROIs of this pair (0 if none)
+  const int64_t kc = (nk + a.chunks - 1) / a.chunks;
+  const int64_t k0 = c * kc, k1 = min(nk, k0 + kc);
+  if (k0 >= k1) return;
+  const int64_t roi0 = xcd + 8 * p + stride * k0, roi_end = xcd + 8 * p + stride * (k1 - 1) + 1;
+  if (slot & 1) rf2_body<1>(a, smem, roi0, stride, roi_end);
+  else rf2_body<0>(a, smem, roi0, stride, roi_end);
 }
 
 
@@ -1740,7 +1756,12 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   // (2.03-2.05 vs 1.96-1.98M ROIs/s over four interleaved pairs against one ROI per workgroup)
   const int64_t groups =
       std::min<int64_t>((a.R + 7) / 8, g_rf3_groups > 0 ? g_rf3_groups : std::max(1, ncu / 16 - 2));
-  hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups)), dim3(512), RF2_LDS,
+  // chunks: no more than the ROIs a pair has (an empty generation would only launch and exit)
+  const int64_t per_pair = ((a.R + 7) / 8 + groups - 1) / groups;
+  const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(g_rf3_chunks, per_pair));
+  a.pairs = (int)groups;
+  a.chunks = (int)chunks;
+  hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
                      reinterpret_cast<hipStream_t>(stream), a);
   return trk::check_launch("rmb_front3_kernel");
 }

@@ -55,6 +55,8 @@ const char* trk_last_error(void);
  *                    (weights straight into VGPRs); 0: gemm4 (weights through LDS), same sums
  *   "rf3_groups"     0 (default: CUs / 16 - 2): trk_enc_rmb_front_means workgroup pairs per XCD
  *                    (1..64; all bit-identical)
+ *   "rf3_chunks"     1 (default): trk_enc_rmb_front_means as one persistent generation of
+ *                    workgroups; n: n generations, each pair's ROIs in n chunks (bit-identical)
  *   "se_waves", "head_waves"  8 or 16 (default) waves per SE / head workgroup
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
  *                    given (the device tracker), else the detection-tile kernel; 1: the

@@ -748,16 +748,18 @@ def _front_operands(gpu, R, seed):
     return ops, X, W1, wdw, W2, b2, se
 
 
-@pytest.mark.parametrize("groups", [0, 1, 14, 16, 64])
+@pytest.mark.parametrize("groups,chunks", [(0, 1), (1, 1), (14, 1), (16, 1), (64, 1), (16, 4), (1, 7), (0, 64)])
 @pytest.mark.parametrize("R", [1, 37, 2048])
-def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups):
+def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups, chunks):
     """trk_enc_rmb_front_means (first 1x1 convs + depthwise + DSC GEMMs in one kernel, Y2 in
     LDS, the squeeze means written by the kernel) vs enc_g1_dwconv -> enc_dsc_gemm -> enc_se:
     the same MFMA shape, K order and bf16 roundings, so XRN must be bit-identical; the means add
     the same f32 activations in another order (tol 1e-5 of the largest mean).  R = 2048 is the
     bench's c3 launch.  groups: rf3_groups, the persistent grid's workgroup pairs per XCD (0 =
     CUs / 16 - 2, the default; 1 pair: 256 ROIs per workgroup at R = 2048, the LDS counters
-    counting on across all of them; 64: more pairs than ROIs)."""
+    counting on across all of them; 64: more pairs than ROIs); chunks: rf3_chunks, the grid as
+    that many generations of workgroups, each running one chunk of its pair's ROIs (more
+    chunks than a pair has ROIs: capped, or empty workgroups exit)."""
     ops, X, W1, wdw, W2, b2, se = _front_operands(gpu, R, R)
     L = trk.lib()
     P = 100
@@ -767,13 +769,14 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups):
     W1p, W2p = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2)
     # the packing is a permutation: fragment (g, s, n, lane) holds W[g*512+16n+lane%16][32s+8(lane//16)+j]
     assert W1p[1, 3, 5, 2, 7, 4].item() == W1[512 + 16 * 5 + 7, 32 * 3 + 8 * 2 + 4].item()
-    assert L.trk_set_tuning(b"rf3_groups", groups) == 0
+    assert L.trk_set_tuning(b"rf3_groups", groups) == 0 and L.trk_set_tuning(b"rf3_chunks", chunks) == 0
     try:
         XRN1, m_r1, m_n1 = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
         XRN1b, m_r1b, m_n1b = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)  # deterministic
         torch.cuda.synchronize()
     finally:
         L.trk_set_tuning(b"rf3_groups", 0)
+        L.trk_set_tuning(b"rf3_chunks", 1)
     assert torch.equal(XRN1, XRN2)
     for a, b in ((m_r1, m_r2), (m_n1, m_n2)):
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
