@@ -24,6 +24,12 @@
 //    one frame (batch index) run on one XCD and its NHWC map stays in that L2.
 #include "trk_common.h"
 
+// cache policy of the row sweep's output stores (buffer aux bits; 2 = nt, non-temporal: the
+// 210 MB of ROI features stream past L2 instead of evicting the frame's map rows)
+#ifndef ROI_OUT_POLICY
+#define ROI_OUT_POLICY 0
+#endif
+
 #include <type_traits>
 
 namespace {
@@ -803,12 +809,12 @@ roi_sweep_kernel(const float* __restrict__ in,  // [B,H,W,C]
             if constexpr (OUT_BF16) {
               typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
               __builtin_amdgcn_raw_buffer_store_b64(u32x2{trk::pack2_bf16(v[0], v[1]), trk::pack2_bf16(v[2], v[3])},
-                                                    ors, ovoff[h], so_, 0);
+                                                    ors, ovoff[h], so_, ROI_OUT_POLICY);
             } else {
               typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
               __builtin_amdgcn_raw_buffer_store_b128(u32x4_{__float_as_uint(v[0]), __float_as_uint(v[1]),
                                                             __float_as_uint(v[2]), __float_as_uint(v[3])},
-                                                     ors, ovoff[h], so_, 0);
+                                                     ors, ovoff[h], so_, ROI_OUT_POLICY);
             }
           }
         }
