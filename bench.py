@@ -221,11 +221,19 @@ class Pipeline:
         # rmb_front live 657 vs 741 us)
         self.roi_after = os.environ.get("TRK_ROI_AFTER", "dsc") if self.roi_stream is not None else ""
         self.roi_gate = None
-        if self.roi_after:
+        # TRK_EMBED_OVERLAP=1 (with TRK_EMBED_STREAMS=2): frame f+1's encoder, on the other
+        # embedding stream, waits only for frame f's front (not its SE and transition), so the
+        # next front's workgroups fill the CUs the transition's last round leaves idle
+        self.overlap = os.environ.get("TRK_EMBED_OVERLAP", "0") == "1" and n_side > 1
+        self.front_ev = None
+        if self.roi_after or self.overlap:
             def hook(name):
                 if name == self.roi_after:
                     self.roi_gate = torch.cuda.Event()
                     self.roi_gate.record(torch.cuda.current_stream())
+                if self.overlap and name == "dsc":
+                    self.front_ev = torch.cuda.Event()
+                    self.front_ev.record(torch.cuda.current_stream())
             self.model.stage_hook = hook
         # NCHW maps, TRK_MAP_AHEAD=1: frame f's NCHW -> NHWC copy (roi_align's first kernel)
         # issued on the tracker's stream two frames ahead, right after frame f-2's tracker
@@ -295,6 +303,8 @@ class Pipeline:
         # and writes buffers of its own (kept alive for main by record_stream); main waits on
         # `ev`.  So the encoder runs back to back on its stream while the tracker overlaps it)
         with torch.cuda.stream(side):
+            if self.overlap and self.front_ev is not None:
+                side.wait_event(self.front_ev)  # the previous frame's front is done
             if self.graphs is not None:
                 g, rois, emb = self.graphs[f & 1]
                 rois.copy_(self.sc["rois"][f], non_blocking=True)
@@ -951,7 +961,7 @@ def main():
     rf["env"] = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL",
                                                 "AMD_SERIALIZE_COPY", "HIP_VISIBLE_DEVICES", "OMP_NUM_THREADS")
                  if os.environ.get(k) is not None}
-    rf["streams"] = {"embed": len(pipe.sides), "head_on_track_stream": pipe.defer_head,
+    rf["streams"] = {"embed": len(pipe.sides), "embed_overlap": pipe.overlap, "head_on_track_stream": pipe.defer_head,
                      "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
                      "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,
