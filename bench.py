@@ -89,7 +89,6 @@ if __name__ == "__main__":
     _spawn_ranks()
 
 import argparse
-import ctypes
 import importlib
 import json
 import time
@@ -182,10 +181,10 @@ class Pipeline:
         self.sc, self.model, self.S = sc, model, S
         self.tracker = trk.MultiStreamTracker(sc["streams"], capacity=1024, device=sc["feat"].device)
         self.ids = {}
-        # consecutive frames' embeddings alternate between two side streams, so the
-        # low-occupancy tail of frame f's encoder (SE / head: 128 workgroups) runs
-        # beside frame f+1's ROI Align and first GEMM instead of before them
-        n_side = int(os.environ.get("TRK_EMBED_STREAMS", "1"))
+        # consecutive frames' embeddings alternate between two side streams (default 2 since
+        # r05, with TRK_EMBED_OVERLAP below), so frame f's SE and transition run beside frame
+        # f+1's front instead of before it
+        n_side = int(os.environ.get("TRK_EMBED_STREAMS", "2"))
         self.sides = [torch.cuda.Stream(device=sc["feat"].device) for _ in range(n_side)]
         self.side = self.sides[0]
         self.pending = {}  # frame -> (embeddings, ready event)
@@ -221,10 +220,12 @@ class Pipeline:
         # rmb_front live 657 vs 741 us)
         self.roi_after = os.environ.get("TRK_ROI_AFTER", "dsc") if self.roi_stream is not None else ""
         self.roi_gate = None
-        # TRK_EMBED_OVERLAP=1 (with TRK_EMBED_STREAMS=2): frame f+1's encoder, on the other
-        # embedding stream, waits only for frame f's front (not its SE and transition), so the
-        # next front's workgroups fill the CUs the transition's last round leaves idle
-        self.overlap = os.environ.get("TRK_EMBED_OVERLAP", "0") == "1" and n_side > 1
+        # TRK_EMBED_OVERLAP=1 (with TRK_EMBED_STREAMS=2, both the default since r05): frame f+1's
+        # encoder, on the other embedding stream, waits only for frame f's front (not its SE and
+        # transition), so the next front's workgroups fill the CUs the transition's last round
+        # leaves idle: 2.092-2.138 vs 2.048-2.082M ROIs/s in six interleaved pairs (r5c, r5d); the
+        # front's live launch window then includes the transition it shares the GPU with
+        self.overlap = os.environ.get("TRK_EMBED_OVERLAP", "1") == "1" and n_side > 1
         self.front_ev = None
         if self.roi_after or self.overlap:
             def hook(name):
@@ -400,30 +401,13 @@ class Pipeline:
 
 
 # ----------------------------------------------------------- measurement --
-class ProfRegion:
-    """rocprofv3 --selected-regions support: the profiler collects only between
-    roctxProfilerResume(0) and roctxProfilerPause(0).  TRK_PROF_REGION picks the region this
-    run opens: "timed" (default: exactly the timed region's launches, after its opening
-    barrier + sync, closed after its closing sync) or "isolated" (kernel_pass, the
-    back-to-back launches after it).  Without rocprofv3's selected-regions mode (its
-    ROCPROF_SELECTED_REGIONS in the environment) every call is a no-op."""
-
-    def __init__(self):
-        self.which = os.environ.get("TRK_PROF_REGION", "timed")
-        self._lib = None
-        if os.environ.get("ROCPROF_SELECTED_REGIONS", "").lower() in ("1", "true", "yes", "on"):
-            lib = ctypes.CDLL("librocprofiler-sdk-roctx.so")
-            lib.roctxProfilerResume.argtypes = lib.roctxProfilerPause.argtypes = [ctypes.c_uint64]
-            self._lib = lib
-            self.pause()  # the preload starts collecting: nothing before the chosen region
-
-    def resume(self, which):
-        if self._lib is not None and which == self.which:
-            self._lib.roctxProfilerResume(0)
-
-    def pause(self):
-        if self._lib is not None:
-            self._lib.roctxProfilerPause(0)
+def prof_mark():
+    """One marker kernel (torch.cuda._sleep -> `spin_kernel`) then a device sync: bench.py
+    brackets its timed region and its isolated kernel pass with one each side, so a
+    rocprofv3 trace or counter pass of the whole run splits into those two windows by
+    dispatch order (tools/prof_window.py).  Outside the timed clock."""
+    torch.cuda._sleep(1)
+    torch.cuda.synchronize()
 
 
 def _ev():
@@ -722,24 +706,25 @@ def cpu_baseline(sc, sd, budget_s=20.0, frames_vec=20, frames_lit=6):
                 legs=legs)
 
 
-def timed_region(step, steps, dist, sync, red_dev, finish=None, own=None, region=None):
+def timed_region(step, steps, dist, sync, red_dev, finish=None, own=None, mark=None):
     """Run `steps` steps between a barrier + device sync on both sides; return
     the MAX elapsed time over ranks (one all_reduce) and the step outputs
-    (this rank's own elapsed time is appended to `own` if given).  region: a
-    ProfRegion opened right after the opening sync and closed after the closing one."""
+    (this rank's own elapsed time is appended to `own` if given).  mark: called
+    right after the opening sync and after the closing one, outside the clock
+    (prof_mark)."""
     if dist is not None:
         dist.barrier()
     sync()
-    if region is not None:
-        region.resume("timed")
+    if mark is not None:
+        mark()
     t0 = time.perf_counter()
     out = [step(k) for k in range(steps)]
     if finish is not None:
         finish()  # every frame's assignment indices read on the host
     sync()
     el = time.perf_counter() - t0
-    if region is not None:
-        region.pause()
+    if mark is not None:
+        mark()
     if own is not None:
         own.append(el)
     if dist is not None:
@@ -763,7 +748,6 @@ def main():
                          "launches on the side stream, so off by default)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
-    region = ProfRegion()  # before any GPU work: a --selected-regions profile holds only the chosen region
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -822,7 +806,7 @@ def main():
     pipe.tracker.sync_wait_s = 0.0
     own = []
     el, results = timed_region(lambda k: pipe.step(PREROLL + args.warmup + k), args.steps, dist,
-                               torch.cuda.synchronize, red_dev, finish=pipe.tracker.drain, own=own, region=region)
+                               torch.cuda.synchronize, red_dev, finish=pipe.tracker.drain, own=own, mark=prof_mark)
     el_own = own[0]
     probe.on = False
     kernel_sum = probe.sum_per_step_us(args.steps)
@@ -835,11 +819,9 @@ def main():
     value = rois_total / el
     ident = float(np.mean([pipe.check_identity(PREROLL + args.warmup + k, r) for k, r in enumerate(results)]))
 
-    torch.cuda.synchronize()
-    region.resume("isolated")
+    prof_mark()
     iso, M, iso_info = kernel_pass(pipe, f - 1)
-    torch.cuda.synchronize()
-    region.pause()
+    prof_mark()
     # per-launch device time: live (timed region) where probed, else isolated
     kt = dict(iso)
     kt.update(live)
@@ -855,7 +837,6 @@ def main():
         return
     Fs, N, S = sc["streams"], sc["N"], 10
     K = Fs * N
-    # algorithmic work per launch; DESIGN.md §Roofline
     # algorithmic work per launch: bytes that
     # must cross HBM and flops on the kernel's matrix core; the binding roof is
     # the larger of bytes / HBM peak and flops / MFMA peak
@@ -913,8 +894,8 @@ def main():
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
           "time_us": per[dom]["us"],
           "time_source": ("live: mean of the HIP-event pairs around this kernel's launches inside the timed "
-                          "region, on the stream it is launched on (the same launches a rocprofv3 "
-                          "--selected-regions run profiles, TRK_PROF_REGION=timed)" if dom in live else
+                          "region, on the stream it is launched on (the same launches tools/kernel_stats.py "
+                          "takes from a rocprofv3 trace: its timed window)" if dom in live else
                           "isolated: back-to-back launches after the timed region"),
           "isolated_time_us": None if t_iso is None else round(t_iso, 2),
           "isolated_frac": None if t_iso is None else round(per[dom]["work"] / (t_iso * 1e-6) /
@@ -944,6 +925,12 @@ def main():
                         "frac": round(value / world / cap, 4), "bytes_per_roi": round(b_roi),
                         "flops_per_roi": ENC_FLOP_PER_ROI[S],
                         "cap_rule": "min(8 TB/s / bytes_per_roi, 2.5 PFLOP/s / flops_per_roi)"}
+    # the encoder's flops per step over the step time: what the MFMA pipes achieve in the
+    # pipeline, whatever the streams' overlap does to any one launch's event window
+    enc_fl, ms = K * ENC_FLOP_PER_ROI[S], el / args.steps * 1e3
+    rf["encoder_in_pipeline"] = {"achieved": round(enc_fl / (ms * 1e-3) / 1e12, 2), "unit": "TFLOP/s",
+                                 "peak": BF16_PEAK_TFLOPS, "frac": round(enc_fl / (ms * 1e-3) / (BF16_PEAK_TFLOPS * 1e12), 4),
+                                 "rule": "encoder flops per step (all ROIs of the step) / ms_per_step"}
     # PMC bytes over algorithmic bytes per kernel (committed profile), beside each stage's fraction
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as fh:

@@ -2,21 +2,22 @@
 rocprofv3 --pmc passes (counter_collection.csv).  FETCH_SIZE is reported in
 KiB by rocprofv3 and, on gfx950, tallies 64 B per 128-B request of wide
 streaming reads (MI355X_MICROARCH.md §HBM): the corrected read bytes are
-2 x FETCH_SIZE x 1024 for 16-B/lane loads; other widths are uncalibrated."""
-import csv
-import glob
+2 x FETCH_SIZE x 1024 for 16-B/lane loads; other widths are uncalibrated.  Only the launches of
+bench.py's timed region count (tools/prof_window.py)."""
 import json
 import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_window import rows_of, select  # noqa: E402
+
 
 def load(d, counter):
-    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     acc = defaultdict(list)
-    for f in files:
+    if True:
         cost3 = []
-        for r in csv.DictReader(open(f)):
+        for r in select(rows_of(d, "*counter_collection.csv"), "timed"):
             if r.get("Counter_Name") != counter:
                 continue
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
@@ -68,7 +69,8 @@ def main():
                     tab[nm] = dict(read_bytes=round(v["read_bytes_corrected"]), write_bytes=round(v["write_bytes"]),
                                    launches=v["launches"], kernel=k[:120])
         with open(sys.argv[3], "w") as f:
-            json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (separate runs); "
+            json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (separate runs), the "
+                                 "timed region's launches only (tools/prof_window.py); "
                                  "read = 2 x FETCH_SIZE (gfx950 64-B tally of 128-B requests, MI355X_MICROARCH.md "
                                  "§HBM), per launch averages", "kernels": tab}, f, indent=1)
 
