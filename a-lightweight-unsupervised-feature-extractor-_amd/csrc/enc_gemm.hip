@@ -1588,6 +1588,281 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
   }
 }
 
+// ---------------------------------------------------------------------------
+// trans5 (trk_set_tuning("enc_trans", 2)): trans4 on 32x32x16 MFMAs.  A 16x16x32 MFMA holds the
+// SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 one for 8 of 32 (MI355X_MICROARCH.md,
+// constants table), so per flop the two co-resident workgroups' epilogue VALU, fragment reads
+// and loads get twice the issue slots beside the matrix pipe.  Same tiles, ring, SE scaling
+// and packed weight image as trans4: wave w owns 64 output columns (2 blocks of 32) for all 128
+// rows (4 blocks of 32), 16 MFMAs per K step; a lane's four B fragments of a step are gathered
+// from trans4's image (16-col tile 2 cb + ((l >> 4) & 1), chunk 2 kh + (l >> 5), row l & 15 =
+// column l & 31, k 16 kh + 8 (l >> 5) of block cb).  The ring's chunk swizzle is x32 (the
+// 32-row fragment reads' lane groups, MI355X_MICROARCH.md §LDS).  Epilogue: bias + SiLU, then
+// per-ROI column sums of SiLU(T) in f32 on the VALU (a 64-row half spans at most 2 ROIs for
+// P >= 64, 3 for P >= 43), int64 fixed point per 64-row half and lane half.  T and the sums differ from
+// trans4's by f32 rounding only (another MFMA shape and summation order).
+__device__ __forceinline__ int x32(int r) { return (r >> 2) & 3; }
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void t5_loadB(const uint4* bp, int kt, u32x4 (&d)[4]) {
+  asm volatile("" : "+v"(bp));  // per call: keeps the compiler from hoisting all 32 step addresses
+  const uint4* p = bp + kt * 32 * 64;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d[0]) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:512" : "=v"(d[1]) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:2048" : "=v"(d[2]) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:2560" : "=v"(d[3]) : "v"(p) : "memory");
+}
+
+template <int SPS, int BD>
+__global__ void __launch_bounds__(256, 2) trans5_kernel(EncGemmArgs a, const uint4* Wtp, int64_t ntiles) {
+  static_assert(t4_vm_ok<SPS, BD>(), "trans5 vmcnt out of the rf_vmwait range");
+  constexpr int NS = T4_NK / SPS, NSLOT = 3 * SPS;
+  constexpr size_t RING = (size_t)NSLOT * T4_BUF * 16;
+  static_assert(NSLOT == 3, "trans5's sum partials use ring slots 0 and 2");
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t lb = xcd_remap(blockIdx.x, ntiles);
+  uint4* ring = reinterpret_cast<uint4*>(smem);
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntile_n = a.N / 256;
+  const int n0 = (int)(lb % ntile_n) * 256;
+  const int64_t m0 = lb / ntile_n * 128;
+  const int64_t roi_base = m0 / a.P;
+  const int l32 = lane & 31, lh = lane >> 5;
+
+  const uint16_t* asrc[2];
+  int arow[2], achk[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x32(r);
+    arow[q] = r;
+    achk[q] = c;
+    asrc[q] = a.A + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
+  }
+  const uint4* bp = Wtp + (size_t)(n0 / 16 + wave * 4) * 64 + 64 * ((lane >> 4) & 1) + 16 * lh + (lane & 15);
+  u32x4 bq[BD + 1][4];
+  auto issueA = [&](int st) {  // the SPS K steps of stage st
+#pragma unroll
+    for (int u = 0; u < SPS; ++u) {
+      const int kt = st * SPS + u;
+      uint4* d = ring + (kt % NSLOT) * T4_BUF + wave * 64;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
+    }
+  };
+  auto loadB = [&](int kt) { t5_loadB(bp, kt, bq[kt % (BD + 1)]); };
+
+  float* stile = reinterpret_cast<float*>(smem + RING);
+  const float* srow[2];
+  {
+    const int per = 512 / 4;
+    const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
+    const int tslots = min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = q * 256 + tid;
+      if (p >= tslots * per) continue;
+      const int slot = min(p / per, G4_SLOTS - 1);
+      const int64_t roi = min(roi_base + slot, nroi - 1);
+      __builtin_amdgcn_global_load_lds(GPTR(a.scale + roi * 512 + (p % per) * 4),
+                                       LPTR(reinterpret_cast<uint4*>(stile) + q * 256 + wave * 64), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t row = min(m0 + arow[q], (int64_t)a.M - 1);
+      srow[q] = stile + (int)(row / a.P - roi_base) * 512 + achk[q] * 8;
+    }
+  }
+  auto transform = [&](int kt) {
+    const uint32_t d = lds_addr(ring + (kt % NSLOT) * T4_BUF + tid);
+    u32x4 v[2], s4[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      v[q] = lds_read128(d + q * 256 * 16);
+      const uint32_t sa = lds_addr(srow[q] + kt * BK);
+      s4[q][0] = lds_read128(sa);
+      s4[q][1] = lds_read128(sa + 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(s4[0][0]), "+v"(s4[0][1]), "+v"(s4[1][0]),
+                 "+v"(s4[1][1])::"memory");
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float s_lo = __uint_as_float(s4[q][e >> 1][(2 * e) & 3]);
+        const float s_hi = __uint_as_float(s4[q][e >> 1][(2 * e + 1) & 3]);
+        o[e] = pack_bf16x2(__uint_as_float(v[q][e] << 16) * s_lo, __uint_as_float(v[q][e] & 0xffff0000u) * s_hi);
+      }
+      lds_write128(d + q * 256 * 16, o);
+    }
+  };
+  auto transform_stage = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < SPS; ++u)
+      if ((st * SPS + u) * BK < 512) transform(st * SPS + u);
+  };
+
+  // fragment (row block rb, k half kh) of a stage: row 32 rb + (l & 31), chunk 2 kh + (l >> 5)
+  const int lt0 = l32 * 4 + ((0 + lh) ^ x32(l32)), lt1 = l32 * 4 + ((2 + lh) ^ x32(l32));
+  f16v acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][c][v] = 0.f;
+
+  unsigned long long pst[8];
+  const bool prof = a.prof != nullptr;
+  if (prof) pst[0] = eg_stamp();
+  issueA(0);
+  loadB(0);
+  issueA(1);
+  loadB(1);
+#pragma unroll
+  for (int b = 2; b < BD; ++b) loadB(b);
+  rf_vmwait(t4_vm<SPS, BD>(-1), bq[0]);
+  g4_barrier();
+  transform_stage(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  g4_barrier();
+  auto step = [&](auto ktc) {
+    constexpr int kt = decltype(ktc)::value;
+    const uint4* buf = ring + (kt % NSLOT) * T4_BUF;
+    bf8v afr[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      afr[i][0] = *reinterpret_cast<const bf8v*>(buf + lt0 + i * 128);
+      afr[i][1] = *reinterpret_cast<const bf8v*>(buf + lt1 + i * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              afr[i][kh], __builtin_bit_cast(bf8v, bq[kt % (BD + 1)][c * 2 + kh]), acc[i][c], 0, 0, 0);
+      if (i == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kt + BD < T4_NK) loadB(kt + BD);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (i == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (kt + 1 < T4_NK) {
+      rf_vmwait(t4_vm<SPS, BD>(kt), bq[(kt + 1) % (BD + 1)]);
+      if constexpr ((kt + 1) % SPS == 0) {
+        transform_stage((kt + 1) / SPS);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        g4_barrier();
+      }
+    }
+  };
+  seq_for(step, std::make_integer_sequence<int, T4_NK>{});
+  if (prof) pst[1] = eg_stamp();
+
+  // ---- SiLU(T + bias): lane l holds column 32 c + (l & 31) of the wave's 64, rows
+  // 32 i + 8 (v >> 2) + 4 (l >> 5) + (v & 3)
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float bv = a.bias[n0 + wave * 64 + c * 32 + l32];
+    const f2v b2 = {bv, bv};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; v += 2) {
+        f2v x = f2v{acc[i][c][v], acc[i][c][v + 1]} + b2;
+        x = silu2(x);
+        acc[i][c][v] = x.x;
+        acc[i][c][v + 1] = x.y;
+      }
+  }
+  if (prof) pst[2] = eg_stamp();
+  // ---- per-ROI column sums per 64-row half h: the half's rows fall into NS consecutive ROI
+  // slots from its first row's (NS = 2 for P >= 64, 3 down to P = 43), rows past M into none.
+  // Partials [h][slot][256] of lane half 0 in ring slot 0, of lane half 1 in ring slot 2
+  // (both idle since step 30's barrier)
+  {
+    float* part = reinterpret_cast<float*>(smem + (lh ? 2 : 0) * T4_BUF * 16);
+    const int P = a.P;
+    const int off = (int)(m0 - roi_base * P);
+    const int ml = (int)min((int64_t)128, (int64_t)a.M - m0) - 4 * lh;
+    auto half_sums = [&](auto ns_c) {
+      constexpr int NS = decltype(ns_c)::value;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int slot0 = (off + 64 * h) / P;
+        int lim[NS];  // rows r < lim[j] (and past the slots before) belong to slot slot0 + j
+#pragma unroll
+        for (int j = 0; j < NS; ++j) lim[j] = min((slot0 + 1 + j) * P - off - 4 * lh, ml);
+        lim[NS - 1] = ml;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          float sj[NS];
+#pragma unroll
+          for (int j = 0; j < NS; ++j) sj[j] = 0.f;
+#pragma unroll
+          for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+              const int r = i * 32 + 8 * (v >> 2) + (v & 3);
+              const float x = acc[i][c][v];
+              sj[0] += r < lim[0] ? x : 0.f;
+#pragma unroll
+              for (int j = 1; j < NS; ++j) sj[j] += (r >= lim[j - 1] && r < lim[j]) ? x : 0.f;
+            }
+          const int col = wave * 64 + c * 32 + l32;
+#pragma unroll
+          for (int ts = 0; ts < G4_SLOTS; ++ts) {
+            float o = 0.f;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) o = ts == slot0 + j ? sj[j] : o;
+            part[(h * G4_SLOTS + ts) * 256 + col] = o;
+          }
+        }
+      }
+    };
+    if (P >= 64) half_sums(std::integral_constant<int, 2>{});
+    else half_sums(std::integral_constant<int, 3>{});
+  }
+  if (prof) pst[3] = eg_stamp();
+  __syncthreads();
+  {
+    const float* p0 = reinterpret_cast<const float*>(smem);
+    const float* p1 = reinterpret_cast<const float*>(smem + 2 * T4_BUF * 16);
+    const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
+    const int nslot = (int)(last_row / a.P - roi_base) + 1;
+    for (int q = tid; q < nslot * 256; q += 256) {
+      const int slot = q >> 8, c = q & 255;
+      const int64_t roi = roi_base + slot;
+      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
+      const int i0 = slot * 256 + c, i1 = (G4_SLOTS + slot) * 256 + c;
+      a.sums[(roi * kPart + j) * a.ld_sums + n0 + c] = llrintf(p0[i0] * kFix) + llrintf(p0[i1] * kFix) +
+                                                       llrintf(p1[i0] * kFix) + llrintf(p1[i1] * kFix);
+    }
+  }
+  if (prof) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pst[4] = eg_stamp();
+    if (tid == 0) {
+      unsigned long long* o = a.prof + lb * 8;
+      for (int q = 0; q < 4; ++q) o[q] = pst[q + 1] - pst[q];
+      o[4] = pst[4] - pst[0];
+      o[5] = o[6] = o[7] = 0;
+    }
+  }
+}
+
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
@@ -1679,11 +1954,16 @@ extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, i
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  if (g_enc_trans == 1 && Wtp) {
+  if (g_enc_trans >= 1 && Wtp) {
     const int64_t nwg = ((int64_t)M + 127) / 128 * (N / 256);
     TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
     a.prof = g_enc_prof;
     const size_t slds = (size_t)G4_SLOTS * 512 * 4;
+    if (g_enc_trans == 2) {
+      hipLaunchKernelGGL((trans5_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a,
+                         reinterpret_cast<const uint4*>(Wtp), nwg);
+      return trk::check_launch("trans5_kernel");
+    }
     hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a,
                        reinterpret_cast<const uint4*>(Wtp), nwg);
     return trk::check_launch("trans4_kernel");

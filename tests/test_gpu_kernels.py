@@ -705,6 +705,39 @@ def test_enc_transition_trans4_vs_gemm4(trk, gpu, P, R):
         ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp[:-1])
 
 
+@pytest.mark.parametrize("P,R", [(100, 1), (100, 37), (100, 2048), (200, 23), (49, 29), (43, 7)])
+def test_enc_transition_trans5_vs_fp32(trk, gpu, P, R):
+    """trans5 (enc_trans 2: trans4 on 32x32x16 MFMAs, the ROI sums on the VALU) vs a torch
+    fp32 reference on the same SE-scaled bf16 rows (2e-3 of the largest sum, as the other
+    transition paths) and vs trans4 (f32 rounding apart: 1e-4 of the largest sum); ROIs
+    straddle the 128-row tiles and 64-row halves, the last tile is partial; deterministic."""
+    import torch.nn.functional as F
+    from importlib import import_module
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    g = torch.Generator().manual_seed(3000 + R + P)
+    M, Ng = R * P, 512
+    XRN = torch.randn(M, 2 * Ng, generator=g).to(gpu).bfloat16()
+    s = torch.rand(R, Ng, generator=g).to(gpu)
+    Wt = (torch.randn(Ng, 2 * Ng, generator=g) / 32).to(gpu).bfloat16()
+    bt = (torch.randn(Ng, generator=g) / 4).to(gpu)
+    Wtp = ops.enc_pack_fragments_k(Wt)
+    L = trk.lib()
+    try:
+        assert L.trk_set_tuning(b"enc_trans", 1) == 0
+        t4 = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+        assert L.trk_set_tuning(b"enc_trans", 2) == 0
+        got = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+        got2 = ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+    finally:
+        L.trk_set_tuning(b"enc_trans", 1)
+    assert torch.equal(got, got2)
+    xs = (XRN[:, :Ng].float().view(R, P, Ng) * s[:, None, :]).bfloat16().float().view(M, Ng)
+    ref = F.silu(torch.cat([xs, XRN[:, Ng:].float()], 1) @ Wt.float().t() + bt).view(R, P, Ng).sum(1)
+    top = ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= 2e-3 * top
+    assert (got - t4).abs().max().item() <= 1e-4 * top
+
+
 @pytest.mark.parametrize("N", [768, 1024])
 def test_enc_transition_packed_weights_need_n512(trk, gpu, N):
     """trans4 steps one K step of its packed fragments as 32 column tiles (N = 512): packed
