@@ -823,6 +823,38 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups, chunks):
         ops.enc_rmb_front_means(X, W1p, wdw, W2.reshape(1024, 512), b2)
 
 
+@pytest.mark.parametrize("groups,chunks", [(0, 1), (1, 1), (16, 4)])
+@pytest.mark.parametrize("R", [1, 37, 2048])
+def test_enc_rmb_front_mfma32_vs_mfma16(trk, gpu, R, groups, chunks):
+    """rf_mfma 32 (rmb_front3 on 32x32x16 MFMAs: 128-pixel tiles whose pixels 100..127 read the
+    next LDS block's rows and are dropped, the ROI sums by a halving butterfly) vs the default
+    16x16x32 front on the same packed weights: the GEMMs sum the same bf16 products in another
+    grouping, so a Y1 / Y2 / XRN value can round to the neighbouring bf16 (2^-8 relative) and
+    move what it feeds; bounded: XRN within 2e-2 of its largest value and >= 95 % identical, the
+    means within 2e-3 of the largest mean; deterministic run to run."""
+    ops, X, W1, wdw, W2, b2, se = _front_operands(gpu, R, 5000 + R)
+    L = trk.lib()
+    W1p, W2p = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2)
+    assert L.trk_set_tuning(b"rf3_groups", groups) == 0 and L.trk_set_tuning(b"rf3_chunks", chunks) == 0
+    try:
+        XRN16, m_r16, m_n16 = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        assert L.trk_set_tuning(b"rf_mfma", 32) == 0
+        XRN32, m_r32, m_n32 = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        XRN32b, m_r32b, m_n32b = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        torch.cuda.synchronize()
+    finally:
+        L.trk_set_tuning(b"rf_mfma", 16)
+        L.trk_set_tuning(b"rf3_groups", 0)
+        L.trk_set_tuning(b"rf3_chunks", 1)
+    assert torch.equal(XRN32, XRN32b) and torch.equal(m_r32, m_r32b) and torch.equal(m_n32, m_n32b)
+    assert torch.isfinite(XRN32.float()).all()
+    d = (XRN32.float() - XRN16.float()).abs()
+    assert d.max().item() <= 2e-2 * XRN16.float().abs().max().item()
+    assert (d == 0).float().mean().item() >= 0.95
+    for a, b in ((m_r32, m_r16), (m_n32, m_n16)):
+        assert (a - b).abs().max().item() <= 2e-3 * b.abs().max().item()
+
+
 def _partials(total, P, parts=3):
     """split int64 per-ROI totals [R, ld] into the GEMMs' partial layout
     [R, parts, ld] (one entry per 128-row tile covering the ROI; the rest junk)"""

@@ -58,4 +58,4 @@ def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
         found += 1
         bad = IC.scan(body)
         assert not bad, (name, bad[:5])
-    assert found == 3  # rmb_front3 + trans4 + trans5
+    assert found == 4  # rmb_front3<16>, <32> + trans4 + trans5
