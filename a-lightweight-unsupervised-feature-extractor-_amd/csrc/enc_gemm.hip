@@ -23,7 +23,6 @@ unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: per
 int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rmb_front3 workgroup pairs per XCD (0 = CUs / 16 - 2)
 int g_rf3_chunks = 1;  // trk_set_tuning("rf3_chunks"): rmb_front3 generations (each pair's ROIs in that many
                        // chunks, one workgroup each; 1 = one persistent generation)
-int g_rf_mfma = 16;  // trk_set_tuning("rf_mfma"): rmb_front3's MFMA shape, 16 (16x16x32) or 32 (32x32x16)
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
@@ -771,23 +770,19 @@ struct RfArgs {
   unsigned long long* prof;  // trk_enc_set_prof: every wave's phase cycles per ROI (diagnostics)
 };
 
-// chunk swizzle of the front's LDS image rows: (s >> 1) & 3 for the 16x16x32 fragment reads,
-// (s >> 2) & 3 for the 32x32x16 ones (rows 32 pb + (l & 31), chunk 2 kh + (l >> 5): each
-// ds_read_b128 lane group of x16's comment lands on 16 distinct slots)
-template <int MF>
-__device__ __forceinline__ int rf_sw(int s) { return MF == 32 ? (s >> 2) & 3 : (s >> 1) & 3; }
+__device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
 // depthwise 5x5 of output quadrant (QY, QX) for the lane's channel pair, results
 // held as packed bf16 pairs (the caller writes them back in place after a barrier);
 // same per-output FMA order as dw5q_regs.  Pixel s sits at dword b[rf_sw(s)] + 16 s (s is
 // a constant after unrolling).
-template <int MF, int QY, int QX>
+template <int QY, int QX>
 __device__ __forceinline__ void rf_dw5q(const uint32_t* y, const int (&b)[4], const dw_pair_t (&w)[25],
                                         uint32_t (&out)[25]) {
   constexpr int OY0 = 5 * QY, X0 = 5 * QX;
   constexpr int IY0 = OY0 - 2 < 0 ? 0 : OY0 - 2, IY1 = OY0 + 6 > G1_S - 1 ? G1_S - 1 : OY0 + 6;
   constexpr int IX0 = X0 - 2 < 0 ? 0 : X0 - 2, IX1 = X0 + 6 > G1_S - 1 ? G1_S - 1 : X0 + 6;
   constexpr int NX = IX1 - IX0 + 1;
-  auto at = [&](int s) { return y[b[rf_sw<MF>(s)] + s * 16]; };
+  auto at = [&](int s) { return y[b[rf_sw(s)] + s * 16]; };
   dw_pair_t acc[5][5];
 #pragma unroll
   for (int oy = 0; oy < 5; ++oy)
@@ -827,14 +822,14 @@ __device__ __forceinline__ void rf_dw5q(const uint32_t* y, const int (&b)[4], co
 #pragma unroll
     for (int ox = 0; ox < 5; ++ox) out[oy * 5 + ox] = pack_bf16x2(acc[oy][ox].x, acc[oy][ox].y);
 }
-template <int MF, int QY, int QX>
+template <int QY, int QX>
 __device__ __forceinline__ void rf_dw5q_store(uint32_t* y, const int (&b)[4], const uint32_t (&out)[25]) {
 #pragma unroll
   for (int oy = 0; oy < 5; ++oy)
 #pragma unroll
     for (int ox = 0; ox < 5; ++ox) {
       const int s = (5 * QY + oy) * G1_S + 5 * QX + ox;
-      y[b[rf_sw<MF>(s)] + s * 16] = out[oy * 5 + ox];
+      y[b[rf_sw(s)] + s * 16] = out[oy * 5 + ox];
     }
 }
 
@@ -881,93 +876,6 @@ __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f
   }
 }
 
-// The 32x32x16 forms (rf_mfma 32): a wave's 64 channels x 128 pixels (pixels 100..127 are
-// padding: their LDS rows belong to the next block, their results are dropped) as 2 channel
-// blocks x 4 pixel blocks of 32x32, 16 MFMAs per K step instead of 28 (MI355X_MICROARCH.md:
-// a 16x16x32 MFMA holds the SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 one for 8
-// of 32).  Weight fragment (channel block cb, k half kh) gathered from the same packed image
-// (ops.enc_pack_fragments: 16-col tile 2 cb + ((l >> 4) & 1), chunk 2 kh + (l >> 5), row
-// l & 15) at byte offset 2048 cb + 512 kh from the lane's base; lane (l & 31, l >> 5) of
-// tile (pb, cb) ends up with channels 32 cb + 8 q + 4 (l >> 5) .. + 3 (q = 0..3) of pixel
-// 32 pb + (l & 31)
-typedef float f16v __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ void rf_loadB32(const uint4* bp, int kt, u32x4 (&d)[4]) {
-  asm volatile("" : "+v"(bp));  // per call: keeps the compiler from hoisting all 32 step addresses
-  const uint4* p = bp + kt * 32 * 64;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d[0]) : "v"(p) : "memory");
-  asm volatile("global_load_dwordx4 %0, %1, off offset:512" : "=v"(d[1]) : "v"(p) : "memory");
-  asm volatile("global_load_dwordx4 %0, %1, off offset:2048" : "=v"(d[2]) : "v"(p) : "memory");
-  asm volatile("global_load_dwordx4 %0, %1, off offset:2560" : "=v"(d[3]) : "v"(p) : "memory");
-}
-// one K step: the 8 X fragments (pixel block pb, k half kh at byte a_kh + 2048 pb of the
-// block) read up front, each pixel block's 4 MFMAs wait (counted lgkmcnt) for its own two
-__device__ __forceinline__ void rf_mfma_step32(uint32_t a0, uint32_t a1, const u32x4 (&b)[4], f16v (&acc)[4][2]) {
-  u32x4 xq[4][2];
-  asm volatile("ds_read_b128 %0, %1" : "=v"(xq[0][0]) : "v"(a0) : "memory");
-  asm volatile("ds_read_b128 %0, %1" : "=v"(xq[0][1]) : "v"(a1) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(xq[1][0]) : "v"(a0) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(xq[1][1]) : "v"(a1) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(xq[2][0]) : "v"(a0) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(xq[2][1]) : "v"(a1) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(xq[3][0]) : "v"(a0) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(xq[3][1]) : "v"(a1) : "memory");
-#pragma unroll
-  for (int pb = 0; pb < 4; ++pb) {
-    __builtin_amdgcn_sched_barrier(0);
-    if (pb == 0) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(xq[0][0]), "+v"(xq[0][1]));
-    else if (pb == 1) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xq[1][0]), "+v"(xq[1][1]));
-    else if (pb == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(xq[2][0]), "+v"(xq[2][1]));
-    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xq[3][0]), "+v"(xq[3][1]));
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-        acc[pb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, b[cb * 2 + kh]),
-                                                              __builtin_bit_cast(bf8v, xq[pb][kh]), acc[pb][cb], 0, 0, 0);
-  }
-}
-// lane ^ d for d = 1, 2 (DPP quad_perm), 4, 16 (ds_swizzle xor within 32 lanes), 8 (DPP row_ror 8)
-template <int D>
-__device__ __forceinline__ float lane_xor(float v) {
-  const int x = __float_as_int(v);
-  if constexpr (D == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true));
-  else if constexpr (D == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true));
-  else if constexpr (D == 8) return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true));
-  else return __int_as_float(__builtin_amdgcn_ds_swizzle(x, (D << 10) | 0x1F));
-}
-template <int D, int N>
-__device__ __forceinline__ void rf_halve(float (&x)[32], bool up) {
-#pragma unroll
-  for (int j = 0; j < N / 2; ++j) {
-    const float keep = up ? x[j + N / 2] : x[j], send = up ? x[j] : x[j + N / 2];
-    x[j] = keep + lane_xor<D>(send);
-  }
-}
-// the ROI sums of the wave's 64 channels: the pixel blocks added per lane (block 3 for pixels
-// < 100 only), then a halving butterfly over the 32 lanes of each lane half, after which lane l
-// holds value j = l & 31 (channel block j >> 4, element j & 15: rf_lane_ch32)
-__device__ __forceinline__ float rf_colsum32(const f16v (&acc)[4][2], int l32) {
-  float x[32];
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      float t = acc[0][cb][v] + acc[1][cb][v] + acc[2][cb][v];
-      if (l32 < RF_S - 96) t += acc[3][cb][v];
-      x[cb * 16 + v] = t;
-    }
-  rf_halve<16, 32>(x, l32 & 16);
-  rf_halve<8, 16>(x, l32 & 8);
-  rf_halve<4, 8>(x, l32 & 4);
-  rf_halve<2, 4>(x, l32 & 2);
-  rf_halve<1, 2>(x, l32 & 1);
-  return x[0];
-}
-__device__ __forceinline__ int rf_lane_ch32(int wave, int lane) {
-  const int j = lane & 31;
-  return wave * 64 + (j >> 4) * 32 + 8 * ((j & 15) >> 2) + 4 * (lane >> 5) + (j & 3);
-}
-
 // Decoupled halves: half A (waves 0..3, one per SIMD) produces Y1 / Y2 channels 0..255 and
 // half B (waves 4..7) channels 256..511; the depthwise of a half only reads its own half's Y1,
 // so the only cross-half dependencies are GEMM2's K steps 8..15 (Y2(B)) and the LDS regions
@@ -979,7 +887,7 @@ __device__ __forceinline__ int rf_lane_ch32(int wave, int lane) {
 // Y(A); once both halves finished GEMM1, blocks 8..15 = Y(B) and blocks 0..7 = A's output
 // staging; B stages over Y(A) after both halves' GEMM2.
 constexpr int RF2_NB = 24;
-constexpr size_t RF2_CTR = (size_t)(RF2_NB - 1) * RF_KBS * 4 + 128 * 64;  // past block 23's row-127 reads
+constexpr size_t RF2_CTR = (size_t)(RF2_NB - 1) * RF_KBS * 4 + 112 * 64;  // past block 23's row-111 reads
 enum { RF2_CX = 0, RF2_CG1 = 4, RF2_CY1 = 6, RF2_CDW = 8, RF2_CY2 = 12, RF2_CG2 = 14, RF2_CST = 16, RF2_CSD = 18,
        RF2_NCTR = 20 };
 constexpr size_t RF2_LDS = RF2_CTR + RF2_NCTR * 4;
@@ -990,10 +898,9 @@ constexpr uint32_t kRf2Spin = 1u << 22;  // poll bound (~0.1 s): a lost signal e
 
 // Y block of K block kb (32 channels): channels 0..255 in blocks 16..23, 256..511 in 8..15
 __device__ __forceinline__ int rf2_yblk(int kb) { return kb < 8 ? kb + 16 : kb; }
-template <int MF>
 __device__ __forceinline__ int rf2_yaddr(int s, int col) {
   const int kb = col >> 5, c = (col & 31) >> 3, d = (col & 7) >> 1;
-  return rf2_yblk(kb) * RF_KBS + s * 16 + ((c ^ rf_sw<MF>(s)) << 2) + d;
+  return rf2_yblk(kb) * RF_KBS + s * 16 + ((c ^ rf_sw(s)) << 2) + d;
 }
 // this wave's LDS writes (and any LDS-DMA it waited for) have landed: count it (lane 0
 // only).  Both hand-off halves are single asm statements: a C++ loop or lane branch here
@@ -1082,7 +989,7 @@ __device__ __forceinline__ float rf_mean(float sum) {
 // The workgroup's ROIs roi0, roi0 + stride, ...: ROI it + 1's X DMA and GEMM1 start as soon as
 // the blocks they need are free, so half A's GEMM1 of the next ROI runs under half B's epilogue
 // of this one instead of behind a workgroup boundary
-template <int G, int MF>
+template <int G>
 __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride,
                                          int64_t roi_end) {
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
@@ -1110,8 +1017,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   // X -> blocks 0..15, moved by half A only (2 DMA ops per block per wave: pieces
   // 100 hw + lane and 100 hw + 64 + lane < 400, piece p = row p >> 2, slot p & 3)
   const int xp1 = 100 * hw + lane, xp2 = 100 * hw + 64 + lane;
-  const uint16_t* xs1 = a.X + (r0 + (xp1 >> 2)) * 512 + (((xp1 & 3) ^ rf_sw<MF>(xp1 >> 2)) * 8);
-  const uint16_t* xs2 = a.X + (r0 + min(xp2 >> 2, RF_S - 1)) * 512 + (((xp2 & 3) ^ rf_sw<MF>(xp2 >> 2)) * 8);
+  const uint16_t* xs1 = a.X + (r0 + (xp1 >> 2)) * 512 + (((xp1 & 3) ^ rf_sw(xp1 >> 2)) * 8);
+  const uint16_t* xs2 = a.X + (r0 + min(xp2 >> 2, RF_S - 1)) * 512 + (((xp2 & 3) ^ rf_sw(xp2 >> 2)) * 8);
   // the X DMA as asm (M0 and, for the 36-lane second op, exec set explicitly): with the
   // builtin under `if (lane < 36)` the persistent variant's compiler merged the two ops of
   // consecutive blocks across the divergent region and issued a 36-lane op with every lane
@@ -1127,46 +1034,17 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
       rf_dma16_lanes36(p2 + kb * BK, d + 1024);
     }
   };
-  const int l32 = lane & 31, lh = lane >> 5;
-  const int wlane = MF == 32 ? 64 * ((lane >> 4) & 1) + 16 * lh + (lane & 15) : lane;
-  const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + wlane;
-  const uint4* b2p = a.W2p + ((size_t)G * NK * 32 + wave * 4) * 64 + wlane;
+  const uint4* b1p = a.W1p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
+  const uint4* b2p = a.W2p + ((size_t)G * NK * 32 + wave * 4) * 64 + lane;
   u32x4 bq[3][4];
-  const int lterm = fr * 4 + (fc ^ rf_sw<MF>(fr));
+  const int lterm = fr * 4 + (fc ^ rf_sw(fr));
   const uint32_t y_a = lds_addr(Y) + lterm * 16;
-  // 32x32x16: X fragment (pixel block 0, k half kh) at y_k[kh] + the block's byte offset
-  const uint32_t y_k0 = lds_addr(Y) + (l32 * 4 + ((0 + lh) ^ rf_sw<MF>(l32))) * 16;
-  const uint32_t y_k1 = lds_addr(Y) + (l32 * 4 + ((2 + lh) ^ rf_sw<MF>(l32))) * 16;
-  auto loadB = [&](const uint4* bp, int kt, u32x4(&d)[4]) {
-    if constexpr (MF == 32) rf_loadB32(bp, kt, d);
-    else rf_loadB(bp, kt, d);
-  };
-  using AccT = std::conditional_t<MF == 32, f16v[4][2], f4v[7][4]>;
-  AccT acc;
-  auto zero_acc = [&]() {
-    if constexpr (MF == 32) {
+
+  f4v acc[7][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 7; ++i)
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int v = 0; v < 16; ++v) acc[i][c][v] = 0.f;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto mfma_step = [&](uint32_t blk_off, u32x4(&b)[4]) {
-    if constexpr (MF == 32) rf_mfma_step32(y_k0 + blk_off, y_k1 + blk_off, b, acc);
-    else rf_mfma_step(y_a + blk_off, b, acc);
-  };
-  auto acc_last = [&]() {  // an operand that keeps the stamps behind the last MFMA's result
-    if constexpr (MF == 32) return acc[3][1][15];
-    else return acc[6][3][3];
-  };
-  zero_acc();
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
 
   // ---- GEMM1 (K = 512 over X blocks 0..15); A: 8 DMA ops per group, B: none.  One
   // loop per half (HALF a template constant): a half test inside the unrolled loop costs
@@ -1183,8 +1061,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
       issueX(0);
       issueX(1);
     }
-    loadB(b1p, 0, bq[0]);
-    loadB(b1p, 1, bq[1]);
+    rf_loadB(b1p, 0, bq[0]);
+    rf_loadB(b1p, 1, bq[1]);
 #pragma unroll
     for (int kt = 0; kt < NK; ++kt) {
       u32x4(&b)[4] = bq[kt % 3];
@@ -1210,8 +1088,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
         rf_vmwait(kt + 1 < NK ? 4 : 0, b);
         if (kt % 4 == 0) rf2_wait(ctr + RF2_CX + kt / 4, t4);
       }
-      if (kt + 2 < NK) loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
-      mfma_step(kt * RF_KBS * 4, b);
+      if (kt + 2 < NK) rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
+      rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
     }
   };
   __builtin_amdgcn_s_setprio(1);
@@ -1227,7 +1105,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   __builtin_amdgcn_s_setprio(0);
   rf2_signal(ctr + RF2_CG1 + half, lane);  // this wave's reads of X are done
   if (prof) {
-    asm volatile("" ::"v"(acc_last()));
+    asm volatile("" ::"v"(acc[6][3][3]));
     pst[1] = eg_stamp();
   }
   // B's Y1 goes over X blocks 8..15: every wave of both halves must be past GEMM1; A's over
@@ -1239,32 +1117,15 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     rf2_wait(ctr + RF2_CSD + 1, p4);
   }
   // ---- Y1 -> LDS (the wave's 64 channels of its half's region)
-  if constexpr (MF == 32) {
 #pragma unroll
-    for (int pb = 0; pb < 4; ++pb) {
-      const int px = pb * 32 + l32;
-      if (px < RF_S) {
+  for (int i = 0; i < 7; ++i) {
+    const int px = i * 16 + fr;
+    if (px < RF_S) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f16v& v = acc[pb][c];
-            *reinterpret_cast<uint2*>(Y + rf2_yaddr<MF>(px, wave * 64 + c * 32 + 8 * q + 4 * lh)) =
-                make_uint2(pack_bf16x2(v[4 * q], v[4 * q + 1]), pack_bf16x2(v[4 * q + 2], v[4 * q + 3]));
-          }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int px = i * 16 + fr;
-      if (px < RF_S) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f4v v = acc[i][t];
-          *reinterpret_cast<uint2*>(Y + rf2_yaddr<MF>(px, wave * 64 + t * 16 + fc * 4)) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
+      for (int t = 0; t < 4; ++t) {
+        const f4v v = acc[i][t];
+        *reinterpret_cast<uint2*>(Y + rf2_yaddr(px, wave * 64 + t * 16 + fc * 4)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       }
     }
   }
@@ -1276,8 +1137,8 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     for (int k = 0; k < 25; ++k)
       asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(wreg[k]) : "v"(wp + k * 1024) : "memory");
   }
-  loadB(b2p, 0, bq[0]);
-  loadB(b2p, 1, bq[1]);
+  rf_loadB(b2p, 0, bq[0]);
+  rf_loadB(b2p, 1, bq[1]);
   rf2_signal(ctr + RF2_CY1 + half, lane);
   rf2_wait(ctr + RF2_CY1 + half, t4);  // the half's Y1 is in
   if (prof) pst[2] = eg_stamp();
@@ -1295,27 +1156,30 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
                        kb0 * RF_KBS + ((c0 ^ 2) << 2) + d0, kb0 * RF_KBS + ((c0 ^ 3) << 2) + d0};
     uint32_t o0[25], o1[25];
     if ((wave & 1) == 0) {
-      rf_dw5q<MF, 0, 0>(Y, yb, wreg, o0);
-      rf_dw5q<MF, 0, 1>(Y, yb, wreg, o1);
+      rf_dw5q<0, 0>(Y, yb, wreg, o0);
+      rf_dw5q<0, 1>(Y, yb, wreg, o1);
       rf2_signal(ctr + RF2_CDW + cg, lane);
       rf2_wait(ctr + RF2_CDW + cg, 2 * (it + 1));
-      rf_dw5q_store<MF, 0, 0>(Y, yb, o0);
-      rf_dw5q_store<MF, 0, 1>(Y, yb, o1);
+      rf_dw5q_store<0, 0>(Y, yb, o0);
+      rf_dw5q_store<0, 1>(Y, yb, o1);
     } else {
-      rf_dw5q<MF, 1, 0>(Y, yb, wreg, o0);
-      rf_dw5q<MF, 1, 1>(Y, yb, wreg, o1);
+      rf_dw5q<1, 0>(Y, yb, wreg, o0);
+      rf_dw5q<1, 1>(Y, yb, wreg, o1);
       rf2_signal(ctr + RF2_CDW + cg, lane);
       rf2_wait(ctr + RF2_CDW + cg, 2 * (it + 1));
-      rf_dw5q_store<MF, 1, 0>(Y, yb, o0);
-      rf_dw5q_store<MF, 1, 1>(Y, yb, o1);
+      rf_dw5q_store<1, 0>(Y, yb, o0);
+      rf_dw5q_store<1, 1>(Y, yb, o1);
     }
   }
   rf2_signal(ctr + RF2_CY2 + half, lane);
   if (prof) pst[3] = eg_stamp();
 
   // ---- GEMM2: K steps 0..7 read Y2(A), 8..15 Y2(B)
-  float4 bias4[MF == 32 ? 8 : 4];
-  zero_acc();
+  float4 bias4[4];
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
@@ -1323,60 +1187,35 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     rf_vmwait(kt + 1 < NK ? 4 : 0, b);
     if (kt == 0) rf2_wait(ctr + RF2_CY2 + 0, t4);
     if (kt == 8) rf2_wait(ctr + RF2_CY2 + 1, t4);
-    if (kt + 2 < NK) loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
+    if (kt + 2 < NK) rf_loadB(b2p, kt + 2, bq[(kt + 2) % 3]);
     if (kt == NK - 3) {
-      if constexpr (MF == 16) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
-      }
+      for (int t = 0; t < 4; ++t)
+        bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
     }
-    mfma_step(rf2_yblk(kt) * RF_KBS * 4, b);
-  }
-  if constexpr (MF == 32) {  // (32 registers: loaded after the K loop, whose fragments are dead)
-#pragma unroll
-    for (int t = 0; t < 8; ++t)  // channels 32 (t >> 2) + 8 (t & 3) + 4 lh ..
-      bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + (t >> 2) * 32 + 8 * (t & 3) + 4 * lh);
+    rf_mfma_step(y_a + rf2_yblk(kt) * RF_KBS * 4, b, acc);
   }
   __builtin_amdgcn_s_setprio(0);
   rf2_signal(ctr + RF2_CG2 + half, lane);  // this wave's reads of the Y image are done
   if (prof) {
-    asm volatile("" ::"v"(acc_last()));
+    asm volatile("" ::"v"(acc[6][3][3]));
     pst[4] = eg_stamp();
   }
   // ---- epilogue: BN-folded bias + activation, ROI column sums (rf_body's)
-  if constexpr (MF == 32) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
-      const int c = t >> 2, q = t & 3;
+  for (int t = 0; t < 4; ++t) {
+    const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
 #pragma unroll
-      for (int pb = 0; pb < 4; ++pb)
+    for (int i = 0; i < 7; ++i)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f2v v = f2v{acc[pb][c][4 * q + 2 * h], acc[pb][c][4 * q + 2 * h + 1]} + (h ? b23 : b01);
-          v = G == 1 ? hswish2(v) : silu2(v);
-          acc[pb][c][4 * q + 2 * h] = v.x;
-          acc[pb][c][4 * q + 2 * h + 1] = v.y;
-        }
-    }
-    // every lane converts and stores one channel's squeeze mean
-    const float x = rf_colsum32(acc, l32);
-    (G == 0 ? a.m_r : a.m_n)[roi * 512 + rf_lane_ch32(wave, lane)] = rf_mean(x);
-  } else {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const f2v b01 = {bias4[t].x, bias4[t].y}, b23 = {bias4[t].z, bias4[t].w};
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
-          v = G == 1 ? hswish2(v) : silu2(v);
-          acc[i][t][2 * h] = v.x;
-          acc[i][t][2 * h + 1] = v.y;
-        }
-    }
+      for (int h = 0; h < 2; ++h) {
+        f2v v = f2v{acc[i][t][2 * h], acc[i][t][2 * h + 1]} + (h ? b23 : b01);
+        v = G == 1 ? hswish2(v) : silu2(v);
+        acc[i][t][2 * h] = v.x;
+        acc[i][t][2 * h + 1] = v.y;
+      }
+  }
+  {
     // every lane converts and stores one channel's squeeze mean (the butterfly leaves all 16
     // sums of a row group in every lane of it)
     const float x = rf_colsum(acc, fr);
@@ -1392,34 +1231,16 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     rf2_wait(ctr + RF2_CG2 + 1, t4);
   }
   uint32_t* stg = Y + (half ? 16 * RF_KBS : 0);
-  if constexpr (MF == 32) {
 #pragma unroll
-    for (int pb = 0; pb < 4; ++pb) {
-      const int px = pb * 32 + l32;
-      if (px < RF_S) {
+  for (int i = 0; i < 7; ++i) {
+    const int px = i * 16 + fr;
+    if (px < RF_S) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f16v& v = acc[pb][c];
-            const int ch = hw * 64 + c * 32 + 8 * q + 4 * lh;  // channel within the half
-            *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((ch >> 3) ^ (px & 15)) << 2) + ((ch & 7) >> 1)) =
-                make_uint2(pack_bf16x2(v[4 * q], v[4 * q + 1]), pack_bf16x2(v[4 * q + 2], v[4 * q + 3]));
-          }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int px = i * 16 + fr;
-      if (px < RF_S) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f4v v = acc[i][t];
-          const int ch = hw * 64 + t * 16 + fc * 4;  // channel within the half
-          *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((ch >> 3) ^ (px & 15)) << 2) + ((ch & 7) >> 1)) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
+      for (int t = 0; t < 4; ++t) {
+        const f4v v = acc[i][t];
+        const int ch = hw * 64 + t * 16 + fc * 4;  // channel within the half
+        *reinterpret_cast<uint2*>(stg + px * RF2_SROW + (((ch >> 3) ^ (px & 15)) << 2) + ((ch & 7) >> 1)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       }
     }
   }
@@ -1455,7 +1276,6 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
 // the pair's k range -- both groups of a ROI on one XCD, every ROI once.  C = 1: one persistent
 // generation; C > 1: workgroups retire between chunks, so kernels of other streams (the tracker's,
 // at a higher priority) are dispatched there instead of waiting for the whole launch
-template <int MF>
 __global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t per = 16 * (int64_t)a.pairs;
@@ -1470,8 +1290,8 @@ __global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
   const int64_t k0 = c * kc, k1 = min(nk, k0 + kc);
   if (k0 >= k1) return;
   const int64_t roi0 = xcd + 8 * p + stride * k0, roi_end = xcd + 8 * p + stride * (k1 - 1) + 1;
-  if (slot & 1) rf2_body<1, MF>(a, smem, roi0, stride, roi_end);
-  else rf2_body<0, MF>(a, smem, roi0, stride, roi_end);
+  if (slot & 1) rf2_body<1>(a, smem, roi0, stride, roi_end);
+  else rf2_body<0>(a, smem, roi0, stride, roi_end);
 }
 
 
@@ -1768,281 +1588,6 @@ __global__ void __launch_bounds__(256, 2) trans4_kernel(EncGemmArgs a, const uin
   }
 }
 
-// ---------------------------------------------------------------------------
-// trans5 (trk_set_tuning("enc_trans", 2)): trans4 on 32x32x16 MFMAs.  A 16x16x32 MFMA holds the
-// SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 one for 8 of 32 (MI355X_MICROARCH.md,
-// constants table), so per flop the two co-resident workgroups' epilogue VALU, fragment reads
-// and loads get twice the issue slots beside the matrix pipe.  Same tiles, ring, SE scaling
-// and packed weight image as trans4: wave w owns 64 output columns (2 blocks of 32) for all 128
-// rows (4 blocks of 32), 16 MFMAs per K step; a lane's four B fragments of a step are gathered
-// from trans4's image (16-col tile 2 cb + ((l >> 4) & 1), chunk 2 kh + (l >> 5), row l & 15 =
-// column l & 31, k 16 kh + 8 (l >> 5) of block cb).  The ring's chunk swizzle is x32 (the
-// 32-row fragment reads' lane groups, MI355X_MICROARCH.md §LDS).  Epilogue: bias + SiLU, then
-// per-ROI column sums of SiLU(T) in f32 on the VALU (a 64-row half spans at most 2 ROIs for
-// P >= 64, 3 for P >= 43), int64 fixed point per 64-row half and lane half.  T and the sums differ from
-// trans4's by f32 rounding only (another MFMA shape and summation order).
-__device__ __forceinline__ int x32(int r) { return (r >> 2) & 3; }
-typedef float f16v __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ void t5_loadB(const uint4* bp, int kt, u32x4 (&d)[4]) {
-  asm volatile("" : "+v"(bp));  // per call: keeps the compiler from hoisting all 32 step addresses
-  const uint4* p = bp + kt * 32 * 64;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d[0]) : "v"(p) : "memory");
-  asm volatile("global_load_dwordx4 %0, %1, off offset:512" : "=v"(d[1]) : "v"(p) : "memory");
-  asm volatile("global_load_dwordx4 %0, %1, off offset:2048" : "=v"(d[2]) : "v"(p) : "memory");
-  asm volatile("global_load_dwordx4 %0, %1, off offset:2560" : "=v"(d[3]) : "v"(p) : "memory");
-}
-
-template <int SPS, int BD>
-__global__ void __launch_bounds__(256, 2) trans5_kernel(EncGemmArgs a, const uint4* Wtp, int64_t ntiles) {
-  static_assert(t4_vm_ok<SPS, BD>(), "trans5 vmcnt out of the rf_vmwait range");
-  constexpr int NS = T4_NK / SPS, NSLOT = 3 * SPS;
-  constexpr size_t RING = (size_t)NSLOT * T4_BUF * 16;
-  static_assert(NSLOT == 3, "trans5's sum partials use ring slots 0 and 2");
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t lb = xcd_remap(blockIdx.x, ntiles);
-  uint4* ring = reinterpret_cast<uint4*>(smem);
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntile_n = a.N / 256;
-  const int n0 = (int)(lb % ntile_n) * 256;
-  const int64_t m0 = lb / ntile_n * 128;
-  const int64_t roi_base = m0 / a.P;
-  const int l32 = lane & 31, lh = lane >> 5;
-
-  const uint16_t* asrc[2];
-  int arow[2], achk[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int p = q * 256 + tid, r = p >> 2, c = (p & 3) ^ x32(r);
-    arow[q] = r;
-    achk[q] = c;
-    asrc[q] = a.A + min(m0 + r, (int64_t)a.M - 1) * a.lda + c * 8;
-  }
-  const uint4* bp = Wtp + (size_t)(n0 / 16 + wave * 4) * 64 + 64 * ((lane >> 4) & 1) + 16 * lh + (lane & 15);
-  u32x4 bq[BD + 1][4];
-  auto issueA = [&](int st) {  // the SPS K steps of stage st
-#pragma unroll
-    for (int u = 0; u < SPS; ++u) {
-      const int kt = st * SPS + u;
-      uint4* d = ring + (kt % NSLOT) * T4_BUF + wave * 64;
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        __builtin_amdgcn_global_load_lds(GPTR(asrc[q] + kt * BK), LPTR(d + q * 256), 16, 0, 0);
-    }
-  };
-  auto loadB = [&](int kt) { t5_loadB(bp, kt, bq[kt % (BD + 1)]); };
-
-  float* stile = reinterpret_cast<float*>(smem + RING);
-  const float* srow[2];
-  {
-    const int per = 512 / 4;
-    const int64_t nroi = ((int64_t)a.M + a.P - 1) / a.P;
-    const int tslots = min(G4_SLOTS, (127 + a.P - 1) / a.P + 1);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = q * 256 + tid;
-      if (p >= tslots * per) continue;
-      const int slot = min(p / per, G4_SLOTS - 1);
-      const int64_t roi = min(roi_base + slot, nroi - 1);
-      __builtin_amdgcn_global_load_lds(GPTR(a.scale + roi * 512 + (p % per) * 4),
-                                       LPTR(reinterpret_cast<uint4*>(stile) + q * 256 + wave * 64), 16, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int64_t row = min(m0 + arow[q], (int64_t)a.M - 1);
-      srow[q] = stile + (int)(row / a.P - roi_base) * 512 + achk[q] * 8;
-    }
-  }
-  auto transform = [&](int kt) {
-    const uint32_t d = lds_addr(ring + (kt % NSLOT) * T4_BUF + tid);
-    u32x4 v[2], s4[2][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      v[q] = lds_read128(d + q * 256 * 16);
-      const uint32_t sa = lds_addr(srow[q] + kt * BK);
-      s4[q][0] = lds_read128(sa);
-      s4[q][1] = lds_read128(sa + 16);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(s4[0][0]), "+v"(s4[0][1]), "+v"(s4[1][0]),
-                 "+v"(s4[1][1])::"memory");
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      u32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float s_lo = __uint_as_float(s4[q][e >> 1][(2 * e) & 3]);
-        const float s_hi = __uint_as_float(s4[q][e >> 1][(2 * e + 1) & 3]);
-        o[e] = pack_bf16x2(__uint_as_float(v[q][e] << 16) * s_lo, __uint_as_float(v[q][e] & 0xffff0000u) * s_hi);
-      }
-      lds_write128(d + q * 256 * 16, o);
-    }
-  };
-  auto transform_stage = [&](int st) {
-#pragma unroll
-    for (int u = 0; u < SPS; ++u)
-      if ((st * SPS + u) * BK < 512) transform(st * SPS + u);
-  };
-
-  // fragment (row block rb, k half kh) of a stage: row 32 rb + (l & 31), chunk 2 kh + (l >> 5)
-  const int lt0 = l32 * 4 + ((0 + lh) ^ x32(l32)), lt1 = l32 * 4 + ((2 + lh) ^ x32(l32));
-  f16v acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][c][v] = 0.f;
-
-  unsigned long long pst[8];
-  const bool prof = a.prof != nullptr;
-  if (prof) pst[0] = eg_stamp();
-  issueA(0);
-  loadB(0);
-  issueA(1);
-  loadB(1);
-#pragma unroll
-  for (int b = 2; b < BD; ++b) loadB(b);
-  rf_vmwait(t4_vm<SPS, BD>(-1), bq[0]);
-  g4_barrier();
-  transform_stage(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  g4_barrier();
-  auto step = [&](auto ktc) {
-    constexpr int kt = decltype(ktc)::value;
-    const uint4* buf = ring + (kt % NSLOT) * T4_BUF;
-    bf8v afr[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      afr[i][0] = *reinterpret_cast<const bf8v*>(buf + lt0 + i * 128);
-      afr[i][1] = *reinterpret_cast<const bf8v*>(buf + lt1 + i * 128);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-          acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              afr[i][kh], __builtin_bit_cast(bf8v, bq[kt % (BD + 1)][c * 2 + kh]), acc[i][c], 0, 0, 0);
-      if (i == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (kt + BD < T4_NK) loadB(kt + BD);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (i == 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (kt % SPS == 0 && kt / SPS + 2 < NS) issueA(kt / SPS + 2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (kt + 1 < T4_NK) {
-      rf_vmwait(t4_vm<SPS, BD>(kt), bq[(kt + 1) % (BD + 1)]);
-      if constexpr ((kt + 1) % SPS == 0) {
-        transform_stage((kt + 1) / SPS);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        g4_barrier();
-      }
-    }
-  };
-  seq_for(step, std::make_integer_sequence<int, T4_NK>{});
-  if (prof) pst[1] = eg_stamp();
-
-  // ---- SiLU(T + bias): lane l holds column 32 c + (l & 31) of the wave's 64, rows
-  // 32 i + 8 (v >> 2) + 4 (l >> 5) + (v & 3)
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float bv = a.bias[n0 + wave * 64 + c * 32 + l32];
-    const f2v b2 = {bv, bv};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int v = 0; v < 16; v += 2) {
-        f2v x = f2v{acc[i][c][v], acc[i][c][v + 1]} + b2;
-        x = silu2(x);
-        acc[i][c][v] = x.x;
-        acc[i][c][v + 1] = x.y;
-      }
-  }
-  if (prof) pst[2] = eg_stamp();
-  // ---- per-ROI column sums per 64-row half h: the half's rows fall into NS consecutive ROI
-  // slots from its first row's (NS = 2 for P >= 64, 3 down to P = 43), rows past M into none.
-  // Partials [h][slot][256] of lane half 0 in ring slot 0, of lane half 1 in ring slot 2
-  // (both idle since step 30's barrier)
-  {
-    float* part = reinterpret_cast<float*>(smem + (lh ? 2 : 0) * T4_BUF * 16);
-    const int P = a.P;
-    const int off = (int)(m0 - roi_base * P);
-    const int ml = (int)min((int64_t)128, (int64_t)a.M - m0) - 4 * lh;
-    auto half_sums = [&](auto ns_c) {
-      constexpr int NS = decltype(ns_c)::value;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int slot0 = (off + 64 * h) / P;
-        int lim[NS];  // rows r < lim[j] (and past the slots before) belong to slot slot0 + j
-#pragma unroll
-        for (int j = 0; j < NS; ++j) lim[j] = min((slot0 + 1 + j) * P - off - 4 * lh, ml);
-        lim[NS - 1] = ml;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          float sj[NS];
-#pragma unroll
-          for (int j = 0; j < NS; ++j) sj[j] = 0.f;
-#pragma unroll
-          for (int i = 2 * h; i < 2 * h + 2; ++i)
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-              const int r = i * 32 + 8 * (v >> 2) + (v & 3);
-              const float x = acc[i][c][v];
-              sj[0] += r < lim[0] ? x : 0.f;
-#pragma unroll
-              for (int j = 1; j < NS; ++j) sj[j] += (r >= lim[j - 1] && r < lim[j]) ? x : 0.f;
-            }
-          const int col = wave * 64 + c * 32 + l32;
-#pragma unroll
-          for (int ts = 0; ts < G4_SLOTS; ++ts) {
-            float o = 0.f;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) o = ts == slot0 + j ? sj[j] : o;
-            part[(h * G4_SLOTS + ts) * 256 + col] = o;
-          }
-        }
-      }
-    };
-    if (P >= 64) half_sums(std::integral_constant<int, 2>{});
-    else half_sums(std::integral_constant<int, 3>{});
-  }
-  if (prof) pst[3] = eg_stamp();
-  __syncthreads();
-  {
-    const float* p0 = reinterpret_cast<const float*>(smem);
-    const float* p1 = reinterpret_cast<const float*>(smem + 2 * T4_BUF * 16);
-    const int64_t last_row = min(m0 + 128, (int64_t)a.M) - 1;
-    const int nslot = (int)(last_row / a.P - roi_base) + 1;
-    for (int q = tid; q < nslot * 256; q += 256) {
-      const int slot = q >> 8, c = q & 255;
-      const int64_t roi = roi_base + slot;
-      const int j = (int)(m0 / kPartRows - roi * a.P / kPartRows);
-      const int i0 = slot * 256 + c, i1 = (G4_SLOTS + slot) * 256 + c;
-      a.sums[(roi * kPart + j) * a.ld_sums + n0 + c] = llrintf(p0[i0] * kFix) + llrintf(p0[i1] * kFix) +
-                                                       llrintf(p1[i0] * kFix) + llrintf(p1[i1] * kFix);
-    }
-  }
-  if (prof) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pst[4] = eg_stamp();
-    if (tid == 0) {
-      unsigned long long* o = a.prof + lb * 8;
-      for (int q = 0; q < 4; ++q) o[q] = pst[q + 1] - pst[q];
-      o[4] = pst[4] - pst[0];
-      o[5] = o[6] = o[7] = 0;
-    }
-  }
-}
-
 template <int EPI>
 int launch4(const EncGemmArgs& a, hipStream_t st) {
   const int64_t nwg = ((int64_t)a.M + 127) / 128 * (a.N / 256) * a.groups;
@@ -2134,16 +1679,11 @@ extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, i
   a.sums = sums; a.ld_sums = (int)N;
   a.scale = s;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P; a.groups = 1; a.kscale = (int)kscale;
-  if (g_enc_trans >= 1 && Wtp) {
+  if (g_enc_trans == 1 && Wtp) {
     const int64_t nwg = ((int64_t)M + 127) / 128 * (N / 256);
     TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
     a.prof = g_enc_prof;
     const size_t slds = (size_t)G4_SLOTS * 512 * 4;
-    if (g_enc_trans == 2) {
-      hipLaunchKernelGGL((trans5_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a,
-                         reinterpret_cast<const uint4*>(Wtp), nwg);
-      return trk::check_launch("trans5_kernel");
-    }
     hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a,
                        reinterpret_cast<const uint4*>(Wtp), nwg);
     return trk::check_launch("trans4_kernel");
@@ -2185,9 +1725,7 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16) ncu = 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel<16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel<32>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
     attr = true;
   }
@@ -2214,12 +1752,8 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(g_rf3_chunks, per_pair));
   a.pairs = (int)groups;
   a.chunks = (int)chunks;
-  if (g_rf_mfma == 32)
-    hipLaunchKernelGGL(rmb_front3_kernel<32>, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
-                       reinterpret_cast<hipStream_t>(stream), a);
-  else
-    hipLaunchKernelGGL(rmb_front3_kernel<16>, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
-                       reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
+                     reinterpret_cast<hipStream_t>(stream), a);
   return trk::check_launch("rmb_front3_kernel");
 }
 

@@ -54,8 +54,8 @@ def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
                     "enc_gemm.hip"], cwd=c, check=True, capture_output=True)
     lines = asm.read_text().splitlines()
     found = 0
-    for name, body in IC.kernels(lines, ["rmb_front3_kernel", "trans4_kernel", "trans5_kernel"]):
+    for name, body in IC.kernels(lines, ["rmb_front3_kernel", "trans4_kernel"]):
         found += 1
         bad = IC.scan(body)
         assert not bad, (name, bad[:5])
-    assert found == 4  # rmb_front3<16>, <32> + trans4 + trans5
+    assert found == 2  # rmb_front3 + trans4
