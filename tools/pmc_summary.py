@@ -55,7 +55,8 @@ def main():
                        "gemm4_kernel<0": "enc_gemm_dsc", "gemm4_kernel<1": "enc_gemm_trans",
                        "enc_se_kernel": "enc_se", "enc_head_kernel": "enc_head", "det_nms_kernel": "det_nms",
                        "lsap_kernel": "lsap", "act_mean_kernel": "act_mean", "scale_rows_kernel": "scale_rows",
-                       "nchw_to_nhwc_kernel": "nchw_to_nhwc", "track_update_kernel": "track_update"}
+                       "nchw_to_nhwc_kernel": "nchw_to_nhwc", "nchw_to_nhwc4_kernel": "nchw_to_nhwc",
+                       "track_update_kernel": "track_update"}
         tab = {}
         for k, v in out.items():
             if k.startswith("cost3_kernel stage"):
