@@ -890,6 +890,20 @@ def main():
     except (OSError, KeyError, ValueError):
         pass
     t_iso = iso.get(dom)
+    # the committed counter pass's timed window (profiles/pmc_clock.json, tools/pmc_clock.py): the
+    # profiler runs each dispatch alone, so this is the kernel's own time at the clock it held
+    ser = None
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_clock.json")) as fh:
+            pc = json.load(fh)
+        e = pc["timed"].get(dom)
+        if e is not None:
+            ser = {"time_us": e["avg_us"], "clock_ghz": e["clock_ghz"],
+                   "frac": round(per[dom]["work"] / (e["avg_us"] * 1e-6) /
+                                 (per[dom]["peak"] * (1e12 if per[dom]["unit"] == "TFLOP/s" else 1e9)), 4),
+                   "source": pc.get("profile", "profiles/pmc_clock.json")}
+    except (OSError, KeyError, ValueError, TypeError):
+        pass
     rf = {"kernel": dom, "bound": per[dom]["bound"], "achieved": per[dom]["achieved"],
           "peak": per[dom]["peak"], "unit": per[dom]["unit"], "frac": per[dom]["frac"],
           "time_us": per[dom]["us"],
@@ -901,6 +915,7 @@ def main():
           "isolated_frac": None if t_iso is None else round(per[dom]["work"] / (t_iso * 1e-6) /
                                                             (per[dom]["peak"] * (1e12 if per[dom]["unit"] == "TFLOP/s"
                                                                                  else 1e9)), 4),
+          "serialised": ser,
           "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": algo[dom][0],
           "algorithmic_flops_per_launch": algo[dom][1], "kernel_us": {k: round(v, 2) for k, v in kt.items()},
           "kernel_us_source": {k: ("live: HIP events around each launch in the timed region (with two "

@@ -35,7 +35,10 @@ if os.path.exists(pm):
     cp(f"pmc_{tag}_summary.txt", f"{tag}_pmc_summary.txt")
 cp(f"pmc_sq_{tag}.json", f"{tag}_pmc_sq.json")
 cp(f"pmc_sq_{tag}.txt", f"{tag}_pmc_sq.txt")
-cp(f"pmc_clock_{tag}.json", f"{tag}_pmc_clock.json")
+if cp(f"pmc_clock_{tag}.json", f"{tag}_pmc_clock.json"):  # what bench.py's roofline.serialised reads
+    d = json.load(open(os.path.join(out, f"pmc_clock_{tag}.json")))
+    d["profile"] = f"profiles/{tag}_pmc_clock.json"
+    json.dump(d, open(os.path.join(prof, "pmc_clock.json"), "w"), indent=1)
 cp(f"pmc_clock_{tag}.txt", f"{tag}_pmc_clock.txt")
 for name in ("bench.log", f"{tag}_bench.log"):
     p = os.path.join(out, name)
