@@ -859,16 +859,21 @@ __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f
   asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(aq[4]) : "v"(ab) : "memory");
   asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(aq[5]) : "v"(ab) : "memory");
   asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(aq[6]) : "v"(ab) : "memory");
+  // the waits are not tied to aq[i] ("+v" made the compiler treat the asm as a VALU write of
+  // the MFMA's B operand and pad every wait with an s_nop: 224 per wave and ROI); the
+  // scheduling barriers keep each tile's MFMAs behind its wait (tests/test_isa.py checks
+  // the compiled order)
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     __builtin_amdgcn_sched_barrier(0);
-    if (i == 0) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(aq[0]));
-    else if (i == 1) asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(aq[1]));
-    else if (i == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(aq[2]));
-    else if (i == 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(aq[3]));
-    else if (i == 4) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(aq[4]));
-    else if (i == 5) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(aq[5]));
-    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(aq[6]));
+    if (i == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+    else if (i == 1) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
+    else if (i == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    else if (i == 3) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+    else if (i == 4) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+    else if (i == 5) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     const bf8v xf = __builtin_bit_cast(bf8v, aq[i]);
 #pragma unroll
     for (int t = 0; t < 4; ++t)

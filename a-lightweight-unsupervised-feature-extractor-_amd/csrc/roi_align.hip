@@ -123,9 +123,12 @@ nchw_to_nhwc_kernel(const float* __restrict__ in, float* __restrict__ out,
 }
 
 // The same transpose with 16-B accesses on both sides (HW % 4 == 0, C % 4 == 0):
-// 16 lanes read 64 consecutive pixels of one channel, 16 lanes write 64
-// consecutive channels of one pixel (256 B each); the 4 x 4 element turn goes
-// through the LDS tile.  HBM-bound: 2 x 4 B per element.
+// 8 lanes read 32 consecutive pixels of one channel, 8 lanes write 32
+// consecutive channels of one pixel (128 B each); the 4 x 4 element turn goes
+// through the LDS tile.  HBM-bound: 2 x 4 B per element.  Thread -> (q, r0) puts
+// the 32 lanes of a half-wave on q = 8 h + 0..7, r0 = 4 g + 0..3, so their 4-B
+// tile accesses (bank = row + column mod 32 with the 65-float row) fall on 32
+// distinct banks in both phases (16 lanes x 16 q: 2-way conflicts)
 __global__ void __launch_bounds__(256)
 nchw_to_nhwc4_kernel(const float* __restrict__ in, float* __restrict__ out, int C, int HW, int gx, int gy) {
   __shared__ float tile[64][65];
@@ -134,7 +137,8 @@ nchw_to_nhwc4_kernel(const float* __restrict__ in, float* __restrict__ out, int 
   const int c0 = tb.cy * 64, p0 = tb.px * 64;
   const float* src = in + b * (int64_t)C * HW;
   float* dst = out + b * (int64_t)C * HW;
-  const int q = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+  const int t = threadIdx.x;
+  const int q = (((t >> 5) & 1) << 3) | (t & 7), r0 = ((t >> 6) << 2) | ((t >> 3) & 3);
   float4 v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {

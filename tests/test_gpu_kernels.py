@@ -59,6 +59,17 @@ def test_roi_align_bit_exact_vs_oracle(trk, oracle, gpu, N, S):
     assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16())
 
 
+@pytest.mark.parametrize("shape", [(8, 512, 40, 40), (2, 36, 13, 12), (1, 70, 9, 7), (3, 4, 1, 4)])
+def test_nchw_to_nhwc_transpose(trk, gpu, shape):
+    """The map transpose roi_align runs on NCHW input (float4 kernel when C and H*W are
+    multiples of 4, else the scalar one): exactly torch's channels_last copy, partial 64 x 64
+    tiles at the channel and pixel ends included."""
+    x = torch.randn(shape, generator=torch.Generator().manual_seed(sum(shape))).to(gpu)
+    got = trk.nchw_to_nhwc(x)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, x.contiguous(memory_format=torch.channels_last))
+
+
 def test_roi_align_batched_frames_and_edges(trk, oracle, gpu):
     rng = np.random.default_rng(3)
     B, N = 8, 256

@@ -1,4 +1,4 @@
-"""ISA check of the hand-counted vmcnt waits in the rmb kernels (csrc/enc_gemm.hip).
+"""ISA check of the hand-counted vmcnt / lgkmcnt waits in the rmb kernels (csrc/enc_gemm.hip).
 
 rmb_front3 / trans4 issue their K-loop loads (weight fragments, depthwise taps,
 prefetches, LDS-DMA) as asm statements and retire them with counted s_waitcnt vmcnt(N).
@@ -38,6 +38,15 @@ def test_scanner_flags_an_early_use():
     assert IC.scan(["\tglobal_load_dword v3, v[0:1], off", "\tv_mov_b32_e32 v3, 0"])
     assert not IC.scan(["\tglobal_load_dword v3, v[0:1], off", "\tscratch_load_dword v3, off, off offset:4"])
     assert IC.scan(["\tglobal_load_dword v0, v[0:1], off", "\tglobal_load_dword v3, v[0:1], off"])
+    # LDS reads against lgkmcnt: in-order retirement, and nothing retires but lgkmcnt(0) while a
+    # scalar load (out of order) is outstanding
+    lds = ["\tds_read_b128 v[4:7], v0", "\tds_read_b128 v[8:11], v0 offset:1024", "\ts_waitcnt lgkmcnt(1)",
+           "\tv_mfma_f32_16x16x32_bf16 v[20:23], v[12:15], v[4:7], v[20:23]",
+           "\tv_mfma_f32_16x16x32_bf16 v[24:27], v[12:15], v[8:11], v[24:27]"]
+    assert [b[0] for b in IC.scan_lds(lds)] == [4]
+    assert not IC.scan_lds(lds[:2] + ["\ts_waitcnt lgkmcnt(0)"] + lds[3:])
+    assert IC.scan_lds(["\tds_read_b32 v4, v0", "\ts_load_dword s4, s[0:1], 0x0", "\ts_waitcnt lgkmcnt(1)",
+                        "\tv_add_f32_e32 v5, v4, v4"])
 
 
 @pytest.mark.timeout(600)

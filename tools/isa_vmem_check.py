@@ -74,12 +74,58 @@ def scan(body):
     return bad
 
 
+DS = re.compile(r"^ds_")
+SMEM = re.compile(r"^s_(load|buffer_load|memtime|memrealtime|getpc|dcache)")
+
+
+def scan_lds(body):
+    """The same scan for LDS reads and lgkmcnt: ds_* ops count in lgkmcnt in issue order and
+    return in order; a ds_read (or ds_bpermute / ds_swizzle / a returning ds atomic)
+    destination stays pending until an lgkmcnt(N) leaves at most N younger ops.  Scalar
+    memory ops also count in lgkmcnt but may return out of order: while one is outstanding
+    only lgkmcnt(0) retires anything."""
+    out, bad = [], []  # (dest regs, is_smem)
+    for i, ln in enumerate(body):
+        s = ln.split(";")[0].strip()
+        if s.startswith(".LBB") and s.endswith(":"):
+            out = []
+            continue
+        if not s or s.startswith(".") or s.endswith(":"):
+            continue
+        op = s.split()[0]
+        if op == "s_waitcnt":
+            m = re.search(r"lgkmcnt\((\d+)\)", s)
+            if m:
+                n = int(m.group(1))
+                if n == 0:
+                    out = []
+                elif not any(sm for _, sm in out):
+                    while len(out) > n:
+                        out.pop(0)
+            continue
+        pending = set().union(*[d for d, _ in out]) if out else set()
+        used = regs(s)
+        dest = set()
+        is_ds = bool(DS.match(op))
+        returns = is_ds and ("read" in op or "bpermute" in op or "swizzle" in op or "rtn" in op)
+        if returns:
+            dest = regs(s[len(op):].split(",")[0])
+            used -= dest
+        if pending & used:
+            bad.append((i, s, sorted(pending & used)[:4]))
+        if is_ds:
+            out.append((dest, False))
+        elif SMEM.match(op):
+            out.append((set(), True))
+    return bad
+
+
 def main():
     lines = open(sys.argv[1]).read().splitlines()
     pats = sys.argv[2:] or ["rmb_"]
     total = 0
     for name, body in kernels(lines, pats):
-        bad = scan(body)
+        bad = scan(body) + scan_lds(body)
         total += len(bad)
         print(f"{name}: {len(body)} lines, {len(bad)} early uses of in-flight load destinations")
         for i, s, r in bad[:10]:
