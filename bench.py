@@ -207,10 +207,7 @@ class Pipeline:
         # so the encoder stream runs GEMMs only (TRK_ROI_STREAM, default 1 since r03: with
         # NCHW maps and the 75-us sweep, 1.674-1.694 vs 1.641-1.682M ROIs/s in three
         # interleaved pairs; +0.7..2 % with r02's kernels)
-        # TRK_ROI_PRIO=1: the ROI stream at the tracker's high priority (frame f+1's sweep then
-        # takes the CUs frame f's transition releases before that transition's next workgroups)
-        self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device,
-                                             priority=-1 if os.environ.get("TRK_ROI_PRIO", "0") == "1" else 0)
+        self.roi_stream = (torch.cuda.Stream(device=sc["feat"].device)
                            if os.environ.get("TRK_ROI_STREAM", "1") == "1" else None)
         self.roi_pending = {}
         # TRK_ROI_AFTER=g1|dsc: frame f+1's ROI Align waits for frame f's first GEMM / DSC GEMM
