@@ -40,7 +40,7 @@ def apply(v, reset=False):
 for v in variants:  # the defaults to restore: every knob's first-listed value in variant 0, else 0
     for kv in filter(None, v.split(";")):
         k, x = kv.split("=")
-        defaults.setdefault(k, 0 if k != "enc_gemm" else 1)
+        defaults.setdefault(k, {"enc_trans": 1, "rf3_chunks": 1}.get(k, 0))
 ref = None
 for v in variants:
     apply(v)

@@ -1,6 +1,6 @@
 """trans4 phase cycles per workgroup (s_memtime stamps of wave 0, trk_enc_set_prof): K loop,
-SiLU, ROI sums (MFMA), sum stores, total; medians over the 3,200 tiles of the bench shape,
-per t4_mode.  usage: python tools/exp/t4_prof.py"""
+SiLU, ROI sums (MFMA), sum stores, total; medians over the 3,200 tiles of the bench shape.
+usage: python tools/exp/t4_prof.py"""
 import ctypes, importlib, json, os, sys
 import torch
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
@@ -17,16 +17,12 @@ L = ops.lib()
 L.trk_enc_set_prof.argtypes = [ctypes.c_void_p]
 nwg = (R * P + 127) // 128 * 2
 buf = torch.zeros(nwg * 8, dtype=torch.int64, device=dev)
-for mode in (0, 5):
-    L.trk_set_tuning(b"t4_mode", mode)
-    for _ in range(3):
-        ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
-    L.trk_enc_set_prof(ctypes.c_void_p(buf.data_ptr()))
+for _ in range(3):
     ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
-    torch.cuda.synchronize()
-    L.trk_enc_set_prof(None)
-    p = buf.view(nwg, 8)[:, :5].double().cpu()
-    med = p.median(0).values.tolist()
-    print(json.dumps({"t4_mode": mode, "k_loop": round(med[0]), "silu": round(med[1]), "sums": round(med[2]),
-                      "store": round(med[3]), "total": round(med[4])}), flush=True)
-L.trk_set_tuning(b"t4_mode", 5)
+L.trk_enc_set_prof(ctypes.c_void_p(buf.data_ptr()))
+ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+torch.cuda.synchronize()
+L.trk_enc_set_prof(None)
+med = buf.view(nwg, 8)[:, :5].double().cpu().median(0).values.tolist()
+print(json.dumps({"k_loop": round(med[0]), "silu": round(med[1]), "sums": round(med[2]), "store": round(med[3]),
+                  "total": round(med[4])}), flush=True)

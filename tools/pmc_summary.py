@@ -48,10 +48,9 @@ def main():
     print("JSON " + json.dumps(out))
     if len(sys.argv) > 3:  # short-name traffic table for bench.py (profiles/pmc_traffic.json)
         short_names = {"roi_sweep_kernel": "roi_align", "dwconv5_rows2_kernel": "dwconv5",
-                       "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost", "cost3_kernel": "cost", "det_prep_kernel": "cost_prep",
-                       "enc_gemm_kernel<0": "enc_gemm_dsc", "enc_gemm_kernel<1": "enc_gemm_trans",
-                       "enc_gemm_kernel<2": "enc_gemm_plain", "g1dw_kernel": "enc_g1_dwconv", "g1dw4_kernel": "enc_g1_dwconv", "rmb_front_kernel": "enc_rmb_front", "rmb_front2_kernel": "enc_rmb_front", "rmb_front3_kernel": "enc_rmb_front", "rmb_fused_kernel": "enc_rmb_fused", "trans4_kernel": "enc_gemm_trans", "gemm4w_trans_kernel": "enc_gemm_trans",
-                       "g1dw_il_kernel": "enc_g1_dwconv", "g1dw_persist_kernel": "enc_g1_dwconv",
+                       "dwconv5_nhwc_kernel": "dwconv5_generic", "cost_kernel": "cost", "cost3_kernel": "cost",
+                       "det_prep_kernel": "cost_prep", "g1dw4_kernel": "enc_g1_dwconv",
+                       "rmb_front3_kernel": "enc_rmb_front", "trans4_kernel": "enc_gemm_trans",
                        "gemm4_kernel<0": "enc_gemm_dsc", "gemm4_kernel<1": "enc_gemm_trans",
                        "enc_se_kernel": "enc_se", "enc_head_kernel": "enc_head", "det_nms_kernel": "det_nms",
                        "lsap_kernel": "lsap", "act_mean_kernel": "act_mean", "scale_rows_kernel": "scale_rows",

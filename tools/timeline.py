@@ -1,5 +1,5 @@
 """Per-step GPU timeline from a rocprofv3 kernel trace (run_kernel_trace.csv):
-splits the trace at each g1dw_kernel launch (one per frame) and prints, for
+splits the trace at each rmb_front3_kernel launch (one per frame) and prints, for
 the steps named, every kernel's stream, start offset and duration, plus the
 busy fraction of the step (union of kernel intervals).
 usage: python tools/timeline.py TRACE.csv [first_step] [n_steps]"""
@@ -15,8 +15,8 @@ def short(n):
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 k0 = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 nk = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-marks = [i for i, r in enumerate(rows) if "g1dw" in r["Kernel_Name"]]
-print(f"{len(rows)} kernels, {len(marks)} g1dw launches")
+marks = [i for i, r in enumerate(rows) if "rmb_front3_kernel" in r["Kernel_Name"]]
+print(f"{len(rows)} kernels, {len(marks)} front launches")
 for s in range(k0, min(k0 + nk, len(marks) - 1)):
     a, b = marks[s], marks[s + 1]
     t0 = int(rows[a]["Start_Timestamp"]); t1 = int(rows[b]["Start_Timestamp"])
