@@ -18,7 +18,7 @@ L = trk.lib()
 variants = sys.argv[1:] or ["roi_wlds=0", "roi_wlds=1"]
 
 
-DEFAULTS = {"roi_wlds": 1, "roi_sweep": 1, "roi_fma": 1, "roi_asm": 1, "roi_pf": 0}
+DEFAULTS = {"roi_wlds": 1, "roi_sweep": 1, "roi_fma": 1, "roi_asm": 1}
 
 
 def setv(v, reset=False):
