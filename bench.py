@@ -199,10 +199,14 @@ class Pipeline:
         # they dispatch as soon as CUs free up beside the encoder's full-GPU grids
         prio = int(os.environ.get("TRK_TRACK_PRIO", "1"))
         self.track_stream = torch.cuda.Stream(device=sc["feat"].device, priority=-1) if prio else None
-        # the encoder's last kernel (projection head, 128 latency-bound workgroups) launched
-        # on the tracker's stream right before the frame's tracker step, so the next frame's
-        # ROI Align and first GEMM (embedding stream) fill the GPU beside it; no extra stream
-        self.defer_head = os.environ.get("TRK_HEAD_STREAM", "1") == "1" and self.track_stream is not None
+        # TRK_HEAD_STREAM=1: the encoder's last kernel (projection head, 128 latency-bound
+        # workgroups) launched on the tracker's stream right before the frame's tracker step (the
+        # default in r02-r04, with one embedding stream).  Default 0 since r05: with the two
+        # overlapping embedding streams the head stays on its frame's embedding stream behind the
+        # transition, and the tracker stream carries only the tracker step (its live sum ≈ 0.63
+        # vs 0.85 ms per step); pipeline 2.021-2.091 vs 2.008-2.090M ROIs/s, six of seven
+        # interleaved pairs ahead (r5o, r5q)
+        self.defer_head = os.environ.get("TRK_HEAD_STREAM", "0") == "1" and self.track_stream is not None
         # ROI Align of frame f+1 issued on its own stream when frame f's encoder is enqueued,
         # so the encoder stream runs GEMMs only (TRK_ROI_STREAM, default 1 since r03: with
         # NCHW maps and the 75-us sweep, 1.674-1.694 vs 1.641-1.682M ROIs/s in three
