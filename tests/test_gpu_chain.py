@@ -108,6 +108,35 @@ def test_c3_bf16_encoder_full_size_vs_fp32(trk, gpu):
     assert hit >= 0.98, hit
 
 
+@pytest.mark.parametrize("F,N", [(1, 16), (8, 256)])
+def test_s7_bf16_encoder_vs_fp32(trk, gpu, F, N):
+    """The reference's own call site pools 7x7 ROIs (tracking.py:304-309): the bf16 encoder at
+    S = 7 (49 rows per ROI: the first 1x1 convs on hipBLASLt, the depthwise kernel, gemm4's DSC
+    and transition GEMMs with 128-row tiles spanning up to four ROIs, SE, head) against the fp32
+    path on the same ROI Align output, c1's single frame of 16 ROIs and c3's 8 x 256.
+    Tolerances as the 10x10 test's (about 2x the measured error, printed; measured r05: max |d|
+    6.63e-4 / 8.50e-4, min cosine 1 - 3.6e-6 / 1 - 5.3e-6 for 1 x 16 / 8 x 256); deterministic."""
+    rng = np.random.default_rng(700 + N)
+    feat = torch.from_numpy(G.silu_np(rng.standard_normal((F, 512, 40, 40)).astype(np.float32))
+                            .astype(np.float32)).to(gpu)
+    boxes = np.stack([_boxes(rng, N) for _ in range(F)])
+    rois = np.concatenate([np.repeat(np.arange(F), N).astype(np.float32)[:, None], boxes.reshape(-1, 4)], 1)
+    r = torch.from_numpy(rois).to(gpu)
+    model, _ = _model(trk, gpu)
+    with torch.no_grad():
+        z32 = model(trk.roi_align(feat, r, (7, 7), 40 / 1280.0, 2, True))
+        roib = trk.roi_align(feat, r, (7, 7), 40 / 1280.0, 2, True, out_dtype=torch.bfloat16, channels_last=True)
+        zb = model(roib)
+        zb2 = model(roib)
+    assert zb.shape == (F * N, 128) and torch.isfinite(zb).all()
+    assert torch.equal(zb, zb2)
+    cos = (zb * z32).sum(1)
+    print(f"\nS=7 bf16 vs fp32 encoder ({F} x {N}): max |d| {(zb - z32).abs().max().item():.3e}, "
+          f"min cosine {cos.min().item():.7f}")
+    assert (zb - z32).abs().max().item() <= 2e-3
+    assert cos.min().item() >= 1.0 - 1e-5, cos.min().item()
+
+
 def test_c2_chain_fp32_vs_oracle(trk, oracle, gpu):
     rng = np.random.default_rng(64)
     N = 64
