@@ -915,6 +915,10 @@ def main():
                           "region, on the stream it is launched on (the same launches tools/kernel_stats.py "
                           "takes from a rocprofv3 trace: its timed window)" if dom in live else
                           "isolated: back-to-back launches after the timed region"),
+          "time_note": ("with the two overlapping embedding streams a front's live window starts while the "
+                        "previous frame's transition still holds CUs; 'serialised' is the kernel alone (a "
+                        "counter pass runs each dispatch by itself), 'isolated' back to back (power-limited "
+                        "clock), DESIGN.md section 6") if pipe.overlap else None,
           "isolated_time_us": None if t_iso is None else round(t_iso, 2),
           "isolated_frac": None if t_iso is None else round(per[dom]["work"] / (t_iso * 1e-6) /
                                                             (per[dom]["peak"] * (1e12 if per[dom]["unit"] == "TFLOP/s"
