@@ -1152,6 +1152,18 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
                "+v"(wreg[11]), "+v"(wreg[12])::"memory");
   asm volatile("" : "+v"(wreg[13]), "+v"(wreg[14]), "+v"(wreg[15]), "+v"(wreg[16]), "+v"(wreg[17]), "+v"(wreg[18]),
                "+v"(wreg[19]), "+v"(wreg[20]), "+v"(wreg[21]), "+v"(wreg[22]), "+v"(wreg[23]), "+v"(wreg[24]));
+  // L2 prefetch of the workgroup's next ROI's X: one dword of every 128-B line (100 KB, 800
+  // lines: 1-2 loads per thread) loaded now, ~40K cycles before that ROI's DMA, so the DMA finds
+  // it in L2 (per ROI 60.6K vs 65.1K cycles, GEMM1 13.4K vs 18.4K; pipeline 2.077-2.089 vs
+  // 2.050-2.065M ROIs/s in three interleaved pairs).  Younger than GEMM2's first weight loads,
+  // so GEMM2's counted waits only get stricter; the destinations stay live until GEMM2's last
+  // wait retires them
+  uint32_t xpf0 = 0, xpf1 = 0;
+  if (roi + stride < roi_end) {
+    const uint16_t* nx = a.X + (roi + stride) * RF_S * 512;
+    asm volatile("global_load_dword %0, %1, off" : "+v"(xpf0) : "v"(nx + tid * 64) : "memory");
+    if (tid < 800 - 512) asm volatile("global_load_dword %0, %1, off" : "+v"(xpf1) : "v"(nx + (tid + 512) * 64) : "memory");
+  }
 
   // ---- depthwise 5x5 in place: waves 2 cg and 2 cg + 1 own the two output halves of the
   // same 128 channels, so the read-before-overwrite hand-off is between those two only
@@ -1201,6 +1213,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     rf_mfma_step(y_a + rf2_yblk(kt) * RF_KBS * 4, b, acc);
   }
   __builtin_amdgcn_s_setprio(0);
+  asm volatile("" ::"v"(xpf0), "v"(xpf1));  // (retired by GEMM2's last wait)
   rf2_signal(ctr + RF2_CG2 + half, lane);  // this wave's reads of the Y image are done
   if (prof) {
     asm volatile("" ::"v"(acc[6][3][3]));
@@ -1267,9 +1280,9 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pst[7] = eg_stamp();
     if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
-      unsigned long long* o = a.prof + ((roi * 2 + G) * 8 + wave) * 8;  // [ROI][group][wave][8]
+      unsigned long long* o = a.prof + ((roi * 2 + G) * 8 + wave) * 8;  // [ROI][group][wave]: 7 phases, start
       for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
-      o[7] = pst[7] - pst[0];
+      o[7] = pst[0];  // the ROI's absolute start (s_memtime): phase timelines across waves and ROIs
     }
   }
   }  // ROI loop

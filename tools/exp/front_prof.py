@@ -65,7 +65,8 @@ for v in variants:
     ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
     torch.cuda.synchronize()
     L.trk_enc_set_prof(None)
-    p = buf.view(R, 2, 8, 8).double().cpu()   # [roi][group][wave][phase]
+    p = buf.view(R, 2, 8, 8).double().cpu()   # [roi][group][wave][7 phases + absolute start]
+    p[..., 7] = p[..., :7].sum(-1)             # total
     apply(v, reset=True)
     ts = times[v]
     print(json.dumps({"variant": v, "xrn_equal_first": same, "us": round(statistics.median(ts), 1),
