@@ -1016,7 +1016,11 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   const int tid = tid_o, lane = tid & 63;
   const int fr = lane & 15, fc = lane >> 4;
   unsigned long long pst[8];
-  if (prof) pst[0] = eg_stamp();
+  unsigned long long rt0 = 0;
+  if (prof) {
+    pst[0] = eg_stamp();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   const int64_t r0 = roi * RF_S;
 
   // X -> blocks 0..15, moved by half A only (2 DMA ops per block per wave: pieces
@@ -1266,13 +1270,22 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   rf2_wait(ctr + RF2_CST + half, t4);
   if (prof) pst[6] = eg_stamp();
   {
-    uint16_t* dst = a.XRN + r0 * 1024 + G * 512 + half * 256;
+    // XRN rows through a buffer store with sc1: the line leaves the XCD's L2 with the write
+    // (plain stores kept ~2.8 MB of XRN per ROI round in the 4 MB L2, evicting the weight
+    // fragments the 28 workgroups re-read every ROI: front FETCH 413 vs 634 MB per launch)
+    const uint64_t da = (uint64_t)(a.XRN + r0 * 1024 + G * 512 + half * 256);
+    const uint32_t da_lo = __builtin_amdgcn_readfirstlane((uint32_t)da);
+    const uint32_t da_hi = __builtin_amdgcn_readfirstlane((uint32_t)(da >> 32));
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)da_hi << 32) | da_lo), 0, RF_S * 2048, 0x00020000);
     const int ht = tid & 255;
-#pragma unroll 4
-    for (int q = ht; q < RF_S * 32; q += 256) {
+#pragma unroll
+    for (int j = 0; j < (RF_S * 32 + 255) / 256; ++j) {
+      const int q = ht + 256 * j;
+      if (q >= RF_S * 32) break;
       const int row = q >> 5, c = q & 31;
-      *reinterpret_cast<uint4*>(dst + (int64_t)row * 1024 + c * 8) =
-          *reinterpret_cast<const uint4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(stg + row * RF2_SROW + ((c ^ (row & 15)) << 2));
+      __builtin_amdgcn_raw_buffer_store_b128(v, drs, (row * 1024 + c * 8) * 2, 0, 16 /* sc1 */);
     }
   }
   rf2_signal(ctr + RF2_CSD + half, lane);  // this wave's staging reads are done (the next ROI may write)
@@ -1282,7 +1295,11 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     if (lane == 0) {  // every wave's phases: [workgroup][wave][8]
       unsigned long long* o = a.prof + ((roi * 2 + G) * 8 + wave) * 8;  // [ROI][group][wave]: 7 phases, start
       for (int q = 0; q < 7; ++q) o[q] = pst[q + 1] - pst[q];
-      o[7] = pst[0];  // the ROI's absolute start (s_memtime): phase timelines across waves and ROIs
+      // the ROI's start on the 100 MHz clock every CU shares (s_memtime counters are not
+      // comparable across CUs), with the XCD's id in bits 56..59: pair lag and placement
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      o[7] = rt0 | ((unsigned long long)xcc << 56);
     }
   }
   }  // ROI loop

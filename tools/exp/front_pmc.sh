@@ -1,23 +1,26 @@
 #!/bin/bash
-# rmb_front HBM traffic (FETCH_SIZE / WRITE_SIZE passes) per TRK_TUNE variant, isolated launches
-set -u
-ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$ROOT/gpurun_out/front_pmc; mkdir -p "$OUT"; cd /tmp; export TMPDIR=/tmp
-i=0
-for v in "$@"; do
-  i=$((i+1))
-  for PM in FETCH_SIZE WRITE_SIZE; do
-    TRK_TUNE="$v" timeout -k 10 120 rocprofv3 --pmc $PM --kernel-trace -d "$OUT/v${i}_$PM" -o run --output-format csv \
-      -- python3 "$ROOT/tools/exp/front_run.py" > "$OUT/v${i}_$PM.log" 2>&1 || { echo "variant $v $PM failed"; exit 1; }
-  done
-  python3 - "$OUT" "$i" "$v" <<'PY'
-import csv, glob, sys
-out, i, v = sys.argv[1], sys.argv[2], sys.argv[3]
-res = {}
-for pm in ("FETCH_SIZE", "WRITE_SIZE"):
-    f = glob.glob(f"{out}/v{i}_{pm}/**/*counter_collection.csv", recursive=True)
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f[0])) if "rmb_front" in r["Kernel_Name"]]
-    res[pm] = sum(vals) / max(len(vals), 1)
-print(v or "default", "launches", len(vals), "read MB (2x FETCH KiB)", round(2 * res["FETCH_SIZE"] * 1024 / 1e6, 1),
-      "write MB", round(res["WRITE_SIZE"] * 1024 / 1e6, 1))
+# rmb_front3 per library build or environment (isolated launches): phase cycles (front_prof.py)
+# and one L2 counter pass (fabric read requests, L2 hits / misses; RDREQ x 128 B = bytes read
+# from beyond L2).  usage: front_pmc.sh TAG "ENV_A" ["ENV_B" ...]  (each ENV a space-separated
+# VAR=value list, e.g. TRK_LIB_PATH=...; may be empty)
+set -o pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p "$ROOT/gpurun_out"
+TAG=$1; shift
+k=0
+for E in "$@"; do
+  k=$((k+1))
+  env $E timeout -k 10 120 python tools/exp/front_prof.py "" > "gpurun_out/${TAG}_prof_$k.txt" 2>&1 || { echo "prof $k failed"; exit 1; }
+  echo "== $k [$E]"; grep '"variant"' "gpurun_out/${TAG}_prof_$k.txt" | cut -c1-330
+  (cd /tmp && export TMPDIR=/tmp && env $E timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum --kernel-trace \
+    -d "$ROOT/gpurun_out/${TAG}_pmc_$k" -o run --output-format csv -- python3 "$ROOT/tools/exp/front_timeline.py" 1 \
+    > "$ROOT/gpurun_out/${TAG}_pmc_$k.log" 2>&1) || { echo "pmc $k failed"; exit 1; }
+  python3 - "$ROOT/gpurun_out/${TAG}_pmc_$k" <<'PY'
+import csv, glob, sys, collections
+res = collections.defaultdict(list)
+f = glob.glob(f"{sys.argv[1]}/**/*counter_collection.csv", recursive=True)
+for r in csv.DictReader(open(f[0])):
+    if "rmb_front3" in r["Kernel_Name"]:
+        res[r["Counter_Name"]].append(float(r["Counter_Value"]))
+print({k: round(sum(v) / len(v) / 1e6, 3) for k, v in res.items()}, "(millions per launch)")
 PY
 done
