@@ -133,6 +133,10 @@ def _declare(L):
     L.trk_lsap_set_prof.restype = i32
     L.trk_enc_set_prof.argtypes = [P]
     L.trk_enc_set_prof.restype = i32
+    L.trk_enc_set_progress.argtypes = [P]
+    L.trk_enc_set_progress.restype = i32
+    L.trk_stream_gate.argtypes = [P, ctypes.c_uint32, i64, P]
+    L.trk_stream_gate.restype = i32
     L.trk_cost_set_prof.argtypes = [P]
     L.trk_cost_set_prof.restype = i32
     L.trk_head_set_prof.argtypes = [P]

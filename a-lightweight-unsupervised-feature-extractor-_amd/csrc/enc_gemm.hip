@@ -20,6 +20,7 @@
 #include <utility>
 
 unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: per-workgroup phase stamps)
+uint32_t* g_rf_progress = nullptr;          // trk_enc_set_progress: rmb_front3's finished-ROI counter
 int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rmb_front3 workgroup pairs per XCD (0 = CUs / 16 - 2)
 int g_rf3_chunks = 1;  // trk_set_tuning("rf3_chunks"): rmb_front3 generations (each pair's ROIs in that many
                        // chunks, one workgroup each; 1 = one persistent generation)
@@ -768,6 +769,7 @@ struct RfArgs {
   int64_t R;            // ROIs
   int pairs, chunks;    // rmb_front3's grid: workgroup pairs per XCD, generations (ROI chunks)
   unsigned long long* prof;  // trk_enc_set_prof: every wave's phase cycles per ROI (diagnostics)
+  uint32_t* progress;        // trk_enc_set_progress: +1 per finished ROI (group 0's workgroup), or null
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
@@ -1289,6 +1291,10 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     }
   }
   rf2_signal(ctr + RF2_CSD + half, lane);  // this wave's staging reads are done (the next ROI may write)
+  // the ROI's progress count (trk_enc_set_progress): one relaxed device-scope add per ROI, so a
+  // trk_stream_gate on another stream can start its work while this front is in its last round
+  if (G == 0 && threadIdx.x == 0 && a.progress)
+    __hip_atomic_fetch_add(a.progress, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (prof) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pst[7] = eg_stamp();
@@ -1776,6 +1782,7 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   a.m_n = m_n;
   a.R = M / RF_S;
   a.prof = g_enc_prof;
+  a.progress = g_rf_progress;
   // persistent: 16 workgroups per 8 ROIs up to one per CU (a multiple of 16, so both groups of a
   // ROI share an XCD); rf3_groups 0 = two CUs per XCD left free -- the tracker's and the ROI
   // stream's kernels start there instead of waiting for a persistent workgroup to end
@@ -1797,4 +1804,33 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
 extern "C" int trk_enc_set_prof(unsigned long long* buf) {
   g_enc_prof = buf;
   return TRK_OK;
+}
+
+// rmb_front3's finished-ROI counter (one u32 the caller owns, counting on across launches); NULL = off
+extern "C" int trk_enc_set_progress(uint32_t* counter) {
+  g_rf_progress = counter;
+  return TRK_OK;
+}
+
+namespace {
+// one wave: wait until *counter >= target (relaxed device-scope loads, s_sleep between polls) or
+// until max_ticks of the 100 MHz clock have passed, then end: the kernels queued behind it on
+// its stream start then.  A performance gate only: it never blocks longer than its bound
+__global__ void __launch_bounds__(64) stream_gate_kernel(const uint32_t* counter, uint32_t target,
+                                                         unsigned long long max_ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t v = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(16);
+  }
+}
+}  // namespace
+
+extern "C" int trk_stream_gate(const uint32_t* counter, uint32_t target, int64_t max_us, void* stream) {
+  TRK_REQUIRE(counter && max_us >= 0 && max_us <= 1000000, "stream_gate: null counter or max_us outside 0..1e6");
+  hipLaunchKernelGGL(stream_gate_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), counter,
+                     target, (unsigned long long)max_us * 100);
+  return trk::check_launch("stream_gate_kernel");
 }

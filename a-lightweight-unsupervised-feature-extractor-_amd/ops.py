@@ -254,6 +254,28 @@ def enc_rmb_front_means(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W
     return XRN, m[0], m[1]
 
 
+def enc_set_progress(counter: Optional[torch.Tensor]) -> None:
+    """Later enc_rmb_front_means launches add 1 per finished ROI to counter (a one-element
+    int32 device tensor the caller keeps alive and zeroes; the count runs on across
+    launches); None switches it off (trk_enc_set_progress)."""
+    if counter is not None:
+        _need_gpu(counter, "enc_set_progress")
+        if counter.dtype != torch.int32 or counter.numel() < 1:
+            raise TypeError("enc_set_progress: a one-element int32 device tensor required")
+    check(lib().trk_enc_set_progress(_ptr(counter)), "enc_set_progress")
+
+
+def stream_gate(counter: torch.Tensor, target: int, max_us: int = 2000) -> None:
+    """Enqueue on the current stream a one-wave kernel that returns once counter[0] >= target
+    (an enc_set_progress counter another stream's front advances) or after max_us: the work
+    queued behind it starts then (trk_stream_gate; a scheduling hint, not an ordering)."""
+    _need_gpu(counter, "stream_gate")
+    if counter.dtype != torch.int32:
+        raise TypeError("stream_gate: int32 counter required")
+    check(lib().trk_stream_gate(_ptr(counter), ctypes.c_uint32(int(target) & 0xFFFFFFFF), int(max_us),
+                                _stream(counter.device)), "stream_gate")
+
+
 def enc_se_means(m_r: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor):
     """SE excitation from given squeeze means (trk_enc_se_means): s [R, C] f32, bit-identical
     to enc_se's s for the same m_r (card.py:59-78)."""

@@ -167,6 +167,9 @@ def frame_map(sc, f):
     return sc["feat"][f % sc["feat"].shape[0]]
 
 
+_PROGRESS = {}  # device index -> the fronts' finished-ROI counter (trk_enc_set_progress)
+
+
 class Pipeline:
     """The per-frame hot path over a batch of streams.
 
@@ -224,6 +227,24 @@ class Pipeline:
         # rmb_front live 657 vs 741 us)
         self.roi_after = os.environ.get("TRK_ROI_AFTER", "dsc") if self.roi_stream is not None else ""
         self.roi_gate = None
+        # TRK_ROI_GATE_FRAC < 1: instead of frame f's whole front, frame f+1's ROI stage waits
+        # (trk_stream_gate, bounded) until the front has finished that fraction of its ROIs, so it
+        # starts on the CUs the persistent front's last, partly filled round leaves idle (the front
+        # counts finished ROIs into a device counter, trk_enc_set_progress)
+        # Default 0.93 since r05: 2.030-2.053 vs 1.968-2.043M ROIs/s, six of seven interleaved
+        # pairs ahead, +1.1 % in the means (r5l, r5l2); 0.88 / 0.91 / 0.95 / 0.97 within or below
+        self.gate_frac = float(os.environ.get("TRK_ROI_GATE_FRAC", "0.93"))
+        self.progress = None
+        self.fronts_rois = 0       # the count the counter reaches once every enqueued front is done
+        self.roi_gate_target = None
+        if self.roi_after == "dsc" and self.gate_frac < 1:
+            dev = sc["feat"].device
+            # one counter per device for the process: the library keeps its pointer, so it must
+            # never be freed under a later launch
+            self.progress = _PROGRESS.setdefault(dev.index, torch.zeros(1, dtype=torch.int32, device=dev))
+            torch.cuda.synchronize()
+            self.fronts_rois = int(self.progress.item()) & 0xFFFFFFFF
+            trk.ops.enc_set_progress(self.progress)
         # TRK_EMBED_OVERLAP=1 (with TRK_EMBED_STREAMS=2, both the default since r05): frame f+1's
         # encoder, on the other embedding stream, waits only for frame f's front (not its SE and
         # transition), so the next front's workgroups fill the CUs the transition's last round
@@ -233,7 +254,11 @@ class Pipeline:
         self.front_ev = None
         if self.roi_after or self.overlap:
             def hook(name):
-                if name == self.roi_after:
+                if name == "dsc" and self.progress is not None:
+                    r = self.sc["streams"] * self.sc["N"]
+                    self.roi_gate_target = (self.fronts_rois + int(self.gate_frac * r)) & 0xFFFFFFFF
+                    self.fronts_rois = (self.fronts_rois + r) & 0xFFFFFFFF
+                elif name == self.roi_after:
                     self.roi_gate = torch.cuda.Event()
                     self.roi_gate.record(torch.cuda.current_stream())
                 if self.overlap and name == "dsc":
@@ -247,6 +272,14 @@ class Pipeline:
         self.map_ahead = (MAP_LAYOUT == "nchw" and self.track_stream is not None and
                           os.environ.get("TRK_MAP_AHEAD", "0") == "1")
         self.map_pending = {}
+
+    def close_progress(self):
+        """stop the fronts' progress counting (the isolated kernel pass launches fronts the
+        pipeline's targets do not know of)"""
+        if self.progress is not None:
+            torch.cuda.synchronize()
+            trk.ops.enc_set_progress(None)
+            self.progress = None
 
     def _map_ahead(self, f):
         if not self.map_ahead or f in self.map_pending or f >= len(self.sc["rois"]):
@@ -342,6 +375,9 @@ class Pipeline:
         if self.roi_stream is None or f in self.roi_pending or f >= len(self.sc["rois"]):
             return
         with torch.cuda.stream(self.roi_stream):
+            if self.roi_gate_target is not None:
+                trk.ops.stream_gate(self.progress, self.roi_gate_target, 2000)
+                self.roi_gate_target = None
             if self.roi_gate is not None:
                 self.roi_stream.wait_event(self.roi_gate)
                 self.roi_gate = None
@@ -823,6 +859,7 @@ def main():
     value = rois_total / el
     ident = float(np.mean([pipe.check_identity(PREROLL + args.warmup + k, r) for k, r in enumerate(results)]))
 
+    pipe.close_progress()
     prof_mark()
     iso, M, iso_info = kernel_pass(pipe, f - 1)
     prof_mark()
@@ -973,6 +1010,7 @@ def main():
                  if os.environ.get(k) is not None}
     rf["streams"] = {"embed": len(pipe.sides), "embed_overlap": pipe.overlap, "head_on_track_stream": pipe.defer_head,
                      "roi_stream": pipe.roi_stream is not None, "roi_after": pipe.roi_after or None,
+                     "roi_gate_frac": pipe.gate_frac if pipe.gate_frac < 1 else None,
                      "track_prio": pipe.track_stream is not None,
                      "prefetch_depth": pipe.depth, "graphs": pipe.graphs is not None,
                      "tuning": os.environ.get("TRK_TUNE") or None}

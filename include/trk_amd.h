@@ -171,6 +171,15 @@ int trk_lsap_set_prof(unsigned long long* buf);
 /* diagnostics: per-workgroup (gemm4, trans4: 8 u64 each) or per-wave (rmb_front3: [ROI][group]
  * [wave][8] u64) phase timestamps of the encoder GEMMs; NULL = off */
 int trk_enc_set_prof(unsigned long long* buf);
+/* Progress of the persistent encoder front (trk_enc_rmb_front_means): later launches add 1 to
+ * *counter (one u32 in device memory the caller owns and zeroes) for every ROI they finish, so
+ * the count runs on across launches; NULL = off.  trk_stream_gate enqueues on `stream` a
+ * one-wave kernel that returns once *counter >= target, or after max_us microseconds (0..1e6)
+ * whatever the count: work queued behind it on that stream starts when a front on another
+ * stream has finished `target` ROIs.  A scheduling hint only (the bound makes it one); order
+ * that correctness needs still takes events. */
+int trk_enc_set_progress(uint32_t* counter);
+int trk_stream_gate(const uint32_t* counter, uint32_t target, int64_t max_us, void* stream);
 /* diagnostics: per-wave timestamps of the bank-resident cost kernel; NULL = off */
 int trk_cost_set_prof(unsigned long long* buf);
 /* diagnostics: per-wave phase timestamps of enc_head; NULL = off */

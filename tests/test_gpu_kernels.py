@@ -801,6 +801,49 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups, chunks):
         ops.enc_rmb_front_means(X, W1p, wdw, W2.reshape(1024, 512), b2)
 
 
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_enc_front_progress_and_stream_gate(trk, gpu, chunks):
+    """trk_enc_set_progress: every rmb_front3 launch adds one per finished ROI (R = 37 and 300,
+    the persistent grid and 4 generations) to the caller's counter and leaves the results
+    unchanged; NULL stops the count.  trk_stream_gate: returns at once once the count is
+    reached, after its bound otherwise, and the work queued behind it then runs."""
+    import time
+    ops, X, W1, wdw, W2, b2, se = _front_operands(gpu, 300, 300)
+    L = trk.lib()
+    W1p, W2p = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2)
+    ref = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    assert L.trk_set_tuning(b"rf3_chunks", chunks) == 0
+    try:
+        ops.enc_set_progress(cnt)
+        out = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        ops.enc_rmb_front_means(X[: 37 * 100], W1p, wdw, W2p, b2)
+        torch.cuda.synchronize()
+        assert cnt.item() == 337
+        ops.enc_set_progress(None)
+        ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
+        torch.cuda.synchronize()
+        assert cnt.item() == 337
+    finally:
+        ops.enc_set_progress(None)
+        L.trk_set_tuning(b"rf3_chunks", 1)
+    assert all(torch.equal(a, b) for a, b in zip(out, ref))
+    side = torch.cuda.Stream(device=gpu)
+    for target, bound_us, slow in ((300, 500000, False), (338, 20000, True)):
+        flag = torch.zeros(1, dtype=torch.int32, device=gpu)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(side):
+            ops.stream_gate(cnt, target, bound_us)
+            flag.fill_(1)  # queued behind the gate
+        side.synchronize()
+        dt = time.perf_counter() - t0
+        assert flag.item() == 1
+        assert (dt >= 0.015) if slow else (dt < 0.25), (target, dt)
+    with pytest.raises(Exception):
+        ops.stream_gate(cnt, 1, 2_000_000)  # the bound is capped at 1 s
+
+
 def _partials(total, P, parts=3):
     """split int64 per-ROI totals [R, ld] into the GEMMs' partial layout
     [R, parts, ld] (one entry per 128-row tile covering the ROI; the rest junk)"""
