@@ -10,6 +10,7 @@ compiles the file for gfx950 and scans each rmb kernel's straight-line regions
 CPU only (hipcc cross-compiles); skipped without hipcc.
 """
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -68,3 +69,10 @@ def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
         bad = IC.scan(body)
         assert not bad, (name, bad[:5])
     assert found == 2  # rmb_front3 + trans4
+    # no VGPR spills in the two register-bound kernels: a spilling front variant (256 VGPRs,
+    # 14 spilled to scratch) faulted with an illegal address in one of three pipeline runs
+    text = "\n".join(lines)
+    for k in ("rmb_front3_kernel", "trans4_kernel"):
+        meta = [m for m in re.finditer(r"\.name:\s+\S*" + k + r"\S*(.*?)\.vgpr_spill_count:\s+(\d+)", text, re.S)]
+        assert meta, k
+        assert all(int(m.group(2)) == 0 for m in meta), (k, [m.group(2) for m in meta])
