@@ -14,7 +14,7 @@ for i in $(seq 1 "$N"); do
     python3 -c "
 import json,sys
 d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; k=r['kernel_us']
-print(sys.argv[2], d['value'], d['ms_per_step'], 'front', k.get('enc_rmb_front'), 'trans', k.get('enc_gemm_trans'), 'roi', k.get('roi_stage'), 'iso_front', r['isolated_us'].get('enc_rmb_front'))" \
+print(sys.argv[2], d['value'], d['ms_per_step'], 'front', k.get('enc_rmb_front'), 'trans', k.get('enc_gemm_trans'), 'roi', k.get('roi_stage'), 'iso_front', r['isolated_us'].get('enc_rmb_front'), 'iso_trans', r['isolated_us'].get('enc_gemm_trans'))" \
       "gpurun_out/${TAG}_${k}_${i}.json" "$k/$i[$E]"
   done
 done
