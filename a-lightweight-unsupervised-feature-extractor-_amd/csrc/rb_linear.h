@@ -4,7 +4,10 @@
 // the same bits for the same rows.
 //
 // The 16 ROI rows are the A operand (from LDS), each wave owns column tiles of 16 outputs
-// whose weight rows it streams from L2.  Within each 16-wide K block, lane group
+// whose weight rows it streams from L2, pre-packed on the host in fragment order
+// (ops.enc_pack_rows: [N/16][K/16][64 lanes][4], lane = 16 g + r holding W[16 t + r][16 kb + 4 g
+// .. + 3]), so each load instruction reads 1 KiB contiguous instead of 16 rows' 64-B pieces
+// (enc_head 37.1 vs 46.9 us, enc_se 22.3 vs 26.2 us; the same values in the same order).  Within each 16-wide K block, lane group
 // g = lane >> 4 takes k = 4g + t at MFMA t (t = 0..3) for BOTH operands, so every lane
 // reads 16 contiguous bytes of its A row and of its weight row (the sum's order is
 // permuted, not its terms).
@@ -45,7 +48,8 @@ __device__ __forceinline__ void rb_load(const float* xp, int xq, const float* co
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) d.b[u][t] = *reinterpret_cast<const float4*>(wp[t] + kb0 + 16 * u);
+    for (int t = 0; t < NT; ++t)
+      d.b[u][t] = *reinterpret_cast<const float4*>(wp[t] + (kb0 / 16 + u) * 256);
   // A: chunk (kb / 4 + g) ^ (r & 15) of row r = the chunk group kb / 64 plus ((kb / 4) & 15) ^ xq
   // (kb / 4 is a multiple of 4 and g < 4, so kb / 4 + g = kb / 4 ^ g; xq = g ^ (r & 15))
 #pragma unroll
@@ -75,7 +79,8 @@ __device__ __forceinline__ void rb_gemm(const float* __restrict__ Xs, int ldx, c
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const float* wp[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) wp[t] = W + (int64_t)(n0 + 16 * t + r) * ldw + 4 * g;
+  for (int t = 0; t < NT; ++t)
+    wp[t] = W + ((int64_t)(n0 / 16 + t) * (ldw / 16) * 64 + lane) * 4;
   const float* xp = Xs + r * ldx;  // swizzled row (swz_at)
   const int xq = g ^ (r & 15);
   const int nch = K / KC;

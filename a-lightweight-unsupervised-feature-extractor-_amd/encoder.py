@@ -183,6 +183,9 @@ class Model(nn.Module):
                 f32(se[2].weight), f32(se[2].bias)
             w["h0"], w["ln_w"], w["ln_b"] = f32(hd[0].weight), f32(hd[1].weight), f32(hd[1].bias)
             w["h4"], w["h4b"] = f32(hd[4].weight), f32(hd[4].bias)
+            from .ops import enc_pack_rows  # the tail kernels' weight operands in fragment order
+            for k in ("se_w1", "se_w2", "h0", "h4"):
+                w[k + "_pk"] = enc_pack_rows(w[k])
         self._fused, self._fused_key = w, key
         return w
 
@@ -268,12 +271,12 @@ class Model(nn.Module):
                 # SE MLP (+ the squeeze means unless the front wrote them), then Shake2 mix +
                 # projection head: one kernel each
                 if front:
-                    s = enc_se_means(m_r, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+                    s = enc_se_means(m_r, W["se_w1_pk"], W["se_b1"], W["se_w2_pk"], W["se_b2"])
                 else:
-                    m_r, m_n, s = enc_se(sums, ss, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+                    m_r, m_n, s = enc_se(sums, ss, W["se_w1_pk"], W["se_b1"], W["se_w2_pk"], W["se_b2"])
                 tsums = enc_transition_gemm(XRN, ss, s, W["wt_nk"], W["bt_f"], raw=True, Wtp=W.get("wt_pk"))
-                head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0"], W["ln_w"], W["ln_b"],
-                                        self.head.net[1].eps, W["h4"], W["h4b"])
+                head = lambda: enc_head(tsums, ss, s, m_r, m_n, self._alpha(), W["h0_pk"], W["ln_w"], W["ln_b"],
+                                        self.head.net[1].eps, W["h4_pk"], W["h4b"])
                 if not self.defer_head:
                     return head()
                 # the head (128 latency-bound workgroups) is left to the caller, who launches

@@ -276,19 +276,39 @@ def stream_gate(counter: torch.Tensor, target: int, max_us: int = 2000) -> None:
                                 _stream(counter.device)), "stream_gate")
 
 
+def enc_pack_rows(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] f32 weight -> [N/16, K/16, 64, 4], the fragment order the SE / head kernels read
+    (rb_linear.h): lane 16 g + r of (column tile t, K block kb) holds W[16 t + r][16 kb + 4 g .. + 3]."""
+    if w.dim() != 2 or w.shape[0] % 16 or w.shape[1] % 16:
+        raise ValueError("enc_pack_rows: [N, K] with N, K multiples of 16 required")
+    N, K = w.shape
+    return (_f32c(w).reshape(N // 16, 16, K // 16, 4, 4).permute(0, 2, 3, 1, 4).contiguous()
+            .reshape(N // 16, K // 16, 64, 4))
+
+
+def _rows_packed(w: torch.Tensor, what: str):
+    """(packed weight, N, K) from an [N, K] weight (packed here) or an enc_pack_rows result"""
+    if w.dim() == 2:
+        return enc_pack_rows(w), w.shape[0], w.shape[1]
+    if w.dim() == 4 and tuple(w.shape[2:]) == (64, 4) and w.dtype == torch.float32 and w.is_contiguous():
+        return w, w.shape[0] * 16, w.shape[1] * 16
+    raise ValueError(f"{what}: weights must be [N, K] f32 or enc_pack_rows output [N/16, K/16, 64, 4]")
+
+
 def enc_se_means(m_r: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor):
     """SE excitation from given squeeze means (trk_enc_se_means): s [R, C] f32, bit-identical
     to enc_se's s for the same m_r (card.py:59-78)."""
     _need_gpu(m_r, "enc_se_means")
     if m_r.dtype != torch.float32 or m_r.dim() != 2:
         raise TypeError("enc_se_means: m_r must be [R, C] f32")
-    H, C = w1.shape
+    w1, H, C = _rows_packed(w1, "enc_se_means")
+    w2, C2, H2 = _rows_packed(w2, "enc_se_means")
     R = m_r.shape[0]
-    if m_r.shape[1] != C or w2.shape != (C, H) or b1.numel() != H or b2.numel() != C:
+    if m_r.shape[1] != C or (C2, H2) != (C, H) or b1.numel() != H or b2.numel() != C:
         raise ValueError("enc_se_means: shape mismatch")
     m_r = m_r.contiguous()
     s = torch.empty((R, C), device=m_r.device, dtype=torch.float32)
-    w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
+    b1, b2 = _f32c(b1), _f32c(b2)
     check(lib().trk_enc_se_means(_ptr(m_r), R, C, _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2), _ptr(s),
                                  _stream(m_r.device)), "enc_se_means")
     return s
@@ -307,13 +327,14 @@ def enc_se(sums: torch.Tensor, P: int, w1: torch.Tensor, b1: torch.Tensor, w2: t
     _need_gpu(sums, "enc_se")
     if sums.dtype != torch.int64 or sums.dim() != 3 or sums.shape[1] != _lib.TRK_ENC_PARTS:
         raise TypeError("enc_se: sums must be [R, TRK_ENC_PARTS, 2C] int64 partials")
-    H, C = w1.shape
+    w1, H, C = _rows_packed(w1, "enc_se")
+    w2, C2, H2 = _rows_packed(w2, "enc_se")
     R = sums.shape[0]
-    if sums.shape[2] < 2 * C or w2.shape != (C, H) or b1.numel() != H or b2.numel() != C:
+    if sums.shape[2] < 2 * C or (C2, H2) != (C, H) or b1.numel() != H or b2.numel() != C:
         raise ValueError("enc_se: shape mismatch")
     sums = sums.contiguous()
     out = torch.empty((3, R, C), device=sums.device, dtype=torch.float32)
-    w1, b1, w2, b2 = _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
+    b1, b2 = _f32c(b1), _f32c(b2)
     check(lib().trk_enc_se(_ptr(sums), R, sums.stride(1), P, C, _ptr(w1), _ptr(b1), H, _ptr(w2), _ptr(b2),
                            _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _stream(sums.device)), "enc_se")
     return out[0], out[1], out[2]
@@ -328,13 +349,14 @@ def enc_head(tsums: torch.Tensor, P: int, s: torch.Tensor, m_r: torch.Tensor, m_
     if tsums.dtype != torch.int64 or tsums.dim() != 3 or tsums.shape[1] != _lib.TRK_ENC_PARTS:
         raise TypeError("enc_head: tsums must be [R, TRK_ENC_PARTS, C] int64 partials")
     R, _, C = tsums.shape
-    D = w4.shape[0]
-    if (s.shape != (R, C) or m_r.shape != (R, C) or m_n.shape != (R, C) or w0.shape != (C, C) or
-            w4.shape[1] != C or b4.numel() != D or ln_w.numel() != C or ln_b.numel() != C):
+    w0, N0, K0 = _rows_packed(w0, "enc_head")
+    w4, D, K4 = _rows_packed(w4, "enc_head")
+    if (s.shape != (R, C) or m_r.shape != (R, C) or m_n.shape != (R, C) or (N0, K0) != (C, C) or
+            K4 != C or b4.numel() != D or ln_w.numel() != C or ln_b.numel() != C):
         raise ValueError("enc_head: shape mismatch")
     out = torch.empty((R, D), device=tsums.device, dtype=torch.float32)
     tsums, s, m_r, m_n = tsums.contiguous(), _f32c(s), _f32c(m_r), _f32c(m_n)
-    w0, ln_w, ln_b, w4, b4 = _f32c(w0), _f32c(ln_w), _f32c(ln_b), _f32c(w4), _f32c(b4)
+    ln_w, ln_b, b4 = _f32c(ln_w), _f32c(ln_b), _f32c(b4)
     check(lib().trk_enc_head(_ptr(tsums), R, P, C, _ptr(s), _ptr(m_r), _ptr(m_n), float(alpha), _ptr(w0),
                              _ptr(ln_w), _ptr(ln_b), float(ln_eps), _ptr(w4), _ptr(b4), D, _ptr(out),
                              _stream(tsums.device)), "enc_head")

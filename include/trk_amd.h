@@ -275,6 +275,10 @@ int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, int64_t K, c
  *   partials [R][TRK_ENC_PARTS][C]) -> ProjectionHead (card.py:151-169): out [R][D] =
  *   normalize(w4 . silu(LayerNorm(w0 . g; ln_w, ln_b, ln_eps)) + b4), w0 [C][C],
  *   w4 [D][C].  Replaces ~25 small torch launches between and after the GEMMs.
+ * Weight layout (w1, w2, w0, w4; also trk_enc_se_means): an [N][K] f32 weight is passed in
+ *   fragment order, [N/16][K/16][64][4] with element [t][kb][16 g + r][e] = W[16 t + r][16 kb +
+ *   4 g + e] (ops.enc_pack_rows), so each load reads 1 KiB contiguous; the bias vectors are
+ *   plain.  (Row-major weights are not detected: they give wrong results.)
  * C, H, D multiples of 16, <= 1024; P <= 256. */
 int trk_enc_se(const long long* sums, int64_t R, int64_t ld_sums, int64_t P, int64_t C, const float* w1,
                const float* b1, int64_t H, const float* w2, const float* b2, float* m_r, float* m_n, float* s,

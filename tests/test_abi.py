@@ -114,3 +114,19 @@ def test_no_device_allocation_in_the_library():
                     if re.search(r"\bhip(Malloc\w*|Free\w*|Memset\w*|HostAlloc|HostMalloc)\s*\(", line):
                         bad.append(f"{name}:{i}: {line.strip()}")
     assert not bad, bad
+
+
+def test_enc_pack_rows_layout(trk):
+    """the tail kernels' weight operand order (include/trk_amd.h, "Weight layout"): element
+    [t][kb][16 g + r][e] of the packed [N/16][K/16][64][4] is W[16 t + r][16 kb + 4 g + e]"""
+    from importlib import import_module
+    import torch
+    ops = import_module("a-lightweight-unsupervised-feature-extractor-_amd.ops")
+    W = torch.randn(48, 64, generator=torch.Generator().manual_seed(3))
+    Wp = ops.enc_pack_rows(W)
+    assert tuple(Wp.shape) == (3, 4, 64, 4)
+    for t, kb, g, r, e in ((0, 0, 0, 0, 0), (2, 3, 3, 15, 3), (1, 2, 1, 7, 2)):
+        assert Wp[t, kb, 16 * g + r, e].item() == W[16 * t + r, 16 * kb + 4 * g + e].item()
+    assert torch.equal(Wp.reshape(-1).sort().values, W.reshape(-1).sort().values)  # a permutation
+    with pytest.raises(ValueError):
+        ops.enc_pack_rows(torch.zeros(20, 64))

@@ -18,9 +18,9 @@ parts = torch.zeros(R, 3, 1024, dtype=torch.int64); parts[:, 0] = sums
 parts = parts.to(dev)
 tparts = torch.zeros(R, 3, 512, dtype=torch.int64); tparts[:, 0] = (torch.randn(R, 512, generator=g) * 30 * 2 ** 24).to(torch.int64)
 tparts = tparts.to(dev)
-se = lambda: ops.enc_se(parts, P, W["se_w1"], W["se_b1"], W["se_w2"], W["se_b2"])
+se = lambda: ops.enc_se(parts, P, W["se_w1_pk"], W["se_b1"], W["se_w2_pk"], W["se_b2"])
 m_r, m_n, s = se()
-hd = lambda: ops.enc_head(tparts, P, s, m_r, m_n, 0.5, W["h0"], W["ln_w"], W["ln_b"], 1e-5, W["h4"], W["h4b"])
+hd = lambda: ops.enc_head(tparts, P, s, m_r, m_n, 0.5, W["h0_pk"], W["ln_w"], W["ln_b"], 1e-5, W["h4_pk"], W["h4b"])
 def t(fn, n=20):
     fn(); torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
