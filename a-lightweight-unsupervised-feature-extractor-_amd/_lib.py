@@ -90,7 +90,7 @@ def _declare(L):
     L.trk_enc_g1_dwconv.restype = i32
     L.trk_enc_dsc_gemm.argtypes = [P, i64, i64, i64, P, P, i64, P, P, P]
     L.trk_enc_dsc_gemm.restype = i32
-    L.trk_enc_rmb_front_means.argtypes = [P, i64, P, P, P, P, P, P, P, P]
+    L.trk_enc_rmb_front_means.argtypes = [P, i64, P, P, P, P, P, P, P, P, P]
     L.trk_enc_rmb_front_means.restype = i32
     L.trk_enc_se_means.argtypes = [P, i64, i64, P, P, i64, P, P, P, P]
     L.trk_enc_se_means.restype = i32
@@ -133,8 +133,6 @@ def _declare(L):
     L.trk_lsap_set_prof.restype = i32
     L.trk_enc_set_prof.argtypes = [P]
     L.trk_enc_set_prof.restype = i32
-    L.trk_enc_set_progress.argtypes = [P]
-    L.trk_enc_set_progress.restype = i32
     L.trk_stream_gate.argtypes = [P, ctypes.c_uint32, i64, P]
     L.trk_stream_gate.restype = i32
     L.trk_cost_set_prof.argtypes = [P]

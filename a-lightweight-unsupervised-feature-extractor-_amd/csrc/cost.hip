@@ -26,7 +26,7 @@ int g_cost_v2 = 0;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel
                     // its 147 KiB LDS workgroups stall behind the encoder in the pipeline: 1.23M vs 1.51M ROIs/s),
                     // and cost_kernel instead of cost3 on trk_build_cost_dev (A/B); 0 = default
 
-unsigned long long* g_cost_prof = nullptr;  // trk_cost_set_prof (diagnostics)
+trk::DiagBuf g_cost_prof;  // trk_cost_set_prof (diagnostics)
 
 namespace {
 
@@ -747,7 +747,7 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
     if (work && !g_cost_v2 && Tmax <= 32) {
       // the workspace holds all F frames; this chunk's rows start at frame f0
       Cost3Work w = cost3_work(work, F, Nmax);
-      w.prof = g_cost_prof ? g_cost_prof + f0 * ((Mmax + 3) / 4) * 16 : nullptr;
+      w.prof = g_cost_prof.get() ? g_cost_prof.get() + f0 * ((Mmax + 3) / 4) * 16 : nullptr;
       w.dn += f0 * Nmax * D;
       w.dt += f0 * Nmax;
       hipLaunchKernelGGL(det_prep_kernel, dim3((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf), dim3(256), 0, st, a, w);
@@ -770,6 +770,6 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
 // diagnostics: cost3 per-wave s_memtime breakdown [start, bank load, MFMA chain +
 // top-k, epilogue] (u64 x 4 per wave, 4 waves per (frame, row block)); NULL = off
 extern "C" int trk_cost_set_prof(unsigned long long* buf) {
-  g_cost_prof = buf;
+  g_cost_prof.set(buf);
   return TRK_OK;
 }

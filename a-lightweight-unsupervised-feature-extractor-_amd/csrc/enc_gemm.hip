@@ -19,8 +19,7 @@
 
 #include <utility>
 
-unsigned long long* g_enc_prof = nullptr;  // trk_enc_set_prof (diagnostics: per-workgroup phase stamps)
-uint32_t* g_rf_progress = nullptr;          // trk_enc_set_progress: rmb_front3's finished-ROI counter
+trk::DiagBuf g_enc_prof;  // trk_enc_set_prof (diagnostics: per-workgroup phase stamps)
 int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rmb_front3 workgroup pairs per XCD (0 = CUs / 16 - 2)
 int g_rf3_chunks = 1;  // trk_set_tuning("rf3_chunks"): rmb_front3 generations (each pair's ROIs in that many
                        // chunks, one workgroup each; 1 = one persistent generation)
@@ -769,7 +768,7 @@ struct RfArgs {
   int64_t R;            // ROIs
   int pairs, chunks;    // rmb_front3's grid: workgroup pairs per XCD, generations (ROI chunks)
   unsigned long long* prof;  // trk_enc_set_prof: every wave's phase cycles per ROI (diagnostics)
-  uint32_t* progress;        // trk_enc_set_progress: +1 per finished ROI (group 0's workgroup), or null
+  uint32_t* progress;        // the launch's `progress` argument: +1 per finished ROI (group 0's workgroup), or null
 };
 
 __device__ __forceinline__ int rf_sw(int s) { return (s >> 1) & 3; }
@@ -1291,7 +1290,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
     }
   }
   rf2_signal(ctr + RF2_CSD + half, lane);  // this wave's staging reads are done (the next ROI may write)
-  // the ROI's progress count (trk_enc_set_progress): one relaxed device-scope add per ROI, so a
+  // the ROI's progress count (the launch's `progress` argument): one relaxed device-scope add per ROI, so a
   // trk_stream_gate on another stream can start its work while this front is in its last round
   if (G == 0 && threadIdx.x == 0 && a.progress)
     __hip_atomic_fetch_add(a.progress, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1640,7 +1639,7 @@ int launch4(const EncGemmArgs& a, hipStream_t st) {
     attr = true;
   }
   EncGemmArgs b = a;
-  b.prof = g_enc_prof;
+  b.prof = g_enc_prof.get();
   // dynamic LDS: what the tile uses, not the 80 KiB maximum, so the tracker's and ROI
   // Align's workgroups fit beside two gemm4 workgroups on a CU instead of waiting for one
   // to retire (DSC: ring or staging + partials, 74 KiB; transition: ring + the SE scales
@@ -1723,7 +1722,7 @@ extern "C" int trk_enc_transition_gemm2(const void* XRN, int64_t M, int64_t P, i
   if (g_enc_trans == 1 && Wtp) {
     const int64_t nwg = ((int64_t)M + 127) / 128 * (N / 256);
     TRK_REQUIRE(nwg < 0x7fffffff, "enc_transition_gemm: too many workgroups");
-    a.prof = g_enc_prof;
+    a.prof = g_enc_prof.get();
     const size_t slds = (size_t)G4_SLOTS * 512 * 4;
     hipLaunchKernelGGL((trans4_kernel<1, 2>), dim3((unsigned)nwg), dim3(256), 3 * T4_BUF * 16 + slds, st, a,
                        reinterpret_cast<const uint4*>(Wtp), nwg);
@@ -1753,7 +1752,8 @@ extern "C" int trk_enc_g1_dwconv(const void* X, int64_t M, const void* W1, int64
 }
 
 extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                                       const float* bias, void* XRN, float* m_r, float* m_n, void* stream) {
+                                       const float* bias, void* XRN, float* m_r, float* m_n, uint32_t* progress,
+                                       void* stream) {
   TRK_REQUIRE(M >= 0 && M % RF_S == 0, "enc_rmb_front_means: 10x10 ROIs (M %% 100 == 0), C = 512, 4h = 1024");
   if (M == 0) return TRK_OK;
   TRK_REQUIRE(X && W1p && wdw && W2p && bias && XRN && m_r && m_n && aligned16(X) && aligned16(W1p) &&
@@ -1781,8 +1781,8 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   a.m_r = m_r;
   a.m_n = m_n;
   a.R = M / RF_S;
-  a.prof = g_enc_prof;
-  a.progress = g_rf_progress;
+  a.prof = g_enc_prof.get();
+  a.progress = progress;
   // persistent: 16 workgroups per 8 ROIs up to one per CU (a multiple of 16, so both groups of a
   // ROI share an XCD); rf3_groups 0 = two CUs per XCD left free -- the tracker's and the ROI
   // stream's kernels start there instead of waiting for a persistent workgroup to end
@@ -1802,18 +1802,14 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
 // diagnostics: gemm4 per-workgroup phase stamps (8 u64 per workgroup); nullptr
 // switches them off
 extern "C" int trk_enc_set_prof(unsigned long long* buf) {
-  g_enc_prof = buf;
-  return TRK_OK;
-}
-
-// rmb_front3's finished-ROI counter (one u32 the caller owns, counting on across launches); NULL = off
-extern "C" int trk_enc_set_progress(uint32_t* counter) {
-  g_rf_progress = counter;
+  g_enc_prof.set(buf);
   return TRK_OK;
 }
 
 namespace {
-// one wave: wait until *counter >= target (relaxed device-scope loads, s_sleep between polls) or
+// one wave: wait until the wrapping count *counter has reached target ((int32_t)(v - target) >= 0,
+// so a target within 2^31 of the count is ordered correctly across the wrap; relaxed device-scope
+// loads, s_sleep between polls) or
 // until max_ticks of the 100 MHz clock have passed, then end: the kernels queued behind it on
 // its stream start then.  A performance gate only: it never blocks longer than its bound
 __global__ void __launch_bounds__(64) stream_gate_kernel(const uint32_t* counter, uint32_t target,
@@ -1821,7 +1817,7 @@ __global__ void __launch_bounds__(64) stream_gate_kernel(const uint32_t* counter
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     const uint32_t v = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+    if ((int32_t)(__builtin_amdgcn_readfirstlane(v) - target) >= 0) break;
     if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
     __builtin_amdgcn_s_sleep(16);
   }

@@ -19,7 +19,7 @@
 #include "trk_common.h"
 #include "rb_linear.h"
 
-unsigned long long* g_head_prof = nullptr;  // trk_head_set_prof (diagnostics)
+trk::DiagBuf g_head_prof;  // trk_head_set_prof (diagnostics)
 int g_head_waves = 16;  // trk_set_tuning("head_waves"): enc_head workgroup of 8 or 16 waves
 int g_se_waves = 16;    // trk_set_tuning("se_waves"): enc_se workgroup of 8 or 16 waves (16: 26 vs 29 us)
 
@@ -303,7 +303,7 @@ extern "C" int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_
   TRK_REQUIRE(al16(tsums) && al16(s) && al16(m_r) && al16(m_n) && al16(w0) && al16(w4),
               "enc_head: operands must be 16-byte aligned");
   HeadArgs a{tsums, s, m_r, m_n, w0, ln_w, ln_b, w4, b4, out, (int)R, (int)C, (int)D, (int)P, (float)P, ln_eps, alpha,
-             g_head_prof};
+             g_head_prof.get()};
   const size_t lds = (size_t)RB * (2 * ld_rows((int)C) + ld_rows((int)D)) * 4;
   static bool attr = false;
   if (!attr) {
@@ -325,6 +325,6 @@ extern "C" int trk_enc_head(const long long* tsums, int64_t R, int64_t P, int64_
 // diagnostics: enc_head per-wave s_memtime phases (u64 x 5 per wave, 8 waves per
 // 16-ROI workgroup); NULL = off
 extern "C" int trk_head_set_prof(unsigned long long* buf) {
-  g_head_prof = buf;
+  g_head_prof.set(buf);
   return TRK_OK;
 }

@@ -35,7 +35,7 @@
 
 #include <type_traits>
 
-unsigned long long* g_lsap_prof = nullptr;  // trk_lsap_set_prof (diagnostics)
+trk::DiagBuf g_lsap_prof;  // trk_lsap_set_prof (diagnostics)
 int g_lsap_dev_lds_kb = 24;  // trk_set_tuning("lsap_dev_lds_kb"): LDS budget of trk_lsap_dev workgroups.  Small
                              // enough to be placed beside the encoder's workgroups (a CU's whole LDS would wait for
                              // a CU free of them); the leading-row shortcut needs no ring, the sequential rows re-read
@@ -704,7 +704,7 @@ extern "C" int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
-    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 16 : nullptr;
+    a.prof = g_lsap_prof.get() ? g_lsap_prof.get() + f0 * 16 : nullptr;
     int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                              : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
@@ -759,7 +759,7 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
     a.status = status + f0;
     a.assign = assign ? assign + f0 * nr_max : nullptr;
     a.cost_max = cost_max;
-    a.prof = g_lsap_prof ? g_lsap_prof + f0 * 16 : nullptr;
+    a.prof = g_lsap_prof.get() ? g_lsap_prof.get() + f0 * 16 : nullptr;
     const int e = dtype == TRK_F32 ? launch_ks<float>(wc_max, dim3(nf), lds, st, a)
                                    : launch_ks<double>(wc_max, dim3(nf), lds, st, a);
     if (e) return e;
@@ -771,6 +771,6 @@ extern "C" int trk_lsap_dev(int64_t F, const void* C, int dtype, int64_t ld, int
  * into buf [F][16] u64 (solver: wait, scan, dual, augment, iterations, total, nr, nc; workgroup:
  * shortcut pass, loaders + solver, outputs, total, 0...); NULL = off */
 extern "C" int trk_lsap_set_prof(unsigned long long* buf) {
-  g_lsap_prof = buf;
+  g_lsap_prof.set(buf);
   return TRK_OK;
 }

@@ -45,4 +45,21 @@ constexpr int kWave = 64;
 
 inline bool aligned16_ptr(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// A diagnostics buffer set by a trk_*_set_prof call: bound to the device current at that call,
+// and handed only to launches on that same device (get() is null elsewhere), so a stamp buffer
+// never receives another device's writes.  The library's only process-wide device pointers.
+struct DiagBuf {
+  unsigned long long* p = nullptr;
+  int dev = -1;
+  void set(unsigned long long* q) {
+    p = q;
+    dev = -1;
+    if (q && hipGetDevice(&dev) != hipSuccess) p = nullptr;
+  }
+  unsigned long long* get() const {
+    int d = -1;
+    return (p && hipGetDevice(&d) == hipSuccess && d == dev) ? p : nullptr;
+  }
+};
+
 }  // namespace trk

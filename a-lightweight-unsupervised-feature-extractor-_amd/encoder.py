@@ -183,9 +183,13 @@ class Model(nn.Module):
                 f32(se[2].weight), f32(se[2].bias)
             w["h0"], w["ln_w"], w["ln_b"] = f32(hd[0].weight), f32(hd[1].weight), f32(hd[1].bias)
             w["h4"], w["h4b"] = f32(hd[4].weight), f32(hd[4].bias)
-            from .ops import enc_pack_rows  # the tail kernels' weight operands in fragment order
-            for k in ("se_w1", "se_w2", "h0", "h4"):
-                w[k + "_pk"] = enc_pack_rows(w[k])
+            # the tail kernels' weight operands in fragment order: only when the fused tail can
+            # run (every dimension a multiple of 16); other sizes take the plain-torch SE / head
+            tail = ("se_w1", "se_w2", "h0", "h4")
+            if all(w[k].shape[0] % 16 == 0 and w[k].shape[1] % 16 == 0 for k in tail):
+                from .ops import enc_pack_rows
+                for k in tail:
+                    w[k + "_pk"] = enc_pack_rows(w[k])
         self._fused, self._fused_key = w, key
         return w
 
@@ -230,6 +234,8 @@ class Model(nn.Module):
     defer_head = False   # fused tail: return a DeferredHead instead of launching enc_head
     stage_hook = None    # fused bf16 path: called as stage_hook("g1" | "dsc") right after that GEMM is
                          # enqueued (a caller can record an event there to place other streams' work)
+    front_progress = None  # fused front: a one-element int32 device counter the front advances by one
+                           # per finished ROI (enc_rmb_front_means' `progress`; a stream_gate waits on it)
 
     def _forward_device(self, x: torch.Tensor) -> torch.Tensor:
         """GEMMs on hipBLASLt (torch) or the fused trk GEMMs, everything else in trk HIP kernels."""
@@ -249,7 +255,8 @@ class Model(nn.Module):
         ten = fused and S1 == 10 and S2 == 10 and C == 512 and X.is_contiguous()
         front = ten and self.fused_front and "w1_pk" in W and Co == 512
         if front:
-            XRN, m_r, m_n = enc_rmb_front_means(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"])
+            XRN, m_r, m_n = enc_rmb_front_means(X, W["w1_pk"], W["dw_t"], W["w2_pk"], W["b2"],
+                                                progress=self.front_progress)
             if self.stage_hook is not None:
                 self.stage_hook("g1")
                 self.stage_hook("dsc")
@@ -267,7 +274,7 @@ class Model(nn.Module):
                 XRN, sums = enc_dsc_gemm(Y2, ss, W["w2_nk"], W["b2"], raw=True)
                 if self.stage_hook is not None:
                     self.stage_hook("dsc")
-            if self.fused_tail:
+            if self.fused_tail and "se_w1_pk" in W:
                 # SE MLP (+ the squeeze means unless the front wrote them), then Shake2 mix +
                 # projection head: one kernel each
                 if front:
@@ -315,17 +322,18 @@ class Model(nn.Module):
         h4 = W["w1t"].shape[1]
         h2 = h4 // 2
         ss = S1 * S2
+        Co = W["w2r"].shape[1]
         X = x.permute(0, 2, 3, 1).reshape(N * ss, C)
         Y1 = (X @ W["w1t"]).view(N, S1, S2, h4).permute(0, 3, 1, 2)
         Y2 = F.conv2d(Y1, W["dw"], padding=2, groups=h4).permute(0, 2, 3, 1).reshape(N * ss, h4)
-        xr = F.silu(torch.addmm(W["br"], Y2[:, :h2], W["w2r"])).view(N, ss, C)
-        xn = F.hardswish(torch.addmm(W["bn"], Y2[:, h2:], W["w2n"])).view(N, ss, C)
+        xr = F.silu(torch.addmm(W["br"], Y2[:, :h2], W["w2r"])).view(N, ss, Co)
+        xn = F.hardswish(torch.addmm(W["bn"], Y2[:, h2:], W["w2n"])).view(N, ss, Co)
         m_r = xr.mean(1, dtype=torch.float32)
         s = self._se(m_r)
-        xfs = (xr * s.to(dt)[:, None, :]).view(N * ss, C)
+        xfs = (xr * s.to(dt)[:, None, :]).view(N * ss, Co)
         T = torch.addmm(W["bt"], xfs, W["wt1"])
-        T.addmm_(xn.reshape(N * ss, C), W["wt2"])
-        m_cat = F.silu(T).view(N, ss, C).mean(1, dtype=torch.float32)
+        T.addmm_(xn.reshape(N * ss, Co), W["wt2"])
+        m_cat = F.silu(T).view(N, ss, Co).mean(1, dtype=torch.float32)
         m_n = xn.mean(1, dtype=torch.float32)
         a = self._alpha()
         g = 0.5 * m_cat + 0.5 * (a * (s * m_r) + (1 - a) * m_n)

@@ -229,12 +229,14 @@ def enc_sums_reduce(part: torch.Tensor, P: int) -> torch.Tensor:
 
 
 def enc_rmb_front_means(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W2p: torch.Tensor,
-                        bias: torch.Tensor):
+                        bias: torch.Tensor, progress: Optional[torch.Tensor] = None):
     """bf16, 10x10 ROIs of 512 channels: enc_g1_dwconv + enc_dsc_gemm in one kernel
     (trk_enc_rmb_front_means; Y2 stays in LDS).  X [R*100, 512], W1p / W2p from
     enc_pack_fragments, wdw [25, 1024] f32, bias [1024] f32 -> (XRN [R*100, 1024], m_r, m_n
     [R, 512] f32): XRN bit-identical to the two-kernel path, m_r / m_n the squeeze means
-    enc_se takes (of the kernel's own f32 column sums)."""
+    enc_se takes (of the kernel's own f32 column sums).  progress: None, or a one-element
+    int32 tensor on X's device that the launch advances by one per finished ROI (the count a
+    stream_gate on another stream waits for; it wraps at 2^32)."""
     _need_gpu(X, "enc_rmb_front_means")
     if X.dtype != torch.bfloat16 or W1p.dtype != torch.bfloat16 or W2p.dtype != torch.bfloat16:
         raise TypeError("enc_rmb_front_means: bf16 operands required")
@@ -245,30 +247,24 @@ def enc_rmb_front_means(X: torch.Tensor, W1p: torch.Tensor, wdw: torch.Tensor, W
         raise ValueError("enc_rmb_front_means: W1p / W2p must be enc_pack_fragments output [2, 16, 32, 4, 16, 8]")
     if wdw.shape != (25, 1024) or wdw.dtype != torch.float32 or bias.numel() != 1024:
         raise ValueError("enc_rmb_front_means: wdw [25, 1024] f32 and bias [1024] required")
+    if progress is not None and (progress.dtype != torch.int32 or progress.numel() < 1 or
+                                 progress.device != X.device):
+        raise TypeError("enc_rmb_front_means: progress must be a one-element int32 tensor on X's device")
     M = X.shape[0]
     XRN = torch.empty((M, 1024), device=X.device, dtype=torch.bfloat16)
     m = torch.empty((2, M // 100, 512), device=X.device, dtype=torch.float32)
     check(lib().trk_enc_rmb_front_means(_ptr(X), M, _ptr(W1p), _ptr(wdw.contiguous()), _ptr(W2p),
                                         _ptr(bias.to(torch.float32).contiguous()), _ptr(XRN), _ptr(m[0]), _ptr(m[1]),
-                                        _stream(X.device)), "enc_rmb_front_means")
+                                        _ptr(progress), _stream(X.device)), "enc_rmb_front_means")
     return XRN, m[0], m[1]
 
 
-def enc_set_progress(counter: Optional[torch.Tensor]) -> None:
-    """Later enc_rmb_front_means launches add 1 per finished ROI to counter (a one-element
-    int32 device tensor the caller keeps alive and zeroes; the count runs on across
-    launches); None switches it off (trk_enc_set_progress)."""
-    if counter is not None:
-        _need_gpu(counter, "enc_set_progress")
-        if counter.dtype != torch.int32 or counter.numel() < 1:
-            raise TypeError("enc_set_progress: a one-element int32 device tensor required")
-    check(lib().trk_enc_set_progress(_ptr(counter)), "enc_set_progress")
-
-
 def stream_gate(counter: torch.Tensor, target: int, max_us: int = 2000) -> None:
-    """Enqueue on the current stream a one-wave kernel that returns once counter[0] >= target
-    (an enc_set_progress counter another stream's front advances) or after max_us: the work
-    queued behind it starts then (trk_stream_gate; a scheduling hint, not an ordering)."""
+    """Enqueue on the current stream a one-wave kernel that returns once the wrapping u32 count
+    counter[0] has reached target ((int32)(count - target) >= 0: a target within 2^31 of the
+    count; the `progress` counter of enc_rmb_front_means launches on another stream) or after
+    max_us: the work queued behind it starts then (trk_stream_gate; a scheduling hint, not an
+    ordering)."""
     _need_gpu(counter, "stream_gate")
     if counter.dtype != torch.int32:
         raise TypeError("stream_gate: int32 counter required")

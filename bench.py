@@ -167,9 +167,6 @@ def frame_map(sc, f):
     return sc["feat"][f % sc["feat"].shape[0]]
 
 
-_PROGRESS = {}  # device index -> the fronts' finished-ROI counter (trk_enc_set_progress)
-
-
 class Pipeline:
     """The per-frame hot path over a batch of streams.
 
@@ -230,7 +227,7 @@ class Pipeline:
         # TRK_ROI_GATE_FRAC < 1: instead of frame f's whole front, frame f+1's ROI stage waits
         # (trk_stream_gate, bounded) until the front has finished that fraction of its ROIs, so it
         # starts on the CUs the persistent front's last, partly filled round leaves idle (the front
-        # counts finished ROIs into a device counter, trk_enc_set_progress)
+        # counts finished ROIs into a device counter: enc_rmb_front_means' `progress` argument)
         # Default 0.93 since r05: 2.030-2.053 vs 1.968-2.043M ROIs/s, six of seven interleaved
         # pairs ahead, +1.1 % in the means (r5l, r5l2); 0.88 / 0.91 / 0.95 / 0.97 within or below
         self.gate_frac = float(os.environ.get("TRK_ROI_GATE_FRAC", "0.93"))
@@ -238,13 +235,14 @@ class Pipeline:
         self.fronts_rois = 0       # the count the counter reaches once every enqueued front is done
         self.roi_gate_target = None
         if self.roi_after == "dsc" and self.gate_frac < 1:
-            dev = sc["feat"].device
-            # one counter per device for the process: the library keeps its pointer, so it must
-            # never be freed under a later launch
-            self.progress = _PROGRESS.setdefault(dev.index, torch.zeros(1, dtype=torch.int32, device=dev))
-            torch.cuda.synchronize()
-            self.fronts_rois = int(self.progress.item()) & 0xFFFFFFFF
-            trk.ops.enc_set_progress(self.progress)
+            # the pipeline's own counter, passed to its fronts as their `progress` argument (the
+            # library keeps no pointer); started near the u32 wrap (TRK_PROGRESS_START) to show
+            # the gate's wrap-safe comparison in a run
+            start = int(os.environ.get("TRK_PROGRESS_START", "0")) & 0xFFFFFFFF
+            self.progress = torch.tensor([start - (1 << 32) if start >= 1 << 31 else start],
+                                         dtype=torch.int32, device=sc["feat"].device)
+            self.fronts_rois = start
+            self.model.front_progress = self.progress
         # TRK_EMBED_OVERLAP=1 (with TRK_EMBED_STREAMS=2, both the default since r05): frame f+1's
         # encoder, on the other embedding stream, waits only for frame f's front (not its SE and
         # transition), so the next front's workgroups fill the CUs the transition's last round
@@ -274,12 +272,13 @@ class Pipeline:
         self.map_pending = {}
 
     def close_progress(self):
-        """stop the fronts' progress counting (the isolated kernel pass launches fronts the
-        pipeline's targets do not know of)"""
+        """stop the fronts' progress counting and the gates on it (graph capture, and the
+        isolated kernel pass's fronts, which the pipeline's targets do not know of)"""
         if self.progress is not None:
             torch.cuda.synchronize()
-            trk.ops.enc_set_progress(None)
+            self.model.front_progress = None
             self.progress = None
+            self.roi_gate_target = None
 
     def _map_ahead(self, f):
         if not self.map_ahead or f in self.map_pending or f >= len(self.sc["rois"]):
@@ -296,6 +295,14 @@ class Pipeline:
         the embeddings frame f's tracker step is still reading).  Removes the
         launch gaps between the ~30 kernels of the stage."""
         sc = self.sc
+        # graph replays never call the stage hook again: the events and targets it would set up
+        # (the overlap's front_ev, the ROI progress gate) belong to the eager pipeline, so both
+        # are switched off here, before the capture records anything
+        self.close_progress()
+        self.overlap = False
+        self.front_ev = None
+        self.roi_gate = None
+        self.model.stage_hook = None
         self.graphs = []
         for _ in range(2):
             rois = sc["rois"][0].clone()

@@ -167,18 +167,17 @@ int trk_lsap(int64_t F, const void* C, int dtype, int64_t ld, int64_t batch_stri
  * cycle breakdown into buf [F][16] u64 (shader clocks: waiting for rows, scans +
  * argmin, dual updates, augmentation; iterations, total, nr, nc; then the workgroup's
  * shortcut pass, loaders + solver, outputs, total).  NULL = off. */
-int trk_lsap_set_prof(unsigned long long* buf);
+int trk_lsap_set_prof(unsigned long long* buf);  /* (bound to the device current at the call, like every *_set_prof) */
 /* diagnostics: per-workgroup (gemm4, trans4: 8 u64 each) or per-wave (rmb_front3: [ROI][group]
  * [wave][8] u64) phase timestamps of the encoder GEMMs; NULL = off */
 int trk_enc_set_prof(unsigned long long* buf);
-/* Progress of the persistent encoder front (trk_enc_rmb_front_means): later launches add 1 to
- * *counter (one u32 in device memory the caller owns and zeroes) for every ROI they finish, so
- * the count runs on across launches; NULL = off.  trk_stream_gate enqueues on `stream` a
- * one-wave kernel that returns once *counter >= target, or after max_us microseconds (0..1e6)
- * whatever the count: work queued behind it on that stream starts when a front on another
- * stream has finished `target` ROIs.  A scheduling hint only (the bound makes it one); order
- * that correctness needs still takes events. */
-int trk_enc_set_progress(uint32_t* counter);
+/* trk_stream_gate enqueues on `stream` a one-wave kernel that returns once the wrapping u32
+ * count *counter has reached target -- (int32_t)(*counter - target) >= 0, so targets must lie
+ * within 2^31 of the count when the gate runs -- or after max_us microseconds (0..1e6) whatever
+ * the count: work queued behind it on that stream starts when a front on another stream
+ * (trk_enc_rmb_front_means with that counter as its `progress`) has finished `target` ROIs.  A
+ * scheduling hint only (the bound makes it one); order that correctness needs still takes
+ * events.  The counter lives on the device the gate is launched on. */
 int trk_stream_gate(const uint32_t* counter, uint32_t target, int64_t max_us, void* stream);
 /* diagnostics: per-wave timestamps of the bank-resident cost kernel; NULL = off */
 int trk_cost_set_prof(unsigned long long* buf);
@@ -251,9 +250,14 @@ int trk_enc_dsc_gemm(const void* Y2, int64_t M, int64_t P, int64_t Kg, const voi
  *   + j] (trk.ops.enc_pack_fragments); wdw [25][1024] f32, bias [1024] f32 (BN-folded).
  *   XRN [M][1024] is bit-identical to the two-kernel path; m_r = mean SiLU(x_r), m_n = mean
  *   Hardswish(x_n) [R][512] f32 as trk_enc_se computes them from int64 sums, of the kernel's
- *   own f32 column sums.  Pair with trk_enc_se_means. */
+ *   own f32 column sums.  Pair with trk_enc_se_means.
+ *   progress (may be NULL): one u32 in device memory on the launch's device, owned by the
+ *   caller; the launch adds 1 to it (relaxed, device scope) for every ROI it finishes, so a
+ *   trk_stream_gate on another stream can start work before the whole front is done.  The
+ *   count wraps at 2^32; the library keeps no pointer after the call. */
 int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p, const float* wdw, const void* W2p,
-                            const float* bias, void* XRN, float* m_r, float* m_n, void* stream);
+                            const float* bias, void* XRN, float* m_r, float* m_n, uint32_t* progress,
+                            void* stream);
 int trk_enc_transition_gemm(const void* XRN, int64_t M, int64_t P, int64_t K, const float* s, int64_t kscale,
                             const void* Wt, const float* bias, int64_t N, long long* sums, void* stream);
 /* trk_enc_transition_gemm2: the same, also given Wtp = Wt [512][1024] in MFMA fragment order

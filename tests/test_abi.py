@@ -3,9 +3,12 @@ public header declares, and rejects bad arguments on the host before any
 launch (SURVEY.md 8(b) error conventions)."""
 import ctypes
 import os
+from pathlib import Path
 
 import numpy as np
 import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
 
 
 def test_library_exports_header_symbols(trk):
@@ -87,10 +90,10 @@ def test_rmb_front_fragment_packing_and_argument_errors(trk):
     assert torch.equal(ops.enc_pack_fragments(W.view(2, 512, 512)), ops.enc_pack_fragments(W))
     L = trk.lib()
     v = ctypes.c_void_p(16)
-    assert L.trk_enc_rmb_front_means(None, 0, *([None] * 8)) == 0
-    assert L.trk_enc_rmb_front_means(v, 150, *([v] * 8)) == -1
+    assert L.trk_enc_rmb_front_means(None, 0, *([None] * 9)) == 0
+    assert L.trk_enc_rmb_front_means(v, 150, *([v] * 9)) == -1
     assert b"M % 100" in L.trk_last_error()
-    assert L.trk_enc_rmb_front_means(v, 100, *([v] * 5), None, v, v) == -1
+    assert L.trk_enc_rmb_front_means(v, 100, *([v] * 5), None, v, None, v) == -1
     # trk_enc_transition_gemm2: packed weights only for K = 1024, N = 512, kscale = 512
     assert L.trk_enc_transition_gemm2(v, 100, 100, 1024, v, 512, v, v, v, 768, v, None) == -1
     assert b"N = 512" in L.trk_last_error()
@@ -130,3 +133,52 @@ def test_enc_pack_rows_layout(trk):
     assert torch.equal(Wp.reshape(-1).sort().values, W.reshape(-1).sort().values)  # a permutation
     with pytest.raises(ValueError):
         ops.enc_pack_rows(torch.zeros(20, 64))
+
+
+def test_no_mutable_device_pointer_globals_in_csrc():
+    """The library keeps no caller-owned device pointer between calls (r05 verdict: the front's
+    progress counter was a process-global; it is now an argument of the launch).  The only
+    pointer-holding globals are the trk_*_set_prof diagnostics buffers, and those are
+    trk::DiagBuf (bound to the device current when set, handed only to launches on that
+    device).  Scans every namespace-scope declaration in csrc/ for a pointer type."""
+    import re
+    csrc = ROOT / "a-lightweight-unsupervised-feature-extractor-_amd" / "csrc"
+    bad, diag = [], []
+    for f in sorted(list(csrc.glob("*.hip")) + list(csrc.glob("*.cpp")) + list(csrc.glob("*.h"))):
+        depth = 0
+        for ln, line in enumerate(f.read_text().splitlines(), 1):
+            code = line.split("//")[0]
+            at_file_scope = depth == 0 or (depth == 1 and re.match(r"^\S", line) is not None)
+            if at_file_scope and re.match(r"^(static\s+)?(const\s+)?[A-Za-z_][\w:<>]*\s*\*+\s*g_\w+\s*(=|;)", code):
+                bad.append(f"{f.name}:{ln}: {line.strip()}")
+            if re.match(r"^trk::DiagBuf\s+g_\w+;", code):
+                diag.append(f.name)
+            depth += code.count("{") - code.count("}")
+    assert not bad, bad
+    assert sorted(diag) == ["cost.hip", "enc_gemm.hip", "enc_head.hip", "lsap.hip"]
+    src = (csrc / "enc_gemm.hip").read_text()
+    assert "g_rf_progress" not in src and "set_progress" not in src
+    assert "(int32_t)(__builtin_amdgcn_readfirstlane(v) - target) >= 0" in src  # wrap-safe gate
+
+
+def test_encoder_odd_sizes_forward_on_cpu(trk, oracle):
+    """A Model whose SE hidden size (out_channels / 4 = 10) and proj_dim (24) are not
+    multiples of 16 still runs forward (r05 advisor: the tail kernels' weight packing used to
+    raise for every forward, including the CPU / fp32 paths that never read it); the packs are
+    made only when the fused tail can run.  Checked against the oracle's fp32 eval graph."""
+    import torch
+    torch.manual_seed(3)
+    m = trk.Model(in_channels=48, out_channels=40, warmup_epochs=10, proj_dim=24).eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.normal_(0, 0.2)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.normal_(0, 0.1)
+                mod.running_var.uniform_(0.5, 1.5)
+        x = torch.randn(3, 48, 10, 10)
+        z = m(x)
+        assert "se_w1_pk" not in m._fused
+        ref = oracle.encoder_forward({k: v.float() for k, v in m.state_dict().items()}, x)
+    assert z.shape == (3, 24)
+    assert (z - ref).abs().max().item() < 1e-5

@@ -803,33 +803,40 @@ def test_enc_rmb_front_vs_two_kernel_path(trk, gpu, R, groups, chunks):
 
 @pytest.mark.parametrize("chunks", [1, 4])
 def test_enc_front_progress_and_stream_gate(trk, gpu, chunks):
-    """trk_enc_set_progress: every rmb_front3 launch adds one per finished ROI (R = 37 and 300,
-    the persistent grid and 4 generations) to the caller's counter and leaves the results
-    unchanged; NULL stops the count.  trk_stream_gate: returns at once once the count is
-    reached, after its bound otherwise, and the work queued behind it then runs."""
+    """enc_rmb_front_means' `progress` argument: a launch adds one per finished ROI (R = 37 and
+    300, the persistent grid and 4 generations) to the caller's counter and leaves the results
+    unchanged; a launch without it leaves the counter alone (the library keeps no pointer).
+    trk_stream_gate: returns at once once the count is reached, after its bound otherwise, and
+    the work queued behind it then runs.  The counter starts at 0xFFFFFF00, so the fronts carry
+    it across the u32 wrap: the gate's comparison is wrap-safe (a reached target past the wrap
+    opens at once, one not yet reached before the wrap waits for its bound)."""
     import time
     ops, X, W1, wdw, W2, b2, se = _front_operands(gpu, 300, 300)
     L = trk.lib()
     W1p, W2p = ops.enc_pack_fragments(W1), ops.enc_pack_fragments(W2)
     ref = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
-    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    start = 0xFFFFFF00
+    cnt = torch.tensor([start - (1 << 32)], dtype=torch.int32, device=gpu)
+    u32 = lambda: int(cnt.item()) & 0xFFFFFFFF
     assert L.trk_set_tuning(b"rf3_chunks", chunks) == 0
     try:
-        ops.enc_set_progress(cnt)
-        out = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
-        ops.enc_rmb_front_means(X[: 37 * 100], W1p, wdw, W2p, b2)
+        out = ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2, progress=cnt)
+        ops.enc_rmb_front_means(X[: 37 * 100], W1p, wdw, W2p, b2, progress=cnt)
         torch.cuda.synchronize()
-        assert cnt.item() == 337
-        ops.enc_set_progress(None)
+        assert u32() == (start + 337) & 0xFFFFFFFF == 81
         ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2)
         torch.cuda.synchronize()
-        assert cnt.item() == 337
+        assert u32() == 81
     finally:
-        ops.enc_set_progress(None)
         L.trk_set_tuning(b"rf3_chunks", 1)
     assert all(torch.equal(a, b) for a, b in zip(out, ref))
+    with pytest.raises(TypeError, match="progress"):
+        ops.enc_rmb_front_means(X, W1p, wdw, W2p, b2, progress=cnt.to(torch.int64))
     side = torch.cuda.Stream(device=gpu)
-    for target, bound_us, slow in ((300, 500000, False), (338, 20000, True)):
+    # targets as a caller computes them from the start: before the wrap, just past it (both
+    # reached: open at once), and one ROI beyond the count (waits for its bound)
+    for target, bound_us, slow in ((start + 200, 500000, False), ((start + 300) & 0xFFFFFFFF, 500000, False),
+                                   ((start + 338) & 0xFFFFFFFF, 20000, True)):
         flag = torch.zeros(1, dtype=torch.int32, device=gpu)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
