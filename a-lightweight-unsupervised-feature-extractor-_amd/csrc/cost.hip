@@ -27,6 +27,9 @@ int g_cost_v2 = 0;  // trk_set_tuning("cost_v2"): 1 = bank-resident cost2_kernel
                     // and cost_kernel instead of cost3 on trk_build_cost_dev (A/B); 0 = default
 
 trk::DiagBuf g_cost_prof;  // trk_cost_set_prof (diagnostics)
+int g_cost_split = 1;  // trk_set_tuning("cost_split"): 1 (default) = cost3's similarities from f16 hi / lo splits on
+                       // the f16 MFMA (3 products, within 1.1e-6 of exact f32); 0 = exact f32 MFMA
+                       // (bit-identical to cost_kernel)
 
 namespace {
 
@@ -405,6 +408,24 @@ __global__ void __launch_bounds__(256) cost2_kernel(const CostArgs A) {
 //                    cost_kernel's: identical outputs.
 // HBM bytes per launch: the live banks (M x T x 512 B) + the detections twice
 // (N x 512 B) + the cost rows, against cost_kernel's bank read per 32-column tile.
+// The similarity on the f16 MFMA (cost_split 1): each f32 x of a unit row as x ~ hi + 2^-11 lo with
+// hi = f16(x) (f16 subnormals flushed to zero here, so the MFMA multiplies exactly the hi the
+// residual was taken from) and lo = f16((x - hi) * 2^11) (scaled into f16's normal range).  Then
+// a.b = sum hi_a hi_b + 2^-11 sum (hi_a lo_b + lo_a hi_b) + e, three products of exact f16 pairs
+// with f32 accumulation (v_mfma_f32_32x32x16_f16: 32 cycles per 32x32x16, against the exact f32
+// 32x32x2's 64 cycles per 32x32x2: 768 vs 4,096 cycles per 32-detection tile); |e| <= 3 * 2^-22
+// sum |a_k b_k| + 128 * 2^-25 <= 1.1e-6 for unit rows (the dropped lo*lo term, the two f16
+// roundings of lo, lo's subnormal floor), typically ~1e-8
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+struct Split16 {
+  _Float16 hi, lo;
+};
+__device__ __forceinline__ Split16 split16(float x) {
+  _Float16 hh = (_Float16)x;
+  if (__builtin_fabsf((float)hh) < 6.103515625e-05f) hh = (_Float16)0.f;  // below 2^-14: subnormal
+  return {hh, (_Float16)((x - (float)hh) * 2048.f)};
+}
+
 struct Cost3Work {
   float* dn;       // [F][Nmax][D] renormalised detections
   DetTerms* dt;    // [F][Nmax]
@@ -425,6 +446,9 @@ inline Cost3Work cost3_work(void* work, int64_t F, int64_t Nmax) {
   return w;
 }
 
+// SPLIT: the renormalised rows as f16 hi / lo pairs (split16), [Nmax][2][128] f16 in the same 512 B
+// per detection: hi row, then lo row
+template <bool SPLIT>
 __global__ void __launch_bounds__(256) det_prep_kernel(const CostArgs A, Cost3Work w) {
   const int f = blockIdx.y;
   const int N = A.dev_N ? min(A.dev_N[f], A.Nmax) : A.N[f];
@@ -439,9 +463,25 @@ __global__ void __launch_bounds__(256) det_prep_kernel(const CostArgs A, Cost3Wo
   ss += __shfl_xor(ss, 1);
   const float nrm = (float)sqrt(ss) + 1e-12f;
   float* o = w.dn + ((int64_t)f * A.Nmax + j) * D + 64 * h;
+  if (SPLIT) {
+    _Float16* oh = reinterpret_cast<_Float16*>(w.dn + ((int64_t)f * A.Nmax + j) * D) + 64 * h;
 #pragma unroll
-  for (int s = 0; s < 64; s += 4)
-    *reinterpret_cast<float4*>(o + s) = make_float4(b[s] / nrm, b[s + 1] / nrm, b[s + 2] / nrm, b[s + 3] / nrm);
+    for (int s = 0; s < 64; s += 8) {
+      h8v hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const Split16 v = split16(b[s + e] / nrm);
+        hi[e] = v.hi;
+        lo[e] = v.lo;
+      }
+      *reinterpret_cast<h8v*>(oh + s) = hi;
+      *reinterpret_cast<h8v*>(oh + 128 + s) = lo;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 64; s += 4)
+      *reinterpret_cast<float4*>(o + s) = make_float4(b[s] / nrm, b[s + 1] / nrm, b[s + 2] / nrm, b[s + 3] / nrm);
+  }
   if (h == 0) {
     DetTerms t;
     det_terms(A.dbox + ((int64_t)f * A.Nmax + j) * 4, A.conf_cur[(int64_t)f * A.Nmax + j], t.ccx, t.ccy, t.Ac, t.ccv,
@@ -462,8 +502,20 @@ __device__ __forceinline__ void load_b_tile(const float* dnf, int j, int N, int 
   }
 }
 
-// KT: top-k network length (5 when the requested topk <= 5 -- the YAML's 5 -- else kMaxTopk)
-template <int KT>
+// the f16 split B fragments of detection row j: lane half h, K step st holds elements
+// 64 h + 8 st .. + 7 (hi in bh, lo in bl; as load_b_tile, columns past N read row N - 1)
+__device__ __forceinline__ void load_b_split(const float* dnf, int j, int N, int h, h8v (&bh)[8], h8v (&bl)[8]) {
+  const _Float16* p = reinterpret_cast<const _Float16*>(dnf + (int64_t)min(j, N - 1) * D) + 64 * h;
+#pragma unroll
+  for (int st = 0; st < 8; ++st) {
+    bh[st] = *reinterpret_cast<const h8v*>(p + 8 * st);
+    bl[st] = *reinterpret_cast<const h8v*>(p + 128 + 8 * st);
+  }
+}
+
+// KT: top-k network length (5 when the requested topk <= 5 -- the YAML's 5 -- else kMaxTopk).
+// SPLIT: the similarities from f16 hi / lo splits (split16) on the f16 MFMA, else exact f32 MFMA
+template <int KT, bool SPLIT>
 __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const Cost3Work w) {
   const int f = blockIdx.y;
   const int lane = threadIdx.x & 63;
@@ -516,15 +568,12 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
     float* Ca = A.C_app ? A.C_app + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
     // one 32-detection tile, straight-line: the tile's detection terms are loaded first,
     // then the next tile's B fragments (into the other buffer), then the MFMA chain, so
-    // the epilogue's wait for the terms leaves the prefetch in flight
-    auto tile = [&](int j0, const float (&b)[64], float (&bn)[64]) {
+    // the epilogue's wait for the terms leaves the prefetch in flight.  `sims` runs the
+    // chain and leaves the 32 x 32 similarities in the f32x16 accumulator layout
+    auto tile = [&](int j0, auto&& sims) {
       const int j = j0 + col;
       const DetTerms t = dtf[min(j, N - 1)];
-      load_b_tile(dnf, j + 32, N, h, bn);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
-      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  #pragma unroll
-      for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+      const f32x16 acc = sims(j);
       float tk[kMaxTopk];
   #pragma unroll
       for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
@@ -561,12 +610,60 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
         if (Ca) Ca[j] = app;
       }
     };
-    float b0[64], b1[64];
-    load_b_tile(dnf, col, N, h, b0);
-    for (int j0 = 0; j0 < N; j0 += 64) {
-      tile(j0, b0, b1);
-      if (j0 + 32 >= N) break;
-      tile(j0 + 32, b1, b0);
+    if constexpr (SPLIT) {
+      h8v ah[8], al[8];
+  #pragma unroll
+      for (int st = 0; st < 8; ++st)
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const Split16 v = split16(a[8 * st + e]);
+          ah[st][e] = v.hi;
+          al[st][e] = v.lo;
+        }
+      auto chain = [&](const h8v (&bh)[8], const h8v (&bl)[8], h8v (&nh)[8], h8v (&nl)[8]) {
+        return [&](int j) {
+          load_b_split(dnf, j + 32, N, h, nh, nl);
+          __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
+          // one accumulator (a second one spilled the kernel): the 2^11-scaled cross terms
+          // first, scaled back exactly, then the hi x hi products on top
+          f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int st = 0; st < 8; ++st) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[st], bl[st], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[st], bh[st], acc, 0, 0, 0);
+          }
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = acc[r] * (1.0f / 2048.0f);
+  #pragma unroll
+          for (int st = 0; st < 8; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[st], bh[st], acc, 0, 0, 0);
+          return acc;
+        };
+      };
+      h8v h0[8], l0[8], h1[8], l1[8];
+      load_b_split(dnf, col, N, h, h0, l0);
+      for (int j0 = 0; j0 < N; j0 += 64) {
+        tile(j0, chain(h0, l0, h1, l1));
+        if (j0 + 32 >= N) break;
+        tile(j0 + 32, chain(h1, l1, h0, l0));
+      }
+    } else {
+      auto chain = [&](const float (&b)[64], float (&bn)[64]) {
+        return [&](int j) {
+          load_b_tile(dnf, j + 32, N, h, bn);
+          __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
+          f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int s = 0; s < 64; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+          return acc;
+        };
+      };
+      float b0[64], b1[64];
+      load_b_tile(dnf, col, N, h, b0);
+      for (int j0 = 0; j0 < N; j0 += 64) {
+        tile(j0, chain(b0, b1));
+        if (j0 + 32 >= N) break;
+        tile(j0 + 32, chain(b1, b0));
+      }
     }
     if (w.prof) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -750,13 +847,24 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
       w.prof = g_cost_prof.get() ? g_cost_prof.get() + f0 * ((Mmax + 3) / 4) * 16 : nullptr;
       w.dn += f0 * Nmax * D;
       w.dt += f0 * Nmax;
-      hipLaunchKernelGGL(det_prep_kernel, dim3((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf), dim3(256), 0, st, a, w);
-      if (int e = trk::check_launch("det_prep_kernel")) return e;
-      const unsigned c3x = (unsigned)std::min<int64_t>((Mmax + 3) / 4, kCost3Rows / 4);
-      if (host_params->topk <= 5)
-        hipLaunchKernelGGL(cost3_kernel<5>, dim3(c3x, (unsigned)nf), dim3(256), 0, st, a, w);
+      const dim3 pgrid((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf);
+      if (g_cost_split)
+        hipLaunchKernelGGL(det_prep_kernel<true>, pgrid, dim3(256), 0, st, a, w);
       else
-        hipLaunchKernelGGL(cost3_kernel<kMaxTopk>, dim3(c3x, (unsigned)nf), dim3(256), 0, st, a, w);
+        hipLaunchKernelGGL(det_prep_kernel<false>, pgrid, dim3(256), 0, st, a, w);
+      if (int e = trk::check_launch("det_prep_kernel")) return e;
+      const dim3 cgrid((unsigned)std::min<int64_t>((Mmax + 3) / 4, kCost3Rows / 4), (unsigned)nf);
+      if (host_params->topk <= 5) {
+        if (g_cost_split)
+          hipLaunchKernelGGL((cost3_kernel<5, true>), cgrid, dim3(256), 0, st, a, w);
+        else
+          hipLaunchKernelGGL((cost3_kernel<5, false>), cgrid, dim3(256), 0, st, a, w);
+      } else {
+        if (g_cost_split)
+          hipLaunchKernelGGL((cost3_kernel<kMaxTopk, true>), cgrid, dim3(256), 0, st, a, w);
+        else
+          hipLaunchKernelGGL((cost3_kernel<kMaxTopk, false>), cgrid, dim3(256), 0, st, a, w);
+      }
       if (int e = trk::check_launch("cost3_kernel")) return e;
       continue;
     }

@@ -61,6 +61,10 @@ const char* trk_last_error(void);
  *   "cost_v2"        0 (default): the bank-in-registers cost3 kernel where a workspace is
  *                    given (the device tracker), else the detection-tile kernel; 1: the
  *                    LDS bank-resident cost2 kernel (all bit-identical)
+ *   "cost_split"     1 (default): cost3 (trk_build_cost_dev with a workspace) computes the
+ *                    bank x detection similarities from f16 hi / lo splits on the f16 MFMA
+ *                    (NOT bit-identical: within 1.1e-6 of the exact f32 products for unit
+ *                    rows); 0: exact f32 MFMA, bit-identical to the detection-tile kernel
  *   "lsap_dev_lds_kb" LDS budget of trk_lsap_dev workgroups (default 24: they fit beside the
  *                    encoder's workgroups instead of waiting for a whole CU) */
 int trk_set_tuning(const char* key, int value);

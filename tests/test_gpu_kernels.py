@@ -290,15 +290,38 @@ def _run_cost(trk, gpu, bank, blen, pbox, lconf, gm, gs, det, dbox, dconf, gate=
                          gate_on=t(np.ones(M, np.int32), torch.int32),
                          want=("C_total", "C_app", "C_center", "C_scale", "C_conf"))
     res = {k: v[0].cpu().numpy() for k, v in out.items()}
-    # C_total / C_app only: the bank-resident kernel (det_prep + cost3), bit-identical
-    out3 = trk.build_cost(M=[M], N=[N], bank=t(_renorm(bank)), bank_len=t(blen, torch.int32), pbox=t(pbox),
-                          conf_prev=t(lconf), det_emb=t(det[None]), dbox=t(dbox[None]),
-                          conf_cur=t(dconf[None]), params=trk.default_cost_params(gate=gate),
-                          gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
-                          gate_on=t(np.ones(M, np.int32), torch.int32), want=("C_total", "C_app"))
-    for k in ("C_total", "C_app"):
-        assert np.array_equal(out3[k][0].cpu().numpy(), res[k], equal_nan=True), k
+    # C_total / C_app only: the bank-resident kernel (det_prep + cost3).  Exact f32 products
+    # (cost_split 0): bit-identical; the default f16 hi / lo split: within SPLIT_TOL, gate
+    # decisions equal
+    L = trk.lib()
+    for split in (0, 1):
+        assert L.trk_set_tuning(b"cost_split", split) == 0
+        try:
+            out3 = trk.build_cost(M=[M], N=[N], bank=t(_renorm(bank)), bank_len=t(blen, torch.int32), pbox=t(pbox),
+                                  conf_prev=t(lconf), det_emb=t(det[None]), dbox=t(dbox[None]),
+                                  conf_cur=t(dconf[None]), params=trk.default_cost_params(gate=gate),
+                                  gmean=t(gm, torch.float64), gsinv=t(gs, torch.float64),
+                                  gate_on=t(np.ones(M, np.int32), torch.int32), want=("C_total", "C_app"))
+        finally:
+            L.trk_set_tuning(b"cost_split", 1)
+        for k in ("C_total", "C_app"):
+            got3 = out3[k][0].cpu().numpy()
+            if split == 0:
+                assert np.array_equal(got3, res[k], equal_nan=True), k
+            else:
+                assert np.array_equal(np.isnan(got3), np.isnan(res[k])), k
+                assert np.array_equal(got3 >= 1e9, res[k] >= 1e9), k
+                ok = ~np.isnan(got3)
+                assert np.max(np.abs(got3[ok] - res[k][ok]), initial=0.0) <= SPLIT_TOL, k
+        res["split_" + "C_total"], res["split_C_app"] = out3["C_total"][0].cpu().numpy(), out3["C_app"][0].cpu().numpy()
     return res
+
+
+# cost_split (the default cost3 path): the similarity of two unit rows from f16 hi / lo splits is
+# within 1.1e-6 of the exact f32 products (cost.hip split16: the dropped lo*lo term, lo's two f16
+# roundings and its subnormal floor); C_app = 1 - mean of top-k similarities moves by no more, and
+# C_total by w_app (0.6) times that
+SPLIT_TOL = 1.1e-6
 
 
 @pytest.mark.parametrize("name", ["s16", "s64", "reid"])
@@ -357,7 +380,12 @@ def test_cost_kernel_full_size_vs_oracle(trk, oracle, gpu):
     finally:
         assert L.trk_set_tuning(b"cost_v2", 0) == 0
     for k in got:
-        assert np.array_equal(got[k], got1[k]), k
+        if not k.startswith("split_"):
+            assert np.array_equal(got[k], got1[k]), k
+    # the default (split) cost3 outputs against the oracle, as the exact ones above
+    assert np.max(np.abs(got["split_C_app"] - exp["C_app"])) <= 2e-6
+    assert np.array_equal(got["split_C_total"] >= 1e9, exp["C_total"] >= 1e9)
+    assert np.max(np.abs(got["split_C_total"] - exp["C_total"])) <= 2e-6
 
 
 def test_cost_batched_frames_with_row_slots(trk, oracle, gpu):
@@ -431,9 +459,16 @@ def test_cost_dev_bank_resident_vs_det_tile(trk, oracle, gpu):
         return Ct.cpu().numpy(), Ca.cpu().numpy()
 
     work = torch.empty(int(L.trk_cost_work_bytes(F, Nmax)), device=gpu, dtype=torch.uint8)
-    Ct3, Ca3 = run(work)
     Ct1, Ca1 = run(None)
-    assert np.array_equal(Ct3, Ct1) and np.array_equal(Ca3, Ca1)
+    assert L.trk_set_tuning(b"cost_split", 0) == 0
+    try:
+        Ct3e, Ca3e = run(work)
+    finally:
+        L.trk_set_tuning(b"cost_split", 1)
+    assert np.array_equal(Ct3e, Ct1) and np.array_equal(Ca3e, Ca1)  # exact f32 products: bit-identical
+    Ct3, Ca3 = run(work)  # the default f16 split
+    assert np.array_equal(Ct3 >= 1e9, Ct1 >= 1e9)
+    assert np.max(np.abs(Ca3 - Ca1)) <= SPLIT_TOL and np.max(np.abs(Ct3 - Ct1)) <= SPLIT_TOL
     for f in range(F):
         M, N = int(Ms[f]), int(Ns[f])
         assert (Ct3[f, M:] == -7.0).all() and (Ct3[f, :, N:] == -7.0).all()  # nothing written outside M x N

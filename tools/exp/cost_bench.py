@@ -36,23 +36,25 @@ def run(w, pr=prm):
     assert L.trk_build_cost_dev(F, M, N, P(Ms), P(Ns), P(slots), M, T, P(bank), P(blen), P(pbox), P(lconf), P(gm),
                                 P(gs), P(gon), P(det), P(dbox), P(dconf), ctypes.byref(pr), P(C), None,
                                 P(w) if w is not None else None, ops._stream(dev)) == 0
-for name, w, pr in (("cost_kernel", None, prm), ("cost3", work, prm), ("cost3_topk8", work, prm8)) * 2:
-    run_ = lambda w: run(w, pr)
-    for _ in range(3): run_(w)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(20): run_(w)
-    e1.record(); torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / 20 * 1e3
-    flop = 2.0 * F * M * N * 32 * 128
-    print(json.dumps({"kernel": name, "us": round(us, 2), "f32_mfma_TFs": round(flop / us / 1e6, 1)}), flush=True)
-
-prof = torch.zeros(F * ((M + 3) // 4) * 16, dtype=torch.int64, device=dev)
-L.trk_cost_set_prof(P(prof))
-run(work); torch.cuda.synchronize()
-L.trk_cost_set_prof(None)
-pr = prof.view(-1, 4).double().cpu()
-print(json.dumps({"prof_ticks_mean": {"bank": round(pr[:, 1].mean().item()), "chain_topk": round(pr[:, 2].mean().item()),
-                                      "epilogue": round(pr[:, 3].mean().item())},
-                  "tiles": (N + 31) // 32}), flush=True)
+for split in (0, 1):
+    L.trk_set_tuning(b"cost_split", split)
+    for name, w, pr in (("cost_kernel", None, prm), ("cost3", work, prm), ("cost3_topk8", work, prm8)):
+        run_ = lambda w: run(w, pr)
+        for _ in range(3): run_(w)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20): run_(w)
+        e1.record(); torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1e3
+        print(json.dumps({"split": split, "kernel": name, "us": round(us, 2)}), flush=True)
+    prof = torch.zeros(F * ((M + 3) // 4) * 16, dtype=torch.int64, device=dev)
+    L.trk_cost_set_prof(P(prof))
+    run(work); torch.cuda.synchronize()
+    L.trk_cost_set_prof(None)
+    pr = prof.view(-1, 4).double().cpu()
+    print(json.dumps({"split": split, "prof_ticks_mean": {"bank": round(pr[:, 1].mean().item()),
+                                                          "chain_topk": round(pr[:, 2].mean().item()),
+                                                          "epilogue": round(pr[:, 3].mean().item())},
+                      "tiles": (N + 31) // 32}), flush=True)
+L.trk_set_tuning(b"cost_split", 1)
