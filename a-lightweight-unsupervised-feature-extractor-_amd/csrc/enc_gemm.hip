@@ -23,6 +23,7 @@ trk::DiagBuf g_enc_prof;  // trk_enc_set_prof (diagnostics: per-workgroup phase 
 int g_rf3_groups = 0;  // trk_set_tuning("rf3_groups"): rmb_front3 workgroup pairs per XCD (0 = CUs / 16 - 2)
 int g_rf3_chunks = 1;  // trk_set_tuning("rf3_chunks"): rmb_front3 generations (each pair's ROIs in that many
                        // chunks, one workgroup each; 1 = one persistent generation)
+int g_rf_pf = 1;  // trk_set_tuning("rf_pf"): rmb_front3 reads each K step's first X / Y fragment one step ahead
 int g_enc_trans = 1;  // trk_set_tuning("enc_trans"): 1 = trans4 (weights straight into VGPRs, needs the
                       // packed fragments: trk_enc_transition_gemm2; 247.6 vs 281.5 us isolated, pipeline
                       // 1.981/1.939/1.968M vs 1.894/1.881/1.911M ROIs/s interleaved), 0 = gemm4 (through LDS)
@@ -882,6 +883,68 @@ __device__ __forceinline__ void rf_mfma_step(uint32_t ab, const u32x4 (&b)[4], f
   }
 }
 
+// rf_mfma_step with the first fragment read one step ahead: PRE, tile 0's fragment is already in
+// `pre` (its ds_read issued during the previous step, possibly still in flight: it is older than
+// this step's six reads, so the tile-0 wait lgkmcnt(6) retires it); NEXT, the next step's tile-0
+// fragment (LDS byte address nab) is read into `pre` after tile 3's MFMAs, so the next step's
+// first MFMAs do not wait for an LDS read the partner wave may not cover (the read is younger
+// than tiles 4..6's: their waits count it).  The caller passes NEXT only where the next step's
+// block is already in LDS without a wait in between (not across an X group boundary or the
+// Y2(B) hand-off)
+template <bool PRE, bool NEXT>
+__device__ __forceinline__ void rf_mfma_step_pf(uint32_t ab, const u32x4 (&b)[4], f4v (&acc)[7][4], u32x4& pre,
+                                                uint32_t nab) {
+  u32x4 aq[7];
+  if constexpr (!PRE) asm volatile("ds_read_b128 %0, %1" : "=v"(aq[0]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(aq[1]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(aq[2]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(aq[3]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(aq[4]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:5120" : "=v"(aq[5]) : "v"(ab) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(aq[6]) : "v"(ab) : "memory");
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (i == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+    else if (i == 1) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
+    else if (i == 2) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    else if (i == 3) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+    else if (i == 4) {
+      if constexpr (NEXT) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+    } else if (i == 5) {
+      if constexpr (NEXT) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+    } else {
+      if constexpr (NEXT) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const bf8v xf = __builtin_bit_cast(bf8v, (PRE && i == 0) ? pre : aq[i]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, b[t]), xf, acc[i][t], 0, 0, 0);
+    if constexpr (NEXT) {
+      if (i == 3) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(pre) : "v"(nab) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+}
+// one K step with the prefetch flags as compile-time constants of the unrolled loops
+__device__ __forceinline__ void rf_step_pf(bool pre_in, bool next, uint32_t ab, const u32x4 (&b)[4],
+                                           f4v (&acc)[7][4], u32x4& pre, uint32_t nab) {
+  if (pre_in) {
+    if (next) rf_mfma_step_pf<true, true>(ab, b, acc, pre, nab);
+    else rf_mfma_step_pf<true, false>(ab, b, acc, pre, nab);
+  } else {
+    if (next) rf_mfma_step_pf<false, true>(ab, b, acc, pre, nab);
+    else rf_mfma_step_pf<false, false>(ab, b, acc, pre, nab);
+  }
+}
+
 // Decoupled halves: half A (waves 0..3, one per SIMD) produces Y1 / Y2 channels 0..255 and
 // half B (waves 4..7) channels 256..511; the depthwise of a half only reads its own half's Y1,
 // so the only cross-half dependencies are GEMM2's K steps 8..15 (Y2(B)) and the LDS regions
@@ -995,7 +1058,7 @@ __device__ __forceinline__ float rf_mean(float sum) {
 // The workgroup's ROIs roi0, roi0 + stride, ...: ROI it + 1's X DMA and GEMM1 start as soon as
 // the blocks they need are free, so half A's GEMM1 of the next ROI runs under half B's epilogue
 // of this one instead of behind a workgroup boundary
-template <int G>
+template <int G, bool PF>
 __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, int64_t roi0, int64_t stride,
                                          int64_t roi_end) {
   uint32_t* Y = reinterpret_cast<uint32_t*>(smem);
@@ -1055,6 +1118,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
   for (int i = 0; i < 7; ++i)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+  u32x4 apre = {0u, 0u, 0u, 0u};  // PF: the next K step's tile-0 fragment (rf_mfma_step_pf)
 
   // ---- GEMM1 (K = 512 over X blocks 0..15); A: 8 DMA ops per group, B: none.  One
   // loop per half (HALF a template constant): a half test inside the unrolled loop costs
@@ -1080,7 +1144,10 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
         // group boundary: vmcnt(0) (an LDS-DMA may retire after younger VGPR loads), count
         // this wave's share of the group, wait for the other three
         if (kt % 4 == 0) {
-          rf_vmwait(0, b);
+          // PF: LDS-DMA and loads retire in issue order (MI355X_MICROARCH.md, s_waitcnt vmcnt), so
+          // vmcnt(4) retires this group's DMA (issued before B(kt)) and leaves B(kt + 1) in flight;
+          // else vmcnt(0)
+          rf_vmwait(PF ? 4 : 0, b);
           rf2_signal(ctr + RF2_CX + kt / 4, lane);
           rf2_wait(ctr + RF2_CX + kt / 4, t4);
           if (kt == 4) {
@@ -1099,7 +1166,10 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
         if (kt % 4 == 0) rf2_wait(ctr + RF2_CX + kt / 4, t4);
       }
       if (kt + 2 < NK) rf_loadB(b1p, kt + 2, bq[(kt + 2) % 3]);
-      rf_mfma_step(y_a + kt * RF_KBS * 4, b, acc);
+      // PF: the next step's first fragment read ahead, except into a group's first step (its
+      // block is waited for there)
+      rf_step_pf(PF && kt % 4 != 0, PF && kt + 1 < NK && (kt + 1) % 4 != 0, y_a + kt * RF_KBS * 4, b, acc, apre,
+                 y_a + (kt + 1) * RF_KBS * 4);
     }
   };
   __builtin_amdgcn_s_setprio(1);
@@ -1215,7 +1285,9 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
       for (int t = 0; t < 4; ++t)
         bias4[t] = *reinterpret_cast<const float4*>(a.bias + G * 512 + wave * 64 + t * 16 + fc * 4);
     }
-    rf_mfma_step(y_a + rf2_yblk(kt) * RF_KBS * 4, b, acc);
+    // PF: read ahead except into steps 0 and 8 (waits for the halves' Y2)
+    rf_step_pf(PF && kt != 0 && kt != 8, PF && kt + 1 < NK && kt + 1 != 8, y_a + rf2_yblk(kt) * RF_KBS * 4, b, acc,
+               apre, y_a + rf2_yblk(kt + 1 < NK ? kt + 1 : kt) * RF_KBS * 4);
   }
   __builtin_amdgcn_s_setprio(0);
   asm volatile("" ::"v"(xpf0), "v"(xpf1));  // (retired by GEMM2's last wait)
@@ -1316,6 +1388,7 @@ __device__ __forceinline__ void rf2_body(const RfArgs& a, unsigned char* smem, i
 // the pair's k range -- both groups of a ROI on one XCD, every ROI once.  C = 1: one persistent
 // generation; C > 1: workgroups retire between chunks, so kernels of other streams (the tracker's,
 // at a higher priority) are dispatched there instead of waiting for the whole launch
+template <bool PF>
 __global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t per = 16 * (int64_t)a.pairs;
@@ -1330,8 +1403,8 @@ __global__ void __launch_bounds__(512, 1) rmb_front3_kernel(RfArgs a) {
   const int64_t k0 = c * kc, k1 = min(nk, k0 + kc);
   if (k0 >= k1) return;
   const int64_t roi0 = xcd + 8 * p + stride * k0, roi_end = xcd + 8 * p + stride * (k1 - 1) + 1;
-  if (slot & 1) rf2_body<1>(a, smem, roi0, stride, roi_end);
-  else rf2_body<0>(a, smem, roi0, stride, roi_end);
+  if (slot & 1) rf2_body<1, PF>(a, smem, roi0, stride, roi_end);
+  else rf2_body<0, PF>(a, smem, roi0, stride, roi_end);
 }
 
 
@@ -1766,7 +1839,9 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16) ncu = 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rmb_front3_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)RF2_LDS);
     attr = true;
   }
@@ -1794,8 +1869,12 @@ extern "C" int trk_enc_rmb_front_means(const void* X, int64_t M, const void* W1p
   const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(g_rf3_chunks, per_pair));
   a.pairs = (int)groups;
   a.chunks = (int)chunks;
-  hipLaunchKernelGGL(rmb_front3_kernel, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
-                     reinterpret_cast<hipStream_t>(stream), a);
+  if (g_rf_pf)
+    hipLaunchKernelGGL(rmb_front3_kernel<true>, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
+                       reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(rmb_front3_kernel<false>, dim3((unsigned)(16 * groups * chunks)), dim3(512), RF2_LDS,
+                       reinterpret_cast<hipStream_t>(stream), a);
   return trk::check_launch("rmb_front3_kernel");
 }
 

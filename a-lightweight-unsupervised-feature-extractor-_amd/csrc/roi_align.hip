@@ -941,6 +941,7 @@ extern "C" int trk_set_tuning(const char* key, int value) {
   if (!strcmp(key, "roi_fma")) { TRK_REQUIRE(value == 0 || value == 1, "roi_fma in {0, 1}"); g_roi_fma = value; return TRK_OK; }
   if (!strcmp(key, "roi_wlds")) { TRK_REQUIRE(value == 0 || value == 1, "roi_wlds in {0, 1}"); g_roi_wlds = value; return TRK_OK; }
   if (!strcmp(key, "cost_v2")) { extern int g_cost_v2; TRK_REQUIRE(value == 0 || value == 1, "cost_v2 in {0, 1}"); g_cost_v2 = value; return TRK_OK; }
+  if (!strcmp(key, "rf_pf")) { extern int g_rf_pf; TRK_REQUIRE(value == 0 || value == 1, "rf_pf in {0, 1}"); g_rf_pf = value; return TRK_OK; }
   if (!strcmp(key, "cost_split")) { extern int g_cost_split; TRK_REQUIRE(value == 0 || value == 1, "cost_split in {0, 1}"); g_cost_split = value; return TRK_OK; }
   if (!strcmp(key, "enc_trans")) { extern int g_enc_trans; TRK_REQUIRE(value == 0 || value == 1, "enc_trans in {0, 1}"); g_enc_trans = value; return TRK_OK; }
   if (!strcmp(key, "rf3_chunks")) { extern int g_rf3_chunks; TRK_REQUIRE(value >= 1 && value <= 64, "rf3_chunks in 1..64"); g_rf3_chunks = value; return TRK_OK; }

@@ -107,7 +107,7 @@ def test_rmb_kernels_wait_before_using_asm_loads(tmp_path):
         assert not bad, (name, bad[:5])
         bad = IC.scan_lds(body)
         assert not bad, (name, bad[:5])
-    assert found == 2  # rmb_front3 + trans4
+    assert found == 3  # rmb_front3 (with and without the fragment read-ahead) + trans4
     # no VGPR spills in the two register-bound kernels (the faulting r05 variant spilled 14)
     text = "\n".join(lines)
     for k in ("rmb_front3_kernel", "trans4_kernel"):
