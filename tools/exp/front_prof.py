@@ -22,7 +22,7 @@ buf = torch.zeros(2 * R * 8 * 8, dtype=torch.int64, device=dev)
 names = ["gemm1", "y1_store", "depthwise", "gemm2", "act_sums", "staging", "stores", "total"]
 
 
-DEFAULTS = {"rf3_chunks": 1, "enc_trans": 1, "rf_pf": 1, "cost_split": 1}  # knobs whose default is not 0
+DEFAULTS = {"rf3_chunks": 1, "enc_trans": 1, "rf_pf": 1, "cost_split": 1, "rf_front": 3}  # knobs whose default is not 0
 
 
 def apply(v, reset=False):
