@@ -15,6 +15,9 @@ bt = torch.randn(512, device=dev, generator=g) / 4
 Wtp = ops.enc_pack_fragments_k(Wt)
 L = ops.lib()
 L.trk_enc_set_prof.argtypes = [ctypes.c_void_p]
+for kv in sys.argv[1:]:  # tuning knobs k=v
+    k, v = kv.split("=")
+    assert L.trk_set_tuning(k.encode(), int(v)) == 0
 nwg = (R * P + 127) // 128 * 2
 buf = torch.zeros(nwg * 8, dtype=torch.int64, device=dev)
 for _ in range(3):
@@ -24,5 +27,11 @@ ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
 torch.cuda.synchronize()
 L.trk_enc_set_prof(None)
 med = buf.view(nwg, 8)[:, :5].double().cpu().median(0).values.tolist()
-print(json.dumps({"k_loop": round(med[0]), "silu": round(med[1]), "sums": round(med[2]), "store": round(med[3]),
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+ev[0].record()
+for _ in range(10):
+    ops.enc_transition_gemm(XRN, P, s, Wt, bt, Wtp=Wtp)
+ev[1].record()
+torch.cuda.synchronize()
+print(json.dumps({"args": sys.argv[1:], "us": round(ev[0].elapsed_time(ev[1]) * 100, 1), "k_loop": round(med[0]), "silu": round(med[1]), "sums": round(med[2]), "store": round(med[3]),
                   "total": round(med[4])}), flush=True)
