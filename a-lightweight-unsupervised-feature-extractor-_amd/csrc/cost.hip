@@ -99,6 +99,56 @@ __device__ __forceinline__ void topk_insert_k(float (&v)[kMaxTopk], float x) {
   }
 }
 
+// topk_insert on a list of any compile-time length
+template <int K>
+__device__ __forceinline__ void topk_insert_n(float (&v)[K], float x) {
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    float hi = fmaxf(v[q], x);
+    x = fminf(v[q], x);
+    v[q] = hi;
+  }
+}
+// compare-exchange: a = max, b = min (descending order)
+__device__ __forceinline__ void topk_ce(float& a, float& b) {
+  const float hi = fmaxf(a, b);
+  b = fminf(a, b);
+  a = hi;
+}
+// 5-input sorting network (9 compare-exchanges), descending
+__device__ __forceinline__ void sort5_desc(float (&c)[5]) {
+  topk_ce(c[0], c[1]); topk_ce(c[3], c[4]); topk_ce(c[2], c[4]);
+  topk_ce(c[2], c[3]); topk_ce(c[0], c[3]); topk_ce(c[0], c[2]);
+  topk_ce(c[1], c[4]); topk_ce(c[1], c[3]); topk_ce(c[1], c[2]);
+}
+// the top 5 of the union of two descending 5-lists, descending: max(a_i, b_{4-i}) is that set
+// (a bitonic sequence), then sorted
+__device__ __forceinline__ void top5_merge(const float (&a)[5], const float (&b)[5], float (&o)[5]) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) o[i] = fmaxf(a[i], b[4 - i]);
+  sort5_desc(o);
+}
+// the top 5 of 16 values, descending: four sorted quads, two Batcher odd-even merges (4 + 4, the
+// compare-exchange that only orders slots 5 and 6 dropped), the two top-5 lists merged.  95 max /
+// min against 16 insertions' 160; the same multiset in the same order as the insertion network, so
+// every top-k sum is bit-identical to it (tools: a 0/1 exhaustive check of the network)
+__device__ __forceinline__ void top5_of16(float (&x)[16], float (&o)[5]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float* q = x + 4 * g;
+    topk_ce(q[0], q[1]); topk_ce(q[2], q[3]); topk_ce(q[0], q[2]); topk_ce(q[1], q[3]); topk_ce(q[1], q[2]);
+  }
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    float* v = x + 8 * hh;
+    topk_ce(v[0], v[4]); topk_ce(v[1], v[5]); topk_ce(v[2], v[6]); topk_ce(v[3], v[7]);
+    topk_ce(v[2], v[4]); topk_ce(v[3], v[5]);
+    topk_ce(v[1], v[2]); topk_ce(v[3], v[4]);
+  }
+  const float p[5] = {x[0], x[1], x[2], x[3], x[4]}, q[5] = {x[8], x[9], x[10], x[11], x[12]};
+  top5_merge(p, q, o);
+}
+
 // torch's clamp(min=lo): a NaN stays NaN (fmaxf would return lo), so a NaN box or
 // confidence reaches C_total and the solver raises as scipy does
 __device__ __forceinline__ float clamp_lo(float x, float lo) { return x < lo ? lo : x; }
@@ -438,16 +488,26 @@ __device__ __forceinline__ unsigned long long c3_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
+// detection rows padded to whole 32-detection tiles per frame
+__host__ __device__ inline int64_t cost3_np(int64_t Nmax) { return (Nmax + 31) / 32 * 32; }
 inline Cost3Work cost3_work(void* work, int64_t F, int64_t Nmax) {
   Cost3Work w;
   w.dn = reinterpret_cast<float*>(work);
-  w.dt = reinterpret_cast<DetTerms*>(reinterpret_cast<unsigned char*>(work) + (size_t)F * Nmax * D * 4);
+  w.dt = reinterpret_cast<DetTerms*>(reinterpret_cast<unsigned char*>(work) + (size_t)F * cost3_np(Nmax) * D * 4);
   w.prof = nullptr;
   return w;
 }
 
-// SPLIT: the renormalised rows as f16 hi / lo pairs (split16), [Nmax][2][128] f16 in the same 512 B
-// per detection: hi row, then lo row
+// The renormalised rows in MFMA fragment order: per frame, per 32-detection tile, 16 chunks of
+// 1 KiB, chunk q = [lane 0..63][16 B] with lane = 32 h + (j & 31) (the B-operand lane of
+// detection j's column, K half h).  Chunk q of the f32 rows holds elements 64 h + 4 q .. + 3;
+// with SPLIT (f16 hi / lo pairs, split16) chunk 2 st holds the hi and chunk 2 st + 1 the lo of
+// elements 64 h + 8 st .. + 7.  So each of a wave's 16 fragment loads per tile is one
+// contiguous 1 KiB (the row-major image had every lane of a load on its own 512-B row: 64
+// cache lines per load instruction, which bound cost3 at the L1's line rate)
+__device__ __forceinline__ int64_t c3_chunk(int j, int q) {  // in floats, from the frame's base
+  return ((int64_t)(j >> 5) * 16 + q) * 256;
+}
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) det_prep_kernel(const CostArgs A, Cost3Work w) {
   const int f = blockIdx.y;
@@ -462,25 +522,25 @@ __global__ void __launch_bounds__(256) det_prep_kernel(const CostArgs A, Cost3Wo
   for (int s = 0; s < 64; ++s) ss += (double)b[s] * (double)b[s];
   ss += __shfl_xor(ss, 1);
   const float nrm = (float)sqrt(ss) + 1e-12f;
-  float* o = w.dn + ((int64_t)f * A.Nmax + j) * D + 64 * h;
+  float* o = w.dn + (int64_t)f * cost3_np(A.Nmax) * D + (32 * h + (j & 31)) * 4;
   if (SPLIT) {
-    _Float16* oh = reinterpret_cast<_Float16*>(w.dn + ((int64_t)f * A.Nmax + j) * D) + 64 * h;
 #pragma unroll
-    for (int s = 0; s < 64; s += 8) {
+    for (int st = 0; st < 8; ++st) {
       h8v hi, lo;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const Split16 v = split16(b[s + e] / nrm);
+        const Split16 v = split16(b[8 * st + e] / nrm);
         hi[e] = v.hi;
         lo[e] = v.lo;
       }
-      *reinterpret_cast<h8v*>(oh + s) = hi;
-      *reinterpret_cast<h8v*>(oh + 128 + s) = lo;
+      *reinterpret_cast<h8v*>(o + c3_chunk(j, 2 * st)) = hi;
+      *reinterpret_cast<h8v*>(o + c3_chunk(j, 2 * st + 1)) = lo;
     }
   } else {
 #pragma unroll
-    for (int s = 0; s < 64; s += 4)
-      *reinterpret_cast<float4*>(o + s) = make_float4(b[s] / nrm, b[s + 1] / nrm, b[s + 2] / nrm, b[s + 3] / nrm);
+    for (int q = 0; q < 16; ++q)
+      *reinterpret_cast<float4*>(o + c3_chunk(j, q)) =
+          make_float4(b[4 * q] / nrm, b[4 * q + 1] / nrm, b[4 * q + 2] / nrm, b[4 * q + 3] / nrm);
   }
   if (h == 0) {
     DetTerms t;
@@ -490,26 +550,36 @@ __global__ void __launch_bounds__(256) det_prep_kernel(const CostArgs A, Cost3Wo
   }
 }
 
-// B fragment of detection row j (columns past N read row N - 1: their sims are
-// never stored, and an unconditional load keeps the compiler's vmcnt counting exact
-// so the next tile's loads stay in flight across the current MFMA chain)
-__device__ __forceinline__ void load_b_tile(const float* dnf, int j, int N, int h, float (&b)[64]) {
-  const float* p = dnf + (int64_t)min(j, N - 1) * D + 64 * h;
+// B fragments of the 32-detection tile holding detection j, for this lane (fragment order above;
+// a tile past the frame's last reads the last: the sims of columns past N are never stored, and an
+// unconditional load keeps the compiler's vmcnt counting exact so the next tile's loads stay in
+// flight across the current MFMA chain; columns past N in the last tile read rows det_prep did not
+// write, for the same unstored sims)
+// (tile: wave-uniform, so the tile base is a scalar address and the lane's offset one VGPR)
+// (buffer loads on the frame's fragment image: the tile's and 4-KiB group's offset a scalar, the
+// lane's byte offset one VGPR plus an immediate -- with plain pointers the compiler kept a 64-bit
+// address per load live across the loop and spilled them)
+typedef unsigned c3u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ c3u4 c3_frag(__amdgpu_buffer_rsrc_t rs, int tile, int q, int loff) {
+  const int so = __builtin_amdgcn_readfirstlane(tile) * 16384 + (q >> 2) * 4096;
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, loff + (q & 3) * 1024, so, 0);
+}
+__device__ __forceinline__ void load_b_tile(__amdgpu_buffer_rsrc_t rs, int tile, int lane, float (&b)[64]) {
+  const int loff = lane * 16;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
+    const float4 v = __builtin_bit_cast(float4, c3_frag(rs, tile, q, loff));
     b[4 * q + 0] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
   }
 }
 
-// the f16 split B fragments of detection row j: lane half h, K step st holds elements
-// 64 h + 8 st .. + 7 (hi in bh, lo in bl; as load_b_tile, columns past N read row N - 1)
-__device__ __forceinline__ void load_b_split(const float* dnf, int j, int N, int h, h8v (&bh)[8], h8v (&bl)[8]) {
-  const _Float16* p = reinterpret_cast<const _Float16*>(dnf + (int64_t)min(j, N - 1) * D) + 64 * h;
+// the f16 split B fragments (lane half h, K step st: elements 64 h + 8 st .. + 7, hi in bh, lo in bl)
+__device__ __forceinline__ void load_b_split(__amdgpu_buffer_rsrc_t rs, int tile, int lane, h8v (&bh)[8], h8v (&bl)[8]) {
+  const int loff = lane * 16;
 #pragma unroll
   for (int st = 0; st < 8; ++st) {
-    bh[st] = *reinterpret_cast<const h8v*>(p + 8 * st);
-    bl[st] = *reinterpret_cast<const h8v*>(p + 128 + 8 * st);
+    bh[st] = __builtin_bit_cast(h8v, c3_frag(rs, tile, 2 * st, loff));
+    bl[st] = __builtin_bit_cast(h8v, c3_frag(rs, tile, 2 * st + 1, loff));
   }
 }
 
@@ -562,40 +632,87 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
   #pragma unroll
       for (int q = 0; q < 16; ++q) tS[q] = uni_d(A.gsinv[slot * 16 + q]);
     }
-    const float* dnf = w.dn + (int64_t)f * A.Nmax * D;
+    // the frame's fragment image as one buffer (descriptor inputs readfirstlane'd: uniform)
+    // (each half through uint32_t: readfirstlane returns int, whose sign extension would set the
+    // address's upper half to all ones when bit 31 of the lower is set)
+    const uint64_t da = reinterpret_cast<uint64_t>(w.dn + (int64_t)f * cost3_np(A.Nmax) * D);
+    const uint32_t da_lo = __builtin_amdgcn_readfirstlane((uint32_t)da);
+    const uint32_t da_hi = __builtin_amdgcn_readfirstlane((uint32_t)(da >> 32));
+    const __amdgpu_buffer_rsrc_t dnf = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)da_hi << 32) | (uint64_t)da_lo), 0,
+        __builtin_amdgcn_readfirstlane((int)(cost3_np(A.Nmax) * D * 4)), 0x00020000);
     const DetTerms* dtf = w.dt + (int64_t)f * A.Nmax;
     float* Ct = A.C_total ? A.C_total + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
     float* Ca = A.C_app ? A.C_app + ((int64_t)f * A.Mmax + i) * A.Nmax : nullptr;
-    // one 32-detection tile, straight-line: the tile's detection terms are loaded first,
-    // then the next tile's B fragments (into the other buffer), then the MFMA chain, so
-    // the epilogue's wait for the terms leaves the prefetch in flight.  `sims` runs the
-    // chain and leaves the 32 x 32 similarities in the f32x16 accumulator layout
-    auto tile = [&](int j0, auto&& sims) {
-      const int j = j0 + col;
-      const DetTerms t = dtf[min(j, N - 1)];
-      const f32x16 acc = sims(j);
-      float tk[kMaxTopk];
+    // two 32-detection tiles (A = j0.., B = j0 + 32..): each lane reduces its 16 bank rows of both
+    // to partial top-k lists, then lane half h finishes tile h's column (the halves swap the
+    // partial list the other one needs), so the merge, the epilogue and the stores run once per
+    // column instead of once per lane half.  `sims` runs the MFMA chain of one tile (prefetching
+    // the next tile's B fragments) and leaves the 32 x 32 similarities in the f32x16 layout
+    auto pair = [&](int j0, auto&& simsA, auto&& simsB, bool hasB) {
+      const int j = j0 + 32 * h + col;
+      float tk[2][KT];
+      unsigned long long nanb[2];
+      auto partial = [&](const f32x16& acc, float (&o)[KT]) {
+        bool nan = false;
+        float x[16];
   #pragma unroll
-      for (int q = 0; q < kMaxTopk; ++q) tk[q] = -INFINITY;
-      bool nan = false;
+        for (int r = 0; r < 16; ++r) {
+          const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
+          x[r] = tr < T ? acc[r] : -INFINITY;
+          nan |= __builtin_isnan(x[r]);
+        }
+        if constexpr (KT == 5) {
+          float o5[5];
+          top5_of16(x, o5);
   #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int tr = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float x = tr < T ? acc[r] : -INFINITY;
-        nan |= __builtin_isnan(x);
-        topk_insert_k<KT>(tk, x);
+          for (int q = 0; q < 5; ++q) o[q] = o5[q];
+        } else {
+  #pragma unroll
+          for (int q = 0; q < KT; ++q) o[q] = -INFINITY;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) topk_insert_n(o, x[r]);
+        }
+        return __ballot(nan);
+      };
+      nanb[0] = partial(simsA(j0), tk[0]);
+      // this lane's column's box / conf terms, loaded under tile B's chain (its gate terms after it:
+      // registers)
+      const DetTerms* tp = dtf + min(j, N - 1);
+      const float4 tf = *reinterpret_cast<const float4*>(tp);
+      if (hasB) {
+        nanb[1] = partial(simsB(j0 + 32), tk[1]);
+      } else {
+        nanb[1] = 0;
+  #pragma unroll
+        for (int q = 0; q < KT; ++q) tk[1][q] = -INFINITY;
       }
-      float other[KT];
+      const double4 tz = *reinterpret_cast<const double4*>(&tp->z0);
+      float mine[KT], other[KT], fin[KT];
   #pragma unroll
-      for (int q = 0; q < KT; ++q) other[q] = __shfl_xor(tk[q], 32);
+      for (int q = 0; q < KT; ++q) {
+        mine[q] = h ? tk[1][q] : tk[0][q];
+        other[q] = __shfl_xor(h ? tk[0][q] : tk[1][q], 32);
+      }
+      if constexpr (KT == 5) {
+        float o5[5];
+        top5_merge(mine, other, o5);
   #pragma unroll
-      for (int q = 0; q < KT; ++q) topk_insert_k<KT>(tk, other[q]);
+        for (int q = 0; q < 5; ++q) fin[q] = o5[q];
+      } else {
+  #pragma unroll
+        for (int q = 0; q < KT; ++q) fin[q] = mine[q];
+  #pragma unroll
+        for (int q = 0; q < KT; ++q) topk_insert_n(fin, other[q]);
+      }
       const int k = min(topk, T);
       float sum = 0.f;
   #pragma unroll
       for (int q = 0; q < KT; ++q)
-        if (q < k) sum = sum + tk[q];
-      const float app = app_nan(k <= 0 ? 1.0f : 1.0f - sum / (float)k, nan && k > 0, col);
+        if (q < k) sum = sum + fin[q];
+      const unsigned long long nb = h ? nanb[1] : nanb[0];
+      const bool nan = (((nb >> col) | (nb >> (col + 32))) & 1ull) && k > 0;
+      const float app = nan ? __builtin_nanf("") : (k <= 0 ? 1.0f : 1.0f - sum / (float)k);
       if (w.prof) {
         asm volatile("" ::"v"(app));
         const unsigned long long t1 = c3_stamp();
@@ -603,9 +720,9 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
         pt = t1;
       }
       float cen, scl, cf;
-      const float tot = combine(A.p, app, tb, tconf, t.ccx, t.ccy, t.Ac, t.ccv, gate, tg, tS, t.z0, t.z1, t.z2, t.z3,
+      const float tot = combine(A.p, app, tb, tconf, tf.x, tf.y, tf.z, tf.w, gate, tg, tS, tz.x, tz.y, tz.z, tz.w,
                                 cen, scl, cf);
-      if (h == 0 && j < N) {
+      if (j < N) {
         if (Ct) Ct[j] = tot;
         if (Ca) Ca[j] = app;
       }
@@ -621,8 +738,8 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
           al[st][e] = v.lo;
         }
       auto chain = [&](const h8v (&bh)[8], const h8v (&bl)[8], h8v (&nh)[8], h8v (&nl)[8]) {
-        return [&](int j) {
-          load_b_split(dnf, j + 32, N, h, nh, nl);
+        return [&](int jt) {  // jt: the tile's first detection (the next tile is prefetched)
+          load_b_split(dnf, min((jt >> 5) + 1, (N - 1) >> 5), lane, nh, nl);
           __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
           // one accumulator (a second one spilled the kernel): the 2^11-scaled cross terms
           // first, scaled back exactly, then the hi x hi products on top
@@ -640,16 +757,12 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
         };
       };
       h8v h0[8], l0[8], h1[8], l1[8];
-      load_b_split(dnf, col, N, h, h0, l0);
-      for (int j0 = 0; j0 < N; j0 += 64) {
-        tile(j0, chain(h0, l0, h1, l1));
-        if (j0 + 32 >= N) break;
-        tile(j0 + 32, chain(h1, l1, h0, l0));
-      }
+      load_b_split(dnf, 0, lane, h0, l0);
+      for (int j0 = 0; j0 < N; j0 += 64) pair(j0, chain(h0, l0, h1, l1), chain(h1, l1, h0, l0), j0 + 32 < N);
     } else {
       auto chain = [&](const float (&b)[64], float (&bn)[64]) {
-        return [&](int j) {
-          load_b_tile(dnf, j + 32, N, h, bn);
+        return [&](int jt) {
+          load_b_tile(dnf, min((jt >> 5) + 1, (N - 1) >> 5), lane, bn);
           __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the chain
           f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   #pragma unroll
@@ -658,12 +771,8 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
         };
       };
       float b0[64], b1[64];
-      load_b_tile(dnf, col, N, h, b0);
-      for (int j0 = 0; j0 < N; j0 += 64) {
-        tile(j0, chain(b0, b1));
-        if (j0 + 32 >= N) break;
-        tile(j0 + 32, chain(b1, b0));
-      }
+      load_b_tile(dnf, 0, lane, b0);
+      for (int j0 = 0; j0 < N; j0 += 64) pair(j0, chain(b0, b1), chain(b1, b0), j0 + 32 < N);
     }
     if (w.prof) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -802,7 +911,7 @@ extern "C" int trk_build_cost(int64_t F, int64_t Mmax, int64_t Nmax, const int32
 
 extern "C" int64_t trk_cost_work_bytes(int64_t F, int64_t Nmax) {
   if (F <= 0 || Nmax <= 0) return 0;
-  return F * Nmax * (int64_t)(D * 4 + sizeof(DetTerms));
+  return F * (cost3_np(Nmax) * D * 4 + Nmax * (int64_t)sizeof(DetTerms));
 }
 
 extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* dev_M, const int32_t* dev_N,
@@ -845,7 +954,7 @@ extern "C" int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const i
       // the workspace holds all F frames; this chunk's rows start at frame f0
       Cost3Work w = cost3_work(work, F, Nmax);
       w.prof = g_cost_prof.get() ? g_cost_prof.get() + f0 * ((Mmax + 3) / 4) * 16 : nullptr;
-      w.dn += f0 * Nmax * D;
+      w.dn += f0 * cost3_np(Nmax) * D;
       w.dt += f0 * Nmax;
       const dim3 pgrid((unsigned)((2 * Nmax + 255) / 256), (unsigned)nf);
       if (g_cost_split)

@@ -161,6 +161,31 @@ def test_no_mutable_device_pointer_globals_in_csrc():
     assert "(int32_t)(__builtin_amdgcn_readfirstlane(v) - target) >= 0" in src  # wrap-safe gate
 
 
+def test_buffer_descriptor_bases_zero_extend_their_halves():
+    """`__builtin_amdgcn_readfirstlane` returns int: an address half ORed or shifted straight from
+    it sign-extends, so a buffer descriptor built that way gets an upper address half of all ones
+    whenever bit 31 of the lower half is set (an illegal-address fault that depends on where the
+    allocator put the buffer; r06's cost3 fragment image hit it).  Every make_buffer_rsrc base
+    must be assembled from uint32_t variables, with no readfirstlane inside the call."""
+    import re
+    csrc = ROOT / "a-lightweight-unsupervised-feature-extractor-_amd" / "csrc"
+    calls = 0
+    for f in sorted(csrc.glob("*.hip")):
+        src = f.read_text()
+        start = 0
+        while (k := src.find("__builtin_amdgcn_make_buffer_rsrc(", start)) >= 0:
+            i, depth = k + len("__builtin_amdgcn_make_buffer_rsrc("), 1
+            while depth:
+                depth += {"(": 1, ")": -1}.get(src[i], 0)
+                i += 1
+            call = src[k:i]
+            first = re.split(r",\s*0\s*,", call[len("__builtin_amdgcn_make_buffer_rsrc("):])[0]
+            assert "readfirstlane" not in first, f"{f.name}: {call}"
+            calls += 1
+            start = i
+    assert calls >= 4
+
+
 def test_encoder_odd_sizes_forward_on_cpu(trk, oracle):
     """A Model whose SE hidden size (out_channels / 4 = 10) and proj_dim (24) are not
     multiples of 16 still runs forward (r05 advisor: the tail kernels' weight packing used to
