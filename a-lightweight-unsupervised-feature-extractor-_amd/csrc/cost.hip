@@ -687,7 +687,8 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
   #pragma unroll
         for (int q = 0; q < KT; ++q) tk[1][q] = -INFINITY;
       }
-      const double4 tz = *reinterpret_cast<const double4*>(&tp->z0);
+      const double2 tz01 = *reinterpret_cast<const double2*>(&tp->z0);  // (DetTerms: 16-B aligned halves)
+      const double2 tz23 = *reinterpret_cast<const double2*>(&tp->z2);
       float mine[KT], other[KT], fin[KT];
   #pragma unroll
       for (int q = 0; q < KT; ++q) {
@@ -720,7 +721,7 @@ __global__ void __launch_bounds__(256, 2) cost3_kernel(const CostArgs A, const C
         pt = t1;
       }
       float cen, scl, cf;
-      const float tot = combine(A.p, app, tb, tconf, tf.x, tf.y, tf.z, tf.w, gate, tg, tS, tz.x, tz.y, tz.z, tz.w,
+      const float tot = combine(A.p, app, tb, tconf, tf.x, tf.y, tf.z, tf.w, gate, tg, tS, tz01.x, tz01.y, tz23.x, tz23.y,
                                 cen, scl, cf);
       if (j < N) {
         if (Ct) Ct[j] = tot;

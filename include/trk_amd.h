@@ -413,8 +413,10 @@ int trk_step_apply(const trk_step_state* st, const trk_step_config* cfg, const f
  * bounds that size the launch (a larger device size is an error: status -4 for
  * the solver, rows past Mmax are not computed by the cost).  row_slot has row
  * stride rs_ld.  work: device scratch of trk_cost_work_bytes(F, Nmax) bytes, 16-B
- * aligned (the renormalised detections; the bank then is read once per launch
- * instead of once per 32-detection tile), or NULL. */
+ * aligned (the renormalised detections in MFMA fragment order, whole 32-detection
+ * tiles per frame, and their box / conf / KF terms; the bank then is read once per
+ * launch instead of once per 32-detection tile), or NULL.  Its contents are private
+ * to the call (only its size is part of the interface). */
 int64_t trk_cost_work_bytes(int64_t F, int64_t Nmax);
 int trk_build_cost_dev(int64_t F, int64_t Mmax, int64_t Nmax, const int32_t* dev_M, const int32_t* dev_N,
                        const int32_t* row_slot, int64_t rs_ld, int64_t Tmax, const float* bank,

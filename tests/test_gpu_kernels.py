@@ -627,6 +627,21 @@ def test_lsap_full_size_vs_oracle(trk, oracle, gpu):
         assert np.array_equal(r, er) and np.array_equal(c, ec), C.shape
 
 
+def test_lsap_widest_body_vs_oracle(trk, oracle, gpu):
+    """Matrices wider than 1024 columns run the 32-slot body (444 VGPRs per wave, the only
+    instantiation past 256): index-identical to the oracle, f32 and f64, wide and tall (the
+    solver transposes a tall matrix)."""
+    rng = np.random.default_rng(31)
+    for shape in ((300, 1500), (1100, 400)):
+        C = rng.random(shape)
+        er, ec = oracle.lsap(C)
+        for dt in (np.float32, np.float64):
+            Cd = C.astype(dt)
+            er2, ec2 = (er, ec) if dt == np.float64 else oracle.lsap(Cd)
+            r, c = trk.linear_sum_assignment(Cd)
+            assert np.array_equal(r, er2) and np.array_equal(c, ec2), (shape, dt)
+
+
 # ----------------------------------------------------------------- encoder
 @pytest.mark.parametrize("s", [7, 10])
 def test_encoder_gpu_vs_reference_golden(trk, gpu, s):
