@@ -425,6 +425,7 @@ def test_cost_dev_bank_resident_vs_det_tile(trk, oracle, gpu):
     rng = np.random.default_rng(23)
     F, Mmax, Nmax, S, T = 3, 40, 70, 200, 30
     bank = _renorm(rng.standard_normal((S, T, 128)))
+    bank[::7, 1:] = bank[::7, :1]  # ties: every row of these banks the same
     blen = rng.integers(0, 31, S).astype(np.int32)
     bank[np.arange(T)[None, :] >= blen[:, None]] = 0
     pbox = _boxes(rng, S)
@@ -459,6 +460,19 @@ def test_cost_dev_bank_resident_vs_det_tile(trk, oracle, gpu):
         return Ct.cpu().numpy(), Ca.cpu().numpy()
 
     work = torch.empty(int(L.trk_cost_work_bytes(F, Nmax)), device=gpu, dtype=torch.uint8)
+    # cost3's top-k: a sorting network for topk <= 5 (two tiles per step, lane halves swapping the
+    # partial lists), insertion for 6..8; both must give cost_kernel's sums bit for bit, with banks
+    # shorter than topk (blen 0..30) and exact ties (a few banks repeat one row)
+    for topk in (1, 3, 8):
+        params.topk = topk
+        Ct1, Ca1 = run(None)
+        assert L.trk_set_tuning(b"cost_split", 0) == 0
+        try:
+            Ct3e, Ca3e = run(work)
+        finally:
+            L.trk_set_tuning(b"cost_split", 1)
+        assert np.array_equal(Ct3e, Ct1) and np.array_equal(Ca3e, Ca1), topk
+    params.topk = 5
     Ct1, Ca1 = run(None)
     assert L.trk_set_tuning(b"cost_split", 0) == 0
     try:
