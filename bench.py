@@ -919,6 +919,10 @@ def main():
         else:
             per[k] = dict(bound="mfma", us=round(kt[k], 2), achieved=round(fl / t / 1e12, 2), peak=mpeak,
                           unit="TFLOP/s", frac=round(t_mfma / t, 4), work=fl)
+    if "cost" in per:
+        per["cost"]["note"] = ("the exact f32 similarity's flops priced at the f32 MFMA peak; the kernel computes "
+                               "them as three f16 MFMA products (cost_split 1, DESIGN 4.4), so this is the rate "
+                               "an f32 chain would have to reach, not the f16 pipe's load")
     per["encoder_stage"] = dict(bound="mfma", us=round(kt["encoder"], 2),
                                 achieved=round(K * ENC_FLOP_PER_ROI[S] / (kt["encoder"] * 1e-6) / 1e12, 2),
                                 peak=BF16_PEAK_TFLOPS, unit="TFLOP/s",
