@@ -59,6 +59,54 @@ def test_roi_align_bit_exact_vs_oracle(trk, oracle, gpu, N, S):
     assert torch.equal(bf.cpu(), torch.from_numpy(exp).bfloat16())
 
 
+@pytest.mark.parametrize("out", ["f32", "bf16_nhwc"])
+def test_roi_align_full_size_properties(trk, oracle, gpu, out):
+    """The bench's c3 launch ([8, 512, 40, 40] NCHW maps, 8 x 256 ROIs, 10 x 10 bins), where the
+    CPU oracle is too slow to run, checked through properties exact in the arithmetic of both the
+    exact f32 path and the default bf16 channels-last path (fused multiply-adds):
+      * homogeneity: 2 x map -> exactly 2 x output (every product and sum scales by a power of 2);
+      * channel equivariance: permuting the map's channels permutes the output's channels;
+      * frame independence: a ROI on frame b equals the same ROI on a batch whose frame 0 is b;
+      * integer translation: boxes moved by exactly one map cell (32 px at scale 1/32) on a map
+        moved by one cell give the same output, for ROIs clear of the map's edges whose corners
+        are multiples of 1/16 px and sizes of 10/16 px (so every sample coordinate is a short
+        dyadic number and moves by exactly 1.0);
+    and the 2,048 outputs against the oracle for 32 of them (all frames)."""
+    rng = np.random.default_rng(77)
+    B, N, C = 8, 256, 512
+    feat = torch.from_numpy(_feat(rng, B)).to(gpu)
+    boxes = np.stack([_boxes(rng, N) for _ in range(B)])
+    rois = np.concatenate([np.repeat(np.arange(B), N).astype(np.float32)[:, None], boxes.reshape(-1, 4)], 1)
+    r = torch.from_numpy(rois).to(gpu)
+    kw = dict(out_dtype=torch.bfloat16, channels_last=True) if out == "bf16_nhwc" else {}
+    ra = lambda f, rr: trk.roi_align(f, rr, (10, 10), 40 / 1280.0, 2, True, **kw).float()
+    base = ra(feat, r)
+    assert torch.isfinite(base).all()
+    assert torch.equal(ra(feat * 2, r), base * 2)
+    perm = torch.randperm(C, generator=torch.Generator().manual_seed(5)).to(gpu)
+    assert torch.equal(ra(feat[:, perm].contiguous(), r), base[:, perm])
+    sel = torch.arange(0, B * N, 61, device=gpu)  # ROIs of every frame
+    b_of = r[sel, 0].long()
+    r0 = r[sel].clone()
+    r0[:, 0] = 0
+    one = torch.stack([ra(feat[b:b + 1].contiguous(), r0[k:k + 1]) for k, b in enumerate(b_of.tolist())])
+    assert torch.equal(one.squeeze(1), base[sel])
+    # translation: boxes inside cells [2, 36] of the 40 x 40 map, moved by +1 cell in x and y
+    dy = lambda lo, hi, q: torch.from_numpy((np.round(rng.uniform(lo, hi, B * N) / q) * q).astype(np.float32)).to(gpu)
+    x1, y1 = dy(64, 1000, 1 / 16), dy(64, 1000, 1 / 16)
+    w, h = dy(32, 120, 10 / 16), dy(32, 120, 10 / 16)
+    rt = torch.stack([r[:, 0], x1, y1, x1 + w, y1 + h], 1)
+    rs = rt.clone()
+    rs[:, 1:] += 32.0
+    shifted = torch.zeros_like(feat)
+    shifted[:, :, 1:, 1:] = feat[:, :, :-1, :-1]
+    assert torch.equal(ra(shifted, rs), ra(feat, rt))
+    if out == "f32":
+        pick = sel[:32].cpu().numpy()
+        exp = oracle.roi_align(feat.cpu().numpy(), rois[pick], (10, 10), 40 / 1280.0, 2, True)
+        assert np.array_equal(base[sel[:32]].cpu().numpy(), exp)
+
+
 @pytest.mark.parametrize("shape", [(8, 512, 40, 40), (2, 36, 13, 12), (1, 70, 9, 7), (3, 4, 1, 4)])
 def test_nchw_to_nhwc_transpose(trk, gpu, shape):
     """The map transpose roi_align runs on NCHW input (float4 kernel when C and H*W are
