@@ -436,6 +436,62 @@ def test_cost_kernel_full_size_vs_oracle(trk, oracle, gpu):
     assert np.max(np.abs(got["split_C_total"] - exp["C_total"])) <= 2e-6
 
 
+def test_cost_dev_full_size_permutation_properties(trk, gpu):
+    """The bench's cost launch (8 frames x 256 tracks x 256 detections, T = 30, gate on, the
+    default f16-split cost3 through trk_build_cost_dev with a workspace), beyond the oracle's
+    one-frame check: permuting a frame's detections permutes its columns and permuting its row
+    slots permutes its rows, bit for bit (each (track, detection) entry is computed the same way
+    whichever tile and lane hold it), and the launch is deterministic."""
+    import ctypes
+    from importlib import import_module
+    ops = import_module(trk.__name__ + ".ops")
+    rng = np.random.default_rng(41)
+    F, M, N, T = 8, 256, 256, 30
+    S = F * M
+    bank = _renorm(rng.standard_normal((S, T, 128)))
+    blen = np.full(S, T, np.int32)
+    blen[::9] = rng.integers(0, T, len(blen[::9]))
+    bank[np.arange(T)[None, :] >= blen[:, None]] = 0
+    pbox = _boxes(rng, S)
+    lconf = rng.uniform(0.3, 1, S).astype(np.float32)
+    gm = np.concatenate([(pbox[:, :2] + pbox[:, 2:]) / 2, pbox[:, 2:] - pbox[:, :2]], 1).astype(np.float64)
+    gs = np.tile(np.eye(4).reshape(1, 16) * 1e-4, (S, 1))  # gated beyond ~300 px: both outcomes occur
+    det = rng.standard_normal((F, N, 128)).astype(np.float32)
+    dbox = np.stack([_boxes(rng, N) for _ in range(F)])
+    dconf = rng.uniform(0.3, 1, (F, N)).astype(np.float32)
+    slots = np.arange(S, dtype=np.int32).reshape(F, M)
+    t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(gpu, dt)
+    L = trk.lib()
+    params = trk.default_cost_params(gate=True)
+    P = ops._ptr
+    work = torch.empty(int(L.trk_cost_work_bytes(F, N)), device=gpu, dtype=torch.uint8)
+    dev = dict(bank=t(bank), blen=t(blen, torch.int32), pbox=t(pbox), lconf=t(lconf), gm=t(gm, torch.float64),
+               gs=t(gs, torch.float64), gon=t(np.ones(S, np.int32), torch.int32),
+               M=t(np.full(F, M, np.int32), torch.int32), N=t(np.full(F, N, np.int32), torch.int32))
+
+    def run(det_, dbox_, dconf_, slots_):
+        Ct = torch.full((F, M, N), -7.0, device=gpu)
+        Ca = torch.full((F, M, N), -7.0, device=gpu)
+        d, b, c, sl = t(det_), t(dbox_), t(dconf_), t(slots_, torch.int32)
+        rc = L.trk_build_cost_dev(F, M, N, P(dev["M"]), P(dev["N"]), P(sl), M, T, P(dev["bank"]), P(dev["blen"]),
+                                  P(dev["pbox"]), P(dev["lconf"]), P(dev["gm"]), P(dev["gs"]), P(dev["gon"]), P(d),
+                                  P(b), P(c), ctypes.byref(params), P(Ct), P(Ca), P(work), ops._stream(gpu))
+        assert rc == 0
+        torch.cuda.synchronize()
+        return Ct.cpu().numpy(), Ca.cpu().numpy()
+
+    Ct, Ca = run(det, dbox, dconf, slots)
+    Ct2, Ca2 = run(det, dbox, dconf, slots)
+    assert np.array_equal(Ct, Ct2) and np.array_equal(Ca, Ca2)
+    assert 0.05 < (Ct >= 1e9).mean() < 0.95  # the gate is exercised both ways
+    dp = np.stack([rng.permutation(N) for _ in range(F)])
+    rp = np.stack([rng.permutation(M) for _ in range(F)])
+    fi = np.arange(F)[:, None]
+    Ctp, Cap = run(det[fi, dp], dbox[fi, dp], dconf[fi, dp], slots[fi, rp])
+    assert np.array_equal(Ctp, Ct[fi[:, :, None], rp[:, :, None], dp[:, None, :]])
+    assert np.array_equal(Cap, Ca[fi[:, :, None], rp[:, :, None], dp[:, None, :]])
+
+
 def test_cost_batched_frames_with_row_slots(trk, oracle, gpu):
     rng = np.random.default_rng(22)
     F, Mmax, Nmax, S = 3, 40, 48, 200
